@@ -1,0 +1,111 @@
+/*
+ * eon.h -- C ABI of the MI355X (gfx950) prover hot path for the plonky3-eon BN254/KZG stack.
+ *
+ * This is the drop-in boundary: every entry point replaces one reference interface on the
+ * prover path, cited below as reference file:line (reference = Lolazyx/plonky3-eon).  Plain
+ * pointers and sizes only; no torch or HIP types in signatures (streams are passed as void*).
+ * A Rust shim binds these with `extern "C"`.
+ *
+ * Data layout (shared with the reference, zero-copy):
+ *   eon_fr        = p3_bn254::Fr: [u64;4] little-endian Montgomery residue a*2^256 mod r,
+ *                   canonical (< r)                                   (bn254/src/field.rs:98-105)
+ *   matrices      = p3_matrix RowMajorMatrix<Fr>: element (row, col) at values[row*width + col]
+ *                                                                     (matrix/src/dense.rs:24-37)
+ *   eon_g1_affine = BN254 G1 affine point, x and y as Fq Montgomery residues (R = 2^256 mod q),
+ *                   [u64;4] LE each; the point at infinity is encoded as x = y = 0.
+ *
+ * Conventions:
+ *   - return 0 on success, a negative EON_E_* code otherwise; eon_last_error() has the message.
+ *     The reference panics in these cases (assert!/log2_strict_usize/unwrap); a Rust shim
+ *     should panic on a nonzero return to keep that behaviour.
+ *   - `*_dev` entry points take DEVICE pointers and enqueue asynchronously on the context's
+ *     stream (eon_ctx_set_stream); the others take HOST pointers and are synchronous.
+ *   - a context is internally locked: entry points are thread-safe (the reference's DFTs are
+ *     Clone + Sync and share twiddle caches, dft/src/radix_2_dit_parallel.rs:30-40).
+ */
+#ifndef EON_H
+#define EON_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    uint64_t l[4];
+} eon_fr;
+
+typedef struct {
+    uint64_t x[4];
+    uint64_t y[4];
+} eon_g1_affine;
+
+typedef struct eon_ctx eon_ctx;
+typedef struct eon_msm_bases eon_msm_bases;
+
+enum {
+    EON_OK = 0,
+    EON_E_SHAPE = -1,            /* height not a power of two, size mismatch (reference: panic) */
+    EON_E_DEGREE_TOO_LARGE = -2, /* KzgError::DegreeTooLarge (kzg/src/params.rs:164-173) */
+    EON_E_DEVICE = -3,           /* HIP runtime error */
+    EON_E_OOM = -4,              /* device allocation failed */
+    EON_E_ARG = -5               /* null pointer / invalid argument */
+};
+
+enum {
+    EON_ORDER_NATURAL = 0, /* RowMajorMatrix output, as Radix2Dit (dft/src/radix_2_dit.rs:61-77) */
+    EON_ORDER_BITREV = 1   /* storage of Radix2DitParallel's BitReversedMatrixView: storage row
+                              reverse_bits_len(k, log2 h) holds logical row k
+                              (dft/src/radix_2_dit_parallel.rs:146,165,227) */
+};
+
+/* ---- context ---------------------------------------------------------------------------- */
+int eon_ctx_create(int device_ordinal, eon_ctx** out);
+void eon_ctx_destroy(eon_ctx* ctx);
+const char* eon_last_error(const eon_ctx* ctx);
+/* stream (a hipStream_t) used by the *_dev entry points; NULL = the context's own stream */
+int eon_ctx_set_stream(eon_ctx* ctx, void* hip_stream);
+int eon_ctx_synchronize(eon_ctx* ctx);
+/* ABI version; bumped on any signature change */
+uint32_t eon_abi_version(void);
+
+/* ---- TwoAdicSubgroupDft<Fr> (dft/src/traits.rs:27-249) -----------------------------------
+ * `in` is height x width, row-major.  height must be a power of two with log2(height) (+ added
+ * bits) <= 28 (Fr::TWO_ADICITY, bn254/src/field.rs:564).  `in` and `out` may alias. */
+
+/* dft_batch (dft/src/traits.rs:61): coefficients -> evaluations on H. */
+int eon_dft_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height, uint32_t width,
+                  int out_order);
+/* idft_batch (dft/src/traits.rs:111-122): evaluations on H -> coefficients (natural order). */
+int eon_idft_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height, uint32_t width);
+/* coset_dft_batch (dft/src/traits.rs:83-91): coefficients -> evaluations on shift*H. */
+int eon_coset_dft_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                        uint32_t width, const eon_fr* shift, int out_order);
+/* coset_idft_batch (dft/src/traits.rs:144-153): evaluations on shift*H -> coefficients. */
+int eon_coset_idft_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                         uint32_t width, const eon_fr* shift);
+/* coset_lde_batch (dft/src/traits.rs:226-249; Radix2DitParallel override at
+ * dft/src/radix_2_dit_parallel.rs:169-228): evaluations on H -> evaluations on shift*K,
+ * |K| = height << added_bits.  `out` holds (height << added_bits) x width.  shift NULL = ONE
+ * (lde_batch, dft/src/traits.rs:187-192).  Must not alias `in`. */
+int eon_coset_lde_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                        uint32_t width, uint32_t added_bits, const eon_fr* shift, int out_order);
+
+/* device-pointer variants (same semantics, asynchronous on the context stream) */
+int eon_dft_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                      uint32_t width, int out_order);
+int eon_idft_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                       uint32_t width);
+int eon_coset_dft_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                            uint32_t width, const eon_fr* shift, int out_order);
+int eon_coset_idft_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                             uint32_t width, const eon_fr* shift);
+int eon_coset_lde_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                            uint32_t width, uint32_t added_bits, const eon_fr* shift,
+                            int out_order);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EON_H */

@@ -1,0 +1,338 @@
+"""Pure-Python big-integer restatement of the reference's hot-path semantics.
+
+TEST INFRASTRUCTURE ONLY.  This module is the checker: tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg may import it; the product path (plonky3_eon_amd/) never does.
+
+It restates, for small sizes, exactly what the reference computes (citations are into the
+reference tree, /root/reference at survey time):
+
+* Fr: BN254 scalar field in Montgomery form R = 2^256, canonical limbs
+  (bn254/src/field.rs:26-105, constants :248-281, :372-377, :553-574).
+* NaiveDft (dft/src/naive.rs:13-32) and the TwoAdicSubgroupDft trait defaults built on it:
+  idft (dft/src/traits.rs:111-122: dft, divide_by_height, swap rows r <-> h-r), coset_dft
+  (:83-91), coset_idft (:144-153), lde / coset_lde (:187-249); divide_by_height and
+  coset_shift_cols (dft/src/util.rs:15-36).
+* Radix2DitParallel's storage order: a BitReversalPerm view of the natural result
+  (dft/src/radix_2_dit_parallel.rs:165,227; matrix/src/bitrev.rs), i.e. storage row
+  reverse_bits_len(k, log_h) holds logical row k (util/src/lib.rs:70-78).
+* BN254 G1 over Fq (y^2 = x^3 + 3, generator (1, 2)) with naive double-and-add scalar
+  multiplication -- the value G1::multi_exp returns (bn254/src/curve.rs:158-179); halo2curves'
+  msm_best is a third-party dependency (halo2curves 0.9) absent from the reference tree, so the
+  value (which is unique) is restated directly.
+* init_srs_unsafe (kzg/src/params.rs:123-139) and commit_column (kzg/src/util.rs:37-40).
+
+Parity pinning: tests/test_oracle_kats.py checks this module against every known-answer test
+the reference holds for these functions (Fr constants and test_bn254fr, the NaiveDft KAT and
+round trips, divide_by_height / coset_shift_cols KATs, the bit-reversal table, the G1
+multi_exp identities).
+"""
+
+from __future__ import annotations
+
+import struct
+
+# --- constants (bn254/src/field.rs) -------------------------------------------------------
+P = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
+Q = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+R = 1 << 256
+R_MOD_P = R % P
+R_INV_P = pow(R, -1, P)
+R_MOD_Q = R % Q
+R_INV_Q = pow(R, -1, Q)
+GENERATOR = 5
+TWO_ADICITY = 28
+# TWO_ADIC_GENERATOR in Montgomery limbs (bn254/src/field.rs:556-561)
+TWO_ADIC_GENERATOR_MONT = (0x636E735580D13D9C, 0xA22BF3742445FFD6, 0x56452AC01EB203D8, 0x1860EF942963F9E7)
+
+
+def limbs_to_int(limbs) -> int:
+    v = 0
+    for i, x in enumerate(limbs):
+        v |= int(x) << (64 * i)
+    return v
+
+
+def int_to_limbs(v: int):
+    return tuple((v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4))
+
+
+def to_mont(x: int) -> int:
+    """canonical Fr value -> Montgomery residue (what Fr.value holds)."""
+    return (x % P) * R_MOD_P % P
+
+
+def from_mont(m: int) -> int:
+    return m * R_INV_P % P
+
+
+def fq_to_mont(x: int) -> int:
+    return (x % Q) * R_MOD_Q % Q
+
+
+def fq_from_mont(m: int) -> int:
+    return m * R_INV_Q % Q
+
+
+TWO_ADIC_GENERATOR = from_mont(limbs_to_int(TWO_ADIC_GENERATOR_MONT))
+
+
+def two_adic_generator(bits: int) -> int:
+    """bn254/src/field.rs:567-573: square the 2^28-th root (28 - bits) times."""
+    assert bits <= TWO_ADICITY
+    w = TWO_ADIC_GENERATOR
+    for _ in range(bits, TWO_ADICITY):
+        w = w * w % P
+    return w
+
+
+def reverse_bits_len(x: int, bits: int) -> int:
+    """util/src/lib.rs:70-78."""
+    r = 0
+    for _ in range(bits):
+        r = (r << 1) | (x & 1)
+        x >>= 1
+    return r
+
+
+def log2_strict(n: int) -> int:
+    assert n > 0 and n & (n - 1) == 0, "height must be a power of two"
+    return n.bit_length() - 1
+
+
+# --- deterministic input generation ---------------------------------------------------------
+class SplitMix64:
+    """In-repo PRNG for fixtures (the reference's rand::SmallRng stream is not reproducible
+    offline; inputs only need to be deterministic and uniform)."""
+
+    def __init__(self, seed: int):
+        self.s = seed & 0xFFFFFFFFFFFFFFFF
+
+    def next(self) -> int:
+        self.s = (self.s + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        z = self.s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+        return z ^ (z >> 31)
+
+    def fr_mont(self) -> int:
+        """Rejection sampling as Distribution<Fr> (bn254/src/field.rs:534-551): 32 random bytes,
+        top two bits cleared, accepted if < P, interpreted as the Montgomery residue."""
+        while True:
+            v = limbs_to_int([self.next() for _ in range(4)])
+            v &= (1 << 254) - 1
+            if v < P:
+                return v
+
+
+def random_matrix(seed: int, h: int, w: int):
+    """Row-major h x w matrix of canonical Fr values."""
+    rng = SplitMix64(seed)
+    return [[from_mont(rng.fr_mont()) for _ in range(w)] for _ in range(h)]
+
+
+# --- DFT semantics ---------------------------------------------------------------------------
+def naive_dft(mat):
+    """dft/src/naive.rs:13-32: row r = sum_j c_j * g^(r*j), g = two_adic_generator(log h)."""
+    h = len(mat)
+    if h == 0:
+        return []
+    w = len(mat[0])
+    g = two_adic_generator(log2_strict(h))
+    out = [[0] * w for _ in range(h)]
+    point = 1
+    for r in range(h):
+        pp = 1
+        acc = [0] * w
+        for j in range(h):
+            row = mat[j]
+            for c in range(w):
+                acc[c] += pp * row[c]
+            pp = pp * point % P
+        out[r] = [a % P for a in acc]
+        point = point * g % P
+    return out
+
+
+def divide_by_height(mat):
+    """dft/src/util.rs:15-25."""
+    h = len(mat)
+    log2_strict(h)
+    inv = pow(h, -1, P)
+    return [[x * inv % P for x in row] for row in mat]
+
+
+def coset_shift_cols(mat, shift):
+    """dft/src/util.rs:28-36: row i scaled by shift^i."""
+    out = []
+    wgt = 1
+    for row in mat:
+        out.append([x * wgt % P for x in row])
+        wgt = wgt * shift % P
+    return out
+
+
+def dft(mat):
+    return naive_dft(mat)
+
+
+def idft(mat):
+    """dft/src/traits.rs:111-122."""
+    d = divide_by_height(naive_dft(mat))
+    h = len(d)
+    for r in range(1, h // 2):
+        d[r], d[h - r] = d[h - r], d[r]
+    return d
+
+
+def coset_dft(mat, shift):
+    return naive_dft(coset_shift_cols(mat, shift))
+
+
+def coset_idft(mat, shift):
+    return coset_shift_cols(idft(mat), pow(shift, -1, P))
+
+
+def coset_lde(mat, added_bits, shift):
+    """dft/src/traits.rs:226-249 (natural/logical order)."""
+    coeffs = idft(mat)
+    w = len(mat[0]) if mat else 0
+    coeffs = coeffs + [[0] * w for _ in range(len(coeffs) * ((1 << added_bits) - 1))]
+    return coset_dft(coeffs, shift)
+
+
+def lde(mat, added_bits):
+    return coset_lde(mat, added_bits, 1)
+
+
+def bit_reverse_rows(mat):
+    """Storage of a BitReversalPerm view (matrix/src/bitrev.rs): storage[rev(k)] = logical[k]."""
+    h = len(mat)
+    lg = log2_strict(h)
+    out = [None] * h
+    for k in range(h):
+        out[reverse_bits_len(k, lg)] = mat[k]
+    return out
+
+
+# --- G1 over Fq -------------------------------------------------------------------------------
+G1_GEN = (1, 2)  # y^2 = x^3 + 3
+INF = None
+
+
+def g1_is_on_curve(p) -> bool:
+    if p is INF:
+        return True
+    x, y = p
+    return (y * y - x * x * x - 3) % Q == 0
+
+
+def g1_add(a, b):
+    if a is INF:
+        return b
+    if b is INF:
+        return a
+    x1, y1 = a
+    x2, y2 = b
+    if x1 == x2:
+        if (y1 + y2) % Q == 0:
+            return INF
+        lam = 3 * x1 * x1 * pow(2 * y1, -1, Q) % Q
+    else:
+        lam = (y2 - y1) * pow(x2 - x1, -1, Q) % Q
+    x3 = (lam * lam - x1 - x2) % Q
+    y3 = (lam * (x1 - x3) - y1) % Q
+    return (x3, y3)
+
+
+def g1_neg(a):
+    return INF if a is INF else (a[0], (-a[1]) % Q)
+
+
+def g1_mul(p, k: int):
+    """Double-and-add; k is a canonical integer (any size)."""
+    k %= P
+    acc = INF
+    addend = p
+    while k:
+        if k & 1:
+            acc = g1_add(acc, addend)
+        addend = g1_add(addend, addend)
+        k >>= 1
+    return acc
+
+
+def msm(points, scalars):
+    """Value of G1::multi_exp (bn254/src/curve.rs:158-179); empty -> identity."""
+    assert len(points) == len(scalars), "points and scalars must have the same length"
+    acc = INF
+    for p, s in zip(points, scalars):
+        acc = g1_add(acc, g1_mul(p, s))
+    return acc
+
+
+def init_srs_g1(max_degree: int, alpha: int):
+    """kzg/src/params.rs:123-139: g1_powers[i] = alpha^i * G."""
+    out = []
+    pw = 1
+    acc = G1_GEN
+    for _ in range(max_degree + 1):
+        out.append(g1_mul(G1_GEN, pw))
+        pw = pw * alpha % P
+    return out
+
+
+def commit_column(g1_powers, coeffs):
+    """kzg/src/util.rs:37-40."""
+    return msm(g1_powers[: len(coeffs)], coeffs)
+
+
+# --- byte encodings used by fixtures --------------------------------------------------------
+def fr_to_bytes(x: int) -> bytes:
+    """Fr::into_bytes: 32-byte little-endian Montgomery (bn254/src/field.rs:307-310)."""
+    return to_mont(x).to_bytes(32, "little")
+
+
+def fr_from_bytes(b: bytes) -> int:
+    return from_mont(int.from_bytes(b, "little"))
+
+
+def g1_to_bytes(p) -> bytes:
+    """C-ABI eon_g1_affine: x, y as Fq Montgomery LE; identity = all zero (include/eon.h)."""
+    if p is INF:
+        return b"\0" * 64
+    return fq_to_mont(p[0]).to_bytes(32, "little") + fq_to_mont(p[1]).to_bytes(32, "little")
+
+
+def g1_from_bytes(b: bytes):
+    x = int.from_bytes(b[:32], "little")
+    y = int.from_bytes(b[32:], "little")
+    if x == 0 and y == 0:
+        return INF
+    return (fq_from_mont(x), fq_from_mont(y))
+
+
+def mat_to_u64(mat):
+    """Row-major matrix -> flat list of u64 limbs (4 per element, Montgomery)."""
+    out = []
+    for row in mat:
+        for x in row:
+            out.extend(int_to_limbs(to_mont(x)))
+    return out
+
+
+def u64_to_mat(vals, h, w):
+    it = iter(vals)
+    out = []
+    for _ in range(h):
+        row = []
+        for _ in range(w):
+            limbs = [next(it) for _ in range(4)]
+            row.append(from_mont(limbs_to_int(limbs)))
+        out.append(row)
+    return out
+
+
+if __name__ == "__main__":  # quick self-check
+    assert to_mont(1) == limbs_to_int((0xAC96341C4FFFFFFB, 0x36FC76959F60CD29, 0x666EA36F7879462E, 0x0E0A77C19A07DF2F))
+    assert pow(two_adic_generator(28), 1 << 27, P) == P - 1
+    print("ok")

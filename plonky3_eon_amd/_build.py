@@ -1,0 +1,62 @@
+"""Builds libeonhip.so (the C-ABI shared library, include/eon.h) in-tree for gfx950.
+
+Each translation unit is compiled with hipcc --offload-arch=gfx950 into build/, then linked
+into plonky3_eon_amd/libeonhip.so.  Objects are rebuilt only when a source or header is newer.
+"""
+
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+BUILD = ROOT / "build" / "eonhip"
+LIB = PKG / "libeonhip.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
+         "-I" + str(ROOT / "include")]
+
+
+def sources():
+    return sorted(CSRC.glob("*.hip"))
+
+
+def _headers_mtime() -> float:
+    hs = list(CSRC.glob("*.h")) + list((ROOT / "include").glob("*.h"))
+    return max((h.stat().st_mtime for h in hs), default=0.0)
+
+
+def _compile(src: Path) -> Path:
+    obj = BUILD / (src.stem + ".o")
+    if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
+        return obj
+    cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")
+    return obj
+
+
+def build(verbose: bool = False) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    srcs = sources()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(_compile, srcs))
+    newest = max(o.stat().st_mtime for o in objs)
+    if not LIB.exists() or LIB.stat().st_mtime < newest:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    if verbose:
+        print(f"built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)

@@ -1,0 +1,92 @@
+"""ctypes binding of libeonhip.so (include/eon.h).
+
+The product path is native: if the shared library is missing or fails to load this module
+raises -- there is no CPU fallback anywhere in plonky3_eon_amd.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "libeonhip.so"
+
+EON_OK = 0
+EON_E_SHAPE = -1
+EON_E_DEGREE_TOO_LARGE = -2
+EON_E_DEVICE = -3
+EON_E_OOM = -4
+EON_E_ARG = -5
+EON_ORDER_NATURAL = 0
+EON_ORDER_BITREV = 1
+
+_ERRNAMES = {
+    EON_E_SHAPE: "EON_E_SHAPE",
+    EON_E_DEGREE_TOO_LARGE: "EON_E_DEGREE_TOO_LARGE",
+    EON_E_DEVICE: "EON_E_DEVICE",
+    EON_E_OOM: "EON_E_OOM",
+    EON_E_ARG: "EON_E_ARG",
+}
+
+
+class EonError(RuntimeError):
+    """A nonzero return from the C ABI.  The reference panics in these cases."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class eon_fr(ctypes.Structure):
+    _fields_ = [("l", ctypes.c_uint64 * 4)]
+
+
+class eon_g1_affine(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_uint64 * 4), ("y", ctypes.c_uint64 * 4)]
+
+
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_INT = ctypes.c_int
+
+# name -> (restype, argtypes); the full exported surface of include/eon.h
+SIGNATURES = {
+    "eon_abi_version": (_U32, []),
+    "eon_ctx_create": (_INT, [_INT, ctypes.POINTER(_P)]),
+    "eon_ctx_destroy": (None, [_P]),
+    "eon_last_error": (ctypes.c_char_p, [_P]),
+    "eon_ctx_set_stream": (_INT, [_P, _P]),
+    "eon_ctx_synchronize": (_INT, [_P]),
+    "eon_dft_batch": (_INT, [_P, _P, _P, _U64, _U32, _INT]),
+    "eon_idft_batch": (_INT, [_P, _P, _P, _U64, _U32]),
+    "eon_coset_dft_batch": (_INT, [_P, _P, _P, _U64, _U32, _P, _INT]),
+    "eon_coset_idft_batch": (_INT, [_P, _P, _P, _U64, _U32, _P]),
+    "eon_coset_lde_batch": (_INT, [_P, _P, _P, _U64, _U32, _U32, _P, _INT]),
+    "eon_dft_batch_dev": (_INT, [_P, _P, _P, _U64, _U32, _INT]),
+    "eon_idft_batch_dev": (_INT, [_P, _P, _P, _U64, _U32]),
+    "eon_coset_dft_batch_dev": (_INT, [_P, _P, _P, _U64, _U32, _P, _INT]),
+    "eon_coset_idft_batch_dev": (_INT, [_P, _P, _P, _U64, _U32, _P]),
+    "eon_coset_lde_batch_dev": (_INT, [_P, _P, _P, _U64, _U32, _U32, _P, _INT]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libeonhip.so (once).  Raises if it is absent: the product path never falls back."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(os.fspath(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

@@ -1,0 +1,322 @@
+// C ABI: context management and the TwoAdicSubgroupDft<Fr> entry points (include/eon.h).
+//
+// Each entry point is planned as one or two radix-2 networks (ntt.hip) whose first pass folds
+// in the input permutation and coset scaling, mirroring the reference trait defaults:
+//   dft           (dft/src/traits.rs:61)       natural: DIT over bit-reversed gather; bitrev: DIF
+//   idft          (dft/src/traits.rs:111-122)  DIT with inverse twiddles, 1/N folded into the load
+//   coset_dft     (dft/src/traits.rs:83-91)    as dft, coefficient j scaled by shift^j on load
+//   coset_idft    (dft/src/traits.rs:144-153)  as idft, output j scaled by shift^-j on store
+//   coset_lde     (dft/src/traits.rs:226-249, Radix2DitParallel :169-228)
+//        natural: inverse DIF (evals -> bit-reversed coefficients) then a forward DIT of size
+//                 N*2^b that starts at stage b on the spread coefficients (the first b stages
+//                 of a zero-padded DIT only copy), coefficient scaling shift^j / N on load.
+//        bitrev:  inverse DIT (natural coefficients) then forward DIF on the zero-padded
+//                 vector, which lands directly in Radix2DitParallel's bit-reversed storage.
+#include <cstdlib>
+#include <cstring>
+
+#include "context.h"
+#include "ntt.h"
+
+using namespace eon;
+
+namespace eon {
+
+Status ensure_twiddles(eon_ctx* ctx, uint32_t log_n) {
+    if (log_n == 0 || log_n <= ctx->tw_log) return Status::ok();
+    const uint32_t L = log_n < 12 ? 12 : log_n;  // build small tables once
+    const size_t bytes = ((size_t)1 << L) * sizeof(Fr);
+    EON_HIP(ctx->tw_fwd.ensure(bytes));
+    EON_HIP(ctx->tw_inv.ensure(bytes));
+    const Fr root = fr_two_adic_generator(L);
+    EON_HIP(launch_twiddles(ctx->tw_fwd.as<Fr>(), L, root, ctx->stream));
+    EON_HIP(launch_twiddles(ctx->tw_inv.as<Fr>(), L, inverse(root), ctx->stream));
+    ctx->tw_log = L;
+    return Status::ok();
+}
+
+Status get_power_table(eon_ctx* ctx, uint32_t log_n, const Fr& base, const Fr& scale, bool bitrev,
+                       const Fr** out) {
+    std::string key(1, bitrev ? 'r' : 'n');
+    key.push_back((char)log_n);
+    key.append(reinterpret_cast<const char*>(base.v), 32);
+    key.append(reinterpret_cast<const char*>(scale.v), 32);
+    auto it = ctx->tables.find(key);
+    if (it == ctx->tables.end()) {
+        if (ctx->tables.size() >= 64) {
+            // bounded cache: drop everything (tables are cheap to rebuild)
+            EON_HIP(hipStreamSynchronize(ctx->stream));
+            for (auto& kv : ctx->tables) kv.second.release();
+            ctx->tables.clear();
+        }
+        DevBuf buf;
+        const uint64_t n = 1ull << log_n;
+        EON_HIP(buf.ensure(n * sizeof(Fr)));
+        hipError_t e = launch_powers(buf.as<Fr>(), n, base, scale, bitrev ? log_n : NATURAL_IDX,
+                                     ctx->stream);
+        if (e != hipSuccess) {
+            buf.release();
+            EON_HIP(e);
+        }
+        it = ctx->tables.emplace(key, buf).first;
+    }
+    *out = it->second.as<Fr>();
+    return Status::ok();
+}
+
+}  // namespace eon
+
+namespace {
+
+enum class Op { Dft, Idft, CosetDft, CosetIdft, CosetLde };
+
+int finish(eon_ctx* ctx, const Status& s) {
+    if (s.bad()) ctx->last_error = s.msg;
+    return s.code;
+}
+
+Status check_shape(uint64_t height, uint32_t added_bits, uint32_t* log_h) {
+    if (height == 0 || (height & (height - 1)) != 0)
+        return Status::err(EON_E_SHAPE, "height must be a power of two (log2_strict_usize)");
+    const uint32_t lg = 63 - __builtin_clzll(height);
+    if (lg + (uint64_t)added_bits > 28)
+        return Status::err(EON_E_SHAPE, "log2(height) + added_bits exceeds Fr::TWO_ADICITY = 28");
+    *log_h = lg;
+    return Status::ok();
+}
+
+Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint32_t width,
+               uint32_t added_bits, const eon_fr* shift_abi, int out_order) {
+    uint32_t n = 0;
+    EON_TRY(check_shape(height, op == Op::CosetLde ? added_bits : 0, &n));
+    if (out_order != EON_ORDER_NATURAL && out_order != EON_ORDER_BITREV)
+        return Status::err(EON_E_ARG, "out_order must be EON_ORDER_NATURAL or EON_ORDER_BITREV");
+    if (width == 0) return Status::ok();
+    if (!in || !out) return Status::err(EON_E_ARG, "null matrix pointer");
+    Fr shift = Fr::one();
+    if (shift_abi) {
+        shift = fr_from_abi(shift_abi);
+        if (!fr_is_canonical(shift)) return Status::err(EON_E_ARG, "shift is not a canonical Fr");
+    }
+    const bool natural = out_order == EON_ORDER_NATURAL;
+    const uint32_t b = op == Op::CosetLde ? added_bits : 0;
+    EON_TRY(ensure_twiddles(ctx, n + b));
+    const size_t mat_bytes = (size_t)height * width * sizeof(Fr);
+    hipStream_t st = ctx->stream;
+
+    const Fr n_inv = inverse(from_u64<FrP>(height));
+
+    if (op == Op::CosetLde) {
+        EON_HIP(ctx->scratch.ensure(mat_bytes));
+        Fr* coeffs = ctx->scratch.as<Fr>();
+        NetworkSpec a;  // evals -> coefficients (times N), into scratch
+        a.log_m = n;
+        a.src = in;
+        a.dst = coeffs;
+        a.width = width;
+        a.tw = ctx->tw_inv.as<Fr>();
+        NetworkSpec f;  // coefficients -> evaluations on shift * K
+        f.log_m = n + b;
+        f.src = coeffs;
+        f.dst = out;
+        f.width = width;
+        f.tw = ctx->tw_fwd.as<Fr>();
+        const Fr* table = nullptr;
+        if (natural) {
+            a.dif = true;  // natural evals -> bit-reversed coefficients
+            EON_TRY(get_power_table(ctx, n, shift, n_inv, true, &table));
+            f.dif = false;
+            f.first_stage = b;
+            f.load_mode = LOAD_SPREAD;
+            f.load_param = b;
+        } else {
+            a.dif = false;  // bit-reversed gather -> natural coefficients
+            a.load_mode = LOAD_BITREV;
+            a.load_param = n;
+            EON_TRY(get_power_table(ctx, n, shift, n_inv, false, &table));
+            f.dif = true;
+            f.load_mode = LOAD_ZEROPAD;
+            f.load_param = (uint32_t)height;
+        }
+        f.load_scale = table;
+        a.max_stages_per_pass = f.max_stages_per_pass = ctx->ntt_max_stages;
+        EON_HIP(run_network(a, st));
+        EON_HIP(run_network(f, st));
+        return Status::ok();
+    }
+
+    NetworkSpec s;
+    s.log_m = n;
+    s.src = in;
+    s.dst = out;
+    s.width = width;
+    const bool inv = op == Op::Idft || op == Op::CosetIdft;
+    s.tw = inv ? ctx->tw_inv.as<Fr>() : ctx->tw_fwd.as<Fr>();
+    // idft / coset_idft always return natural-order coefficients (RowMajorMatrix)
+    s.dif = !(inv || natural);
+    if (!s.dif) {
+        s.load_mode = LOAD_BITREV;
+        s.load_param = n;
+        if (in == out && n > 0) {  // the gather cannot run in place
+            EON_HIP(ctx->scratch.ensure(mat_bytes));
+            EON_HIP(hipMemcpyAsync(ctx->scratch.p, in, mat_bytes, hipMemcpyDeviceToDevice, st));
+            s.src = ctx->scratch.as<Fr>();
+        }
+    }
+    if (op == Op::CosetDft) {
+        const Fr* table = nullptr;
+        EON_TRY(get_power_table(ctx, n, shift, Fr::one(), false, &table));
+        s.load_scale = table;
+    }
+    if (inv) {
+        s.has_load_const = 1;
+        s.load_const = n_inv;
+    }
+    if (op == Op::CosetIdft) {
+        const Fr* table = nullptr;
+        EON_TRY(get_power_table(ctx, n, inverse(shift), Fr::one(), false, &table));
+        s.store_scale = table;
+    }
+    s.max_stages_per_pass = ctx->ntt_max_stages;
+    EON_HIP(run_network(s, st));
+    return Status::ok();
+}
+
+// Host-pointer wrapper: stage in, run, stage out, synchronize.
+Status dft_host(eon_ctx* ctx, Op op, const eon_fr* in, eon_fr* out, uint64_t height,
+                uint32_t width, uint32_t added_bits, const eon_fr* shift, int out_order) {
+    uint32_t n = 0;
+    EON_TRY(check_shape(height, op == Op::CosetLde ? added_bits : 0, &n));
+    if (width == 0) return Status::ok();
+    if (!in || !out) return Status::err(EON_E_ARG, "null matrix pointer");
+    const size_t in_bytes = (size_t)height * width * sizeof(Fr);
+    const size_t out_bytes = in_bytes << (op == Op::CosetLde ? added_bits : 0);
+    EON_HIP(ctx->stage_in.ensure(in_bytes));
+    EON_HIP(ctx->stage_out.ensure(out_bytes));
+    EON_HIP(hipMemcpyAsync(ctx->stage_in.p, in, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+    EON_TRY(dft_dev(ctx, op, ctx->stage_in.as<Fr>(), ctx->stage_out.as<Fr>(), height, width,
+                    added_bits, shift, out_order));
+    EON_HIP(hipMemcpyAsync(out, ctx->stage_out.p, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    EON_HIP(hipStreamSynchronize(ctx->stream));
+    return Status::ok();
+}
+
+int entry(eon_ctx* ctx, bool dev, Op op, const eon_fr* in, eon_fr* out, uint64_t height,
+          uint32_t width, uint32_t added_bits, const eon_fr* shift, int out_order) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess)
+        return finish(ctx, Status::err(EON_E_DEVICE, "hipSetDevice failed"));
+    Status s = dev ? dft_dev(ctx, op, reinterpret_cast<const Fr*>(in), reinterpret_cast<Fr*>(out),
+                             height, width, added_bits, shift, out_order)
+                   : dft_host(ctx, op, in, out, height, width, added_bits, shift, out_order);
+    return finish(ctx, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t eon_abi_version(void) { return 1; }
+
+int eon_ctx_create(int device_ordinal, eon_ctx** out) {
+    if (!out) return EON_E_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device_ordinal < 0 || device_ordinal >= n)
+        return EON_E_DEVICE;
+    if (hipSetDevice(device_ordinal) != hipSuccess) return EON_E_DEVICE;
+    eon_ctx* c = new eon_ctx();
+    c->device = device_ordinal;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return EON_E_DEVICE;
+    }
+    c->stream = c->own_stream;
+    if (const char* e = getenv("EON_NTT_MAX_STAGES")) c->ntt_max_stages = (uint32_t)atoi(e);
+    *out = c;
+    return EON_OK;
+}
+
+void eon_ctx_destroy(eon_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    ctx->tw_fwd.release();
+    ctx->tw_inv.release();
+    for (auto& kv : ctx->tables) kv.second.release();
+    ctx->scratch.release();
+    ctx->stage_in.release();
+    ctx->stage_out.release();
+    (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+}
+
+const char* eon_last_error(const eon_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+int eon_ctx_set_stream(eon_ctx* ctx, void* hip_stream) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->stream = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+    return EON_OK;
+}
+
+int eon_ctx_synchronize(eon_ctx* ctx) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    (void)hipSetDevice(ctx->device);
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        ctx->last_error = hipGetErrorString(e);
+        return EON_E_DEVICE;
+    }
+    return EON_OK;
+}
+
+int eon_dft_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height, uint32_t width,
+                  int out_order) {
+    return entry(ctx, false, Op::Dft, in, out, height, width, 0, nullptr, out_order);
+}
+int eon_idft_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height, uint32_t width) {
+    return entry(ctx, false, Op::Idft, in, out, height, width, 0, nullptr, EON_ORDER_NATURAL);
+}
+int eon_coset_dft_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                        uint32_t width, const eon_fr* shift, int out_order) {
+    if (!shift) return EON_E_ARG;
+    return entry(ctx, false, Op::CosetDft, in, out, height, width, 0, shift, out_order);
+}
+int eon_coset_idft_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                         uint32_t width, const eon_fr* shift) {
+    if (!shift) return EON_E_ARG;
+    return entry(ctx, false, Op::CosetIdft, in, out, height, width, 0, shift, EON_ORDER_NATURAL);
+}
+int eon_coset_lde_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                        uint32_t width, uint32_t added_bits, const eon_fr* shift, int out_order) {
+    return entry(ctx, false, Op::CosetLde, in, out, height, width, added_bits, shift, out_order);
+}
+
+int eon_dft_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                      uint32_t width, int out_order) {
+    return entry(ctx, true, Op::Dft, in, out, height, width, 0, nullptr, out_order);
+}
+int eon_idft_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                       uint32_t width) {
+    return entry(ctx, true, Op::Idft, in, out, height, width, 0, nullptr, EON_ORDER_NATURAL);
+}
+int eon_coset_dft_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                            uint32_t width, const eon_fr* shift, int out_order) {
+    if (!shift) return EON_E_ARG;
+    return entry(ctx, true, Op::CosetDft, in, out, height, width, 0, shift, out_order);
+}
+int eon_coset_idft_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                             uint32_t width, const eon_fr* shift) {
+    if (!shift) return EON_E_ARG;
+    return entry(ctx, true, Op::CosetIdft, in, out, height, width, 0, shift, EON_ORDER_NATURAL);
+}
+int eon_coset_lde_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
+                            uint32_t width, uint32_t added_bits, const eon_fr* shift,
+                            int out_order) {
+    return entry(ctx, true, Op::CosetLde, in, out, height, width, added_bits, shift, out_order);
+}
+
+}  // extern "C"

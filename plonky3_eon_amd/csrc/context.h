@@ -1,0 +1,122 @@
+// eon_ctx: per-device state behind the C ABI (streams, twiddle and coset tables, scratch).
+#pragma once
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/eon.h"
+#include "field.h"
+
+namespace eon {
+
+// Device buffer that only grows; freed with the context.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+            bytes = 0;
+        }
+        hipError_t e = hipMalloc(&p, need);
+        if (e == hipSuccess) bytes = need;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const {
+        return reinterpret_cast<T*>(p);
+    }
+};
+
+struct Status {
+    int code = EON_OK;
+    std::string msg;
+    static Status ok() { return {}; }
+    static Status err(int c, std::string m) { return {c, std::move(m)}; }
+    bool bad() const { return code != EON_OK; }
+};
+
+#define EON_HIP(call)                                                                     \
+    do {                                                                                  \
+        hipError_t _e = (call);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return ::eon::Status::err(_e == hipErrorOutOfMemory ? EON_E_OOM : EON_E_DEVICE, \
+                                      std::string(#call ": ") + hipGetErrorString(_e));   \
+    } while (0)
+
+#define EON_TRY(expr)                  \
+    do {                               \
+        ::eon::Status _s = (expr);     \
+        if (_s.bad()) return _s;       \
+    } while (0)
+
+}  // namespace eon
+
+struct eon_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::string last_error;
+
+    // stage-concatenated twiddles for sizes up to 2^tw_log (forward and inverse)
+    eon::DevBuf tw_fwd, tw_inv;
+    uint32_t tw_log = 0;
+
+    // coset / scaling tables keyed by (kind, log_n, base, scale)
+    std::map<std::string, eon::DevBuf> tables;
+
+    // EON_NTT_MAX_STAGES: cap on radix-2 stages per NTT pass (0 = tile limit); read at creation
+    uint32_t ntt_max_stages = 0;
+
+    // scratch: NTT intermediates, host-API staging
+    eon::DevBuf scratch, stage_in, stage_out;
+};
+
+namespace eon {
+
+Status ensure_twiddles(eon_ctx* ctx, uint32_t log_n);
+// table[j] = scale * base^j (natural) or table[j] = scale * base^reverse_bits(j, log_n) (bitrev)
+Status get_power_table(eon_ctx* ctx, uint32_t log_n, const Fr& base, const Fr& scale, bool bitrev,
+                       const Fr** out);
+
+inline Fr fr_two_adic_generator(uint32_t bits) {
+    // bn254/src/field.rs:556-573: square TWO_ADIC_GENERATOR (order 2^28) 28 - bits times
+    Fr w;
+    const uint64_t g[4] = {0x636e735580d13d9cull, 0xa22bf3742445ffd6ull, 0x56452ac01eb203d8ull,
+                           0x1860ef942963f9e7ull};
+    for (int i = 0; i < 4; i++) {
+        w.v[2 * i] = (uint32_t)g[i];
+        w.v[2 * i + 1] = (uint32_t)(g[i] >> 32);
+    }
+    for (uint32_t i = bits; i < 28; i++) w = sqr(w);
+    return w;
+}
+
+inline Fr fr_from_abi(const eon_fr* x) {
+    Fr r;
+    for (int i = 0; i < 4; i++) {
+        r.v[2 * i] = (uint32_t)x->l[i];
+        r.v[2 * i + 1] = (uint32_t)(x->l[i] >> 32);
+    }
+    return r;
+}
+
+inline bool fr_is_canonical(const Fr& x) {
+    for (int i = 7; i >= 0; i--) {
+        if (x.v[i] < FrP::P[i]) return true;
+        if (x.v[i] > FrP::P[i]) return false;
+    }
+    return false;
+}
+
+}  // namespace eon

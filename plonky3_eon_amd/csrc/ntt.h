@@ -1,0 +1,43 @@
+// Internal NTT launch API (not part of the C ABI; see include/eon.h).
+#pragma once
+#include "field.h"
+
+namespace eon {
+
+enum LoadMode : uint32_t {
+    LOAD_DIRECT = 0,   // network position p reads source row p
+    LOAD_BITREV = 1,   // reads source row reverse_bits(p, load_param)
+    LOAD_SPREAD = 2,   // reads source row p >> load_param (LDE: bit-reversed coefficients spread)
+    LOAD_ZEROPAD = 3,  // reads source row p if p < load_param, else zero
+};
+
+constexpr uint32_t NATURAL_IDX = 0xffffffffu;
+
+// One radix-2 network of size 2^log_m over `width` independent columns.
+//   DIT (dif=false): stages first_stage .. log_m-1 ascending; bit-reversed input -> natural output.
+//   DIF (dif=true):  stages log_m-1 .. first_stage descending; natural input -> bit-reversed output.
+// The first pass reads `src` through the load transform (and may be out of place); later passes
+// run in place on `dst`.
+struct NetworkSpec {
+    bool dif = false;
+    uint32_t log_m = 0;
+    uint32_t first_stage = 0;
+    const Fr* src = nullptr;
+    Fr* dst = nullptr;
+    uint64_t width = 0;
+    const Fr* tw = nullptr;  // stage-concatenated twiddles (forward or inverse)
+    uint32_t load_mode = LOAD_DIRECT;
+    uint32_t load_param = 0;
+    const Fr* load_scale = nullptr;
+    uint32_t has_load_const = 0;
+    Fr load_const = Fr::one();
+    const Fr* store_scale = nullptr;
+    uint32_t max_stages_per_pass = 0;  // 0 = tile limit; tests force multi-pass plans with it
+};
+
+hipError_t run_network(const NetworkSpec& s, hipStream_t st);
+hipError_t launch_powers(Fr* out, uint64_t n, const Fr& base, const Fr& scale, uint32_t rev_log,
+                         hipStream_t st);
+hipError_t launch_twiddles(Fr* tw, uint32_t L, const Fr& root_L, hipStream_t st);
+
+}  // namespace eon

@@ -1,0 +1,295 @@
+// Batched radix-2 NTT over BN254 Fr on row-major matrices (gfx950).
+//
+// Semantics: p3-dft's TwoAdicSubgroupDft<Fr> (dft/src/traits.rs:27-249), with the output-order
+// conventions of Radix2Dit (natural, dft/src/radix_2_dit.rs:61-77) and Radix2DitParallel
+// (bit-reversed storage, dft/src/radix_2_dit_parallel.rs:146-228).  Any correct NTT returns the
+// same canonical field elements, so outputs are bit-exact with the reference.
+//
+// Structure (MI355X-first, not a translation of the rayon row-chunk schedule):
+//   * A size-2^L network is run as P "passes"; a pass executes k consecutive radix-2 stages
+//     [s0, s0+k) on every group of 2^k rows that share all index bits outside [s0, s0+k).
+//   * One workgroup = one group x CB adjacent columns.  The 2^k x CB tile is staged in LDS as two
+//     16-byte half-planes (conflict-free ds_read/write_b128), the pass's 2^k - 1 twiddles are
+//     staged beside it, and each thread does butterflies with the 256-bit Montgomery product in
+//     registers (field.h).  Global reads/writes are row segments of CB*32 contiguous bytes.
+//   * The first pass folds in the input permutation (bit-reversal gather, LDE spread, zero pad)
+//     and the coset/inverse scaling; the last pass folds in the output scaling.  No standalone
+//     permutation or scaling sweep touches HBM.
+//   * Twiddles: one stage-concatenated table tw[2^s + j] = w_{2^(s+1)}^j (inverse table with
+//     w^-1), built once on device for the largest size seen; smaller transforms use its prefix.
+#include "ntt.h"
+
+namespace eon {
+
+struct PassArgs {
+    const Fr* src;
+    Fr* dst;
+    const Fr* tw;
+    const Fr* load_scale;   // indexed by source row, or null
+    const Fr* store_scale;  // indexed by output row, or null
+    Fr load_const;
+    uint64_t width;
+    uint32_t s0;
+    uint32_t k;
+    uint32_t load_mode;
+    uint32_t load_param;
+    uint32_t has_load_const;
+};
+
+__device__ __forceinline__ void lds_put(uint4* lo, uint4* hi, uint32_t i, const Fr& x) {
+    lo[i] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+    hi[i] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+}
+
+__device__ __forceinline__ Fr lds_get(const uint4* lo, const uint4* hi, uint32_t i) {
+    const uint4 a = lo[i], b = hi[i];
+    Fr x;
+    x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
+    x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+    return x;
+}
+
+__device__ __forceinline__ Fr gload(const Fr* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 a = q[0], b = q[1];
+    Fr x;
+    x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
+    x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+    return x;
+}
+
+__device__ __forceinline__ void gstore(Fr* p, const Fr& x) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+    q[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+}
+
+template <bool DIF, int LOG_CB>
+__global__ void __launch_bounds__(256) k_ntt_pass(PassArgs a) {
+    constexpr uint32_t CB = 1u << LOG_CB;
+    extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+    const uint32_t k = a.k;
+    const uint32_t ne = CB << k;
+    uint4* lo = lds;
+    uint4* hi = lds + ne;
+    Fr* twl = reinterpret_cast<Fr*>(lds + 2 * ne);
+
+    const uint32_t s0 = a.s0;
+    const uint64_t g = blockIdx.x;
+    const uint64_t low = g & ((1ull << s0) - 1);
+    const uint64_t base_row = low + ((g >> s0) << (s0 + k));
+    const uint64_t col0 = (uint64_t)blockIdx.y * CB;
+    const uint64_t width = a.width;
+    const uint32_t T = blockDim.x;
+
+    // Stage the pass's twiddles: LDS slot 2^l + r holds the stage-(s0+l) twiddle for r.
+    for (uint32_t q = threadIdx.x + 1; q < (1u << k); q += T) {
+        const uint32_t l = 31 - __builtin_clz(q);
+        const uint32_t r = q - (1u << l);
+        const uint64_t s = s0 + l;
+        twl[q] = gload(a.tw + (1ull << s) + low + ((uint64_t)r << s0));
+    }
+
+    // Load the tile (row segments of CB columns), applying the input transform.
+    for (uint32_t e = threadIdx.x; e < ne; e += T) {
+        const uint32_t c = e & (CB - 1);
+        const uint32_t m = e >> LOG_CB;
+        const uint64_t p = base_row + ((uint64_t)m << s0);
+        const uint64_t col = col0 + c;
+        Fr x = Fr::zero();
+        if (col < width) {
+            uint64_t r = p;
+            bool present = true;
+            switch (a.load_mode) {
+                case LOAD_BITREV:
+                    r = a.load_param ? (__builtin_bitreverse64(p) >> (64 - a.load_param)) : 0;
+                    break;
+                case LOAD_SPREAD: r = p >> a.load_param; break;
+                case LOAD_ZEROPAD: present = p < a.load_param; break;
+                default: break;
+            }
+            if (present) {
+                x = gload(a.src + r * width + col);
+                if (a.load_scale) x = mul(x, gload(a.load_scale + r));
+                if (a.has_load_const) x = mul(x, a.load_const);
+            }
+        }
+        lds_put(lo, hi, e, x);
+    }
+    __syncthreads();
+
+    for (uint32_t it = 0; it < k; it++) {
+        const uint32_t l = DIF ? (k - 1 - it) : it;
+        const uint32_t half = 1u << l;
+        for (uint32_t b = threadIdx.x; b < (ne >> 1); b += T) {
+            const uint32_t c = b & (CB - 1);
+            const uint32_t j = b >> LOG_CB;
+            const uint32_t r = j & (half - 1);
+            const uint32_t m0 = ((j >> l) << (l + 1)) | r;
+            const uint32_t i0 = (m0 << LOG_CB) | c;
+            const uint32_t i1 = ((m0 + half) << LOG_CB) | c;
+            const Fr x = lds_get(lo, hi, i0);
+            const Fr y = lds_get(lo, hi, i1);
+            // the twiddle is 1 only for the first butterfly of a block in the group at low = 0
+            const bool unit = (r | low) == 0;
+            Fr u, v;
+            if (!DIF) {
+                // DitButterfly (dft/src/butterflies.rs:177-185): (x + w*y, x - w*y)
+                const Fr t = unit ? y : mul(y, twl[half + r]);
+                u = add(x, t);
+                v = sub(x, t);
+            } else {
+                // DIF butterfly: (x + y, (x - y) * w)
+                u = add(x, y);
+                const Fr d = sub(x, y);
+                v = unit ? d : mul(d, twl[half + r]);
+            }
+            lds_put(lo, hi, i0, u);
+            lds_put(lo, hi, i1, v);
+        }
+        __syncthreads();
+    }
+
+    for (uint32_t e = threadIdx.x; e < ne; e += T) {
+        const uint32_t c = e & (CB - 1);
+        const uint32_t m = e >> LOG_CB;
+        const uint64_t p = base_row + ((uint64_t)m << s0);
+        const uint64_t col = col0 + c;
+        if (col < width) {
+            Fr x = lds_get(lo, hi, e);
+            if (a.store_scale) x = mul(x, gload(a.store_scale + p));
+            gstore(a.dst + p * width + col, x);
+        }
+    }
+}
+
+// out[idx(j)] = scale * base^j for j in [0, n); idx(j) = j, or reverse_bits(j, rev_log) when
+// rev_log != NATURAL_IDX.  Each thread walks a contiguous chunk of exponents.
+__global__ void k_powers(Fr* out, uint64_t n, Fr base, Fr scale, uint32_t rev_log, uint32_t chunk) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t j0 = t * chunk;
+    if (j0 >= n) return;
+    // base^j0 by square-and-multiply
+    Fr acc = Fr::one(), b = base;
+    for (uint64_t e = j0; e; e >>= 1) {
+        if (e & 1) acc = mul(acc, b);
+        b = sqr(b);
+    }
+    acc = mul(acc, scale);
+    const uint64_t j1 = (j0 + chunk < n) ? j0 + chunk : n;
+    for (uint64_t j = j0; j < j1; j++) {
+        const uint64_t idx = rev_log == NATURAL_IDX ? j
+                             : (rev_log == 0 ? 0 : (__builtin_bitreverse64(j) >> (64 - rev_log)));
+        gstore(out + idx, acc);
+        acc = mul(acc, base);
+    }
+}
+
+// tw[2^s + j] = tw[2^(L-1) + (j << (L-1-s))] for s < L-1 (sub-sampling the largest stage).
+__global__ void k_tw_fill_lower(Fr* tw, uint32_t L) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t top = 1ull << (L - 1);
+    if (q == 0 || q >= top) return;
+    const uint32_t s = 63 - __builtin_clzll(q);
+    const uint64_t j = q - (1ull << s);
+    tw[q] = tw[top + (j << (L - 1 - s))];
+}
+
+static hipError_t launch_pass(bool dif, uint32_t log_cb, const PassArgs& a, uint64_t groups,
+                              uint64_t col_tiles, hipStream_t st) {
+    const uint32_t ne = (1u << log_cb) << a.k;
+    uint32_t threads = ne / 8;
+    if (threads < 64) threads = 64;
+    if (threads > 256) threads = 256;
+    const size_t lds = (size_t)ne * 32 + ((size_t)1 << a.k) * 32;
+    dim3 grid((unsigned)groups, (unsigned)col_tiles);
+#define EON_LAUNCH(D, C) \
+    hipLaunchKernelGGL((k_ntt_pass<D, C>), grid, dim3(threads), lds, st, a)
+    switch ((dif ? 4 : 0) + log_cb) {
+        case 0: EON_LAUNCH(false, 0); break;
+        case 1: EON_LAUNCH(false, 1); break;
+        case 2: EON_LAUNCH(false, 2); break;
+        case 3: EON_LAUNCH(false, 3); break;
+        case 4: EON_LAUNCH(true, 0); break;
+        case 5: EON_LAUNCH(true, 1); break;
+        case 6: EON_LAUNCH(true, 2); break;
+        case 7: EON_LAUNCH(true, 3); break;
+    }
+#undef EON_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_powers(Fr* out, uint64_t n, const Fr& base, const Fr& scale, uint32_t rev_log,
+                         hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint32_t chunk = n >= (1u << 16) ? 64 : 1;
+    const uint64_t threads = (n + chunk - 1) / chunk;
+    const uint32_t bs = 256;
+    hipLaunchKernelGGL(k_powers, dim3((unsigned)((threads + bs - 1) / bs)), dim3(bs), 0, st, out, n,
+                       base, scale, rev_log, chunk);
+    return hipGetLastError();
+}
+
+hipError_t launch_twiddles(Fr* tw, uint32_t L, const Fr& root_L, hipStream_t st) {
+    // tw has 2^L entries; tw[0] unused.  Stage L-1 table = root_L^j, j < 2^(L-1).
+    if (L == 0) return hipSuccess;
+    hipError_t e = launch_powers(tw + (1ull << (L - 1)), 1ull << (L - 1), root_L, Fr::one(),
+                                 NATURAL_IDX, st);
+    if (e != hipSuccess || L == 1) return e;
+    const uint64_t n = 1ull << (L - 1);
+    hipLaunchKernelGGL(k_tw_fill_lower, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, tw, L);
+    return hipGetLastError();
+}
+
+static uint32_t pick_log_cb(uint64_t width) {
+    if (width >= 8) return 3;
+    if (width >= 4) return 2;
+    if (width >= 2) return 1;
+    return 0;
+}
+
+hipError_t run_network(const NetworkSpec& s, hipStream_t st) {
+    const uint32_t log_cb = pick_log_cb(s.width);
+    uint32_t kmax = 10 - log_cb;  // 1024 elements per tile (32 KiB of LDS)
+    if (s.max_stages_per_pass && s.max_stages_per_pass < kmax) kmax = s.max_stages_per_pass;
+    const uint32_t lo_stage = s.first_stage;
+    const uint32_t n_st = s.log_m > lo_stage ? s.log_m - lo_stage : 0;
+    const uint32_t passes = n_st == 0 ? 1 : (n_st + kmax - 1) / kmax;
+    const uint64_t col_tiles = (s.width + (1u << log_cb) - 1) >> log_cb;
+    // balanced chunk sizes, assigned bottom-up (stage ranges ascending)
+    uint32_t ks[32], s0s[32];
+    uint32_t acc = lo_stage;
+    for (uint32_t i = 0; i < passes; i++) {
+        ks[i] = n_st / passes + (i < n_st % passes ? 1 : 0);
+        s0s[i] = acc;
+        acc += ks[i];
+    }
+    for (uint32_t it = 0; it < passes; it++) {
+        // DIT runs the stage chunks low -> high, DIF high -> low
+        const uint32_t i = s.dif ? passes - 1 - it : it;
+        PassArgs a{};
+        const bool first = it == 0, last = it == passes - 1;
+        a.src = first ? s.src : s.dst;
+        a.dst = s.dst;
+        a.tw = s.tw;
+        a.width = s.width;
+        a.s0 = s0s[i];
+        a.k = ks[i];
+        if (first) {
+            a.load_mode = s.load_mode;
+            a.load_param = s.load_param;
+            a.load_scale = s.load_scale;
+            a.has_load_const = s.has_load_const;
+            a.load_const = s.load_const;
+        } else {
+            a.load_mode = LOAD_DIRECT;
+        }
+        a.store_scale = last ? s.store_scale : nullptr;
+        const uint64_t groups = (1ull << s.log_m) >> a.k;
+        hipError_t e = launch_pass(s.dif, log_cb, a, groups, col_tiles, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace eon

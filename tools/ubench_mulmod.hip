@@ -1,0 +1,101 @@
+// Microbenchmark: 256-bit Montgomery multiply throughput on gfx950 (Fr and Fq), with 1/2/4
+// independent chains per thread.  Prints mulmod/s so the NTT/MSM rooflines use a measured peak.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+#include "../plonky3_eon_amd/csrc/field.h"
+
+using namespace eon;
+
+template <class M, int CH, bool FIPS>
+__global__ void __launch_bounds__(256) k_mul(const Fe<M>* in, Fe<M>* out, int iters) {
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    Fe<M> x[CH];
+    Fe<M> y = in[(tid + 7) & 1023];
+#pragma unroll
+    for (int c = 0; c < CH; c++) x[c] = in[(tid + c) & 1023];
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int c = 0; c < CH; c++) x[c] = FIPS ? mul_fips(x[c], y) : mul_cios(x[c], y);
+    }
+    Fe<M> acc = x[0];
+#pragma unroll
+    for (int c = 1; c < CH; c++) acc = add(acc, x[c]);
+    out[tid] = acc;
+}
+
+template <class M>
+__global__ void k_check(const Fe<M>* a, const Fe<M>* b, int n, unsigned* bad, Fe<M>* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fe<M> x = mul_cios(a[i], b[i]), y = mul_fips(a[i], b[i]);
+    if (x != y) atomicAdd(bad, 1u);
+    out[i] = y;
+}
+
+template <class M, int CH, bool FIPS>
+void run(const char* name, Fe<M>* d_in, Fe<M>* d_out, int blocks, int iters) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    k_mul<M, CH, FIPS><<<blocks, 256>>>(d_in, d_out, 16);
+    hipDeviceSynchronize();
+    hipEventRecord(a);
+    k_mul<M, CH, FIPS><<<blocks, 256>>>(d_in, d_out, iters);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    double n = (double)blocks * 256 * iters * CH;
+    printf("{\"field\":\"%s\",\"fips\":%d,\"chains\":%d,\"blocks\":%d,\"ms\":%.3f,\"mulmod_per_s\":%.4e}\n", name, (int)FIPS, CH,
+           blocks, ms, n / (ms * 1e-3));
+}
+
+int main() {
+    std::vector<Fr> h(1024);
+    for (int i = 0; i < 1024; i++) h[i] = from_u64<FrP>(0x9e3779b97f4a7c15ull * (i + 1));
+    Fr *d_in, *d_out;
+    const int maxblocks = 256 * 32;
+    hipMalloc(&d_in, 1024 * sizeof(Fr));
+    hipMalloc(&d_out, (size_t)maxblocks * 256 * sizeof(Fr));
+    hipMemcpy(d_in, h.data(), 1024 * sizeof(Fr), hipMemcpyHostToDevice);
+    {
+        // correctness: GENERATOR = 5 in Montgomery form (bn254/src/field.rs:372-377)
+        Fr g = from_u64<FrP>(5);
+        const uint32_t G[8] = {0x9fffffe6u, 0x1b0d0ef9u, 0xa32a913fu, 0xeaba68a3u,
+                               0xd8dd0689u, 0x47d8eb76u, 0x20f5bbc3u, 0x15d00855u};
+        bool ok = true;
+        for (int i = 0; i < 8; i++) ok &= g.v[i] == G[i];
+        printf("{\"host_generator_ok\":%d}\n", (int)ok);
+        const int n = 1 << 20;
+        std::vector<Fr> ha(n), hb(n);
+        uint64_t st = 1;
+        auto nx = [&]() { st += 0x9e3779b97f4a7c15ull; uint64_t z = st; z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull; z = (z ^ (z >> 27)) * 0x94d049bb133111ebull; return z ^ (z >> 31); };
+        for (int i = 0; i < n; i++) {
+            ha[i] = from_u64<FrP>(nx()); ha[i] = mul(ha[i], from_u64<FrP>(nx()));
+            hb[i] = from_u64<FrP>(nx()); hb[i] = mul(hb[i], hb[i]);
+        }
+        hb[0] = Fr::zero(); ha[1] = neg(Fr::one()); hb[1] = neg(Fr::one());
+        Fr *da, *db, *dout; unsigned* dbad;
+        hipMalloc(&da, n * sizeof(Fr)); hipMalloc(&db, n * sizeof(Fr)); hipMalloc(&dout, n * sizeof(Fr));
+        hipMalloc(&dbad, 4); hipMemset(dbad, 0, 4);
+        hipMemcpy(da, ha.data(), n * sizeof(Fr), hipMemcpyHostToDevice);
+        hipMemcpy(db, hb.data(), n * sizeof(Fr), hipMemcpyHostToDevice);
+        k_check<FrP><<<n / 256, 256>>>(da, db, n, dbad, dout);
+        unsigned bad = 0; hipMemcpy(&bad, dbad, 4, hipMemcpyDeviceToHost);
+        std::vector<Fr> ho(n); hipMemcpy(ho.data(), dout, n * sizeof(Fr), hipMemcpyDeviceToHost);
+        unsigned badh = 0;
+        for (int i = 0; i < n; i += 97) badh += (mul(ha[i], hb[i]) != ho[i]);
+        printf("{\"device_fips_vs_cios_mismatch\":%u,\"device_vs_host_mismatch\":%u}\n", bad, badh);
+    }
+    for (int blocks : {256 * 8, 256 * 16}) {
+        run<FrP, 1, false>("Fr", d_in, d_out, blocks, 4096);
+        run<FrP, 2, false>("Fr", d_in, d_out, blocks, 2048);
+        run<FrP, 4, false>("Fr", d_in, d_out, blocks, 1024);
+        run<FqP, 2, false>("Fq", (Fq*)d_in, (Fq*)d_out, blocks, 2048);
+        run<FrP, 1, true>("Fr", d_in, d_out, blocks, 4096);
+        run<FrP, 2, true>("Fr", d_in, d_out, blocks, 2048);
+        run<FrP, 4, true>("Fr", d_in, d_out, blocks, 1024);
+    }
+    return 0;
+}

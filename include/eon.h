@@ -64,9 +64,16 @@ enum {
 int eon_ctx_create(int device_ordinal, eon_ctx** out);
 void eon_ctx_destroy(eon_ctx* ctx);
 const char* eon_last_error(const eon_ctx* ctx);
-/* stream (a hipStream_t) used by the *_dev entry points; NULL = the context's own stream */
+/* Stream (a hipStream_t) for all subsequent work of this context, used verbatim: NULL selects
+ * the HIP null (default) stream.  Until the first call the context uses a stream of its own. */
 int eon_ctx_set_stream(eon_ctx* ctx, void* hip_stream);
 int eon_ctx_synchronize(eon_ctx* ctx);
+/* Per-launch kernel timing with HIP events on the launch stream (the analogue of the
+ * reference's tracing spans, e.g. dft/src/radix_2_dit_parallel.rs:168).  eon_ctx_profile(ctx, 1)
+ * clears the record and starts recording; eon_ctx_profile_report writes a JSON object
+ * {kernel: {launches, total_ms, alg_bytes}} into buf (synchronizes on the recorded events). */
+int eon_ctx_profile(eon_ctx* ctx, int enable);
+int eon_ctx_profile_report(eon_ctx* ctx, char* buf, uint64_t len);
 /* ABI version; bumped on any signature change */
 uint32_t eon_abi_version(void);
 
@@ -88,7 +95,7 @@ int eon_coset_idft_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t h
 /* coset_lde_batch (dft/src/traits.rs:226-249; Radix2DitParallel override at
  * dft/src/radix_2_dit_parallel.rs:169-228): evaluations on H -> evaluations on shift*K,
  * |K| = height << added_bits.  `out` holds (height << added_bits) x width.  shift NULL = ONE
- * (lde_batch, dft/src/traits.rs:187-192).  Must not alias `in`. */
+ * (lde_batch, dft/src/traits.rs:187-192).  `shift` is always a host pointer. */
 int eon_coset_lde_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
                         uint32_t width, uint32_t added_bits, const eon_fr* shift, int out_order);
 

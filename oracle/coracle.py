@@ -1,0 +1,192 @@
+"""ctypes binding of the C restatement oracle (oracle/eon_oracle.c -> oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY (tests/, __graft_entry__.smoke(), bench.py cpu_baseline).
+Matrices are numpy uint64 arrays of shape (h, w, 4): Fr Montgomery limbs, row-major.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "liboracle.so"
+
+
+class fr_t(ctypes.Structure):
+    _fields_ = [("v", ctypes.c_uint64 * 4)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        l = ctypes.CDLL(os.fspath(LIB))
+        P, U64, U32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
+        sigs = {
+            "or_radix2dit_dft_batch": [P, U64, U64],
+            "or_idft_batch": [P, U64, U64],
+            "or_coset_dft_batch": [P, U64, U64, fr_t],
+            "or_coset_idft_batch": [P, U64, U64, fr_t],
+            "or_coset_lde_batch": [P, P, U64, U64, U32, fr_t],
+            "or_r2dp_dft_batch": [P, U64, U64],
+            "or_r2dp_coset_lde_batch": [P, P, U64, U64, U32, fr_t],
+            "or_fr_mul_batch": [P, P, P, U64],
+            "or_reverse_matrix_index_bits": [P, U64, U64],
+        }
+        for k, a in sigs.items():
+            getattr(l, k).argtypes = a
+            getattr(l, k).restype = None
+        l.or_fr_from_u64.argtypes = [U64]
+        l.or_fr_from_u64.restype = fr_t
+        l.or_two_adic_generator.argtypes = [U32]
+        l.or_two_adic_generator.restype = fr_t
+        l.or_fr_pow.argtypes = [fr_t, U64]
+        l.or_fr_pow.restype = fr_t
+        l.or_num_threads.restype = ctypes.c_int
+        l.or_eval_poly_col.argtypes = [P, U64, U64, U64, fr_t]
+        l.or_eval_poly_col.restype = fr_t
+        l.or_kzg_evaluations_on_domain.argtypes = [P, U64, U64, U32, fr_t, P]
+        l.or_kzg_evaluations_on_domain.restype = None
+        _lib = l
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def fr(limbs) -> fr_t:
+    s = fr_t()
+    for i in range(4):
+        s.v[i] = int(limbs[i])
+    return s
+
+
+def fr_from_u64(x: int):
+    r = lib().or_fr_from_u64(x)
+    return np.array([r.v[i] for i in range(4)], dtype=np.uint64)
+
+
+def _copy(m):
+    return np.ascontiguousarray(m, dtype=np.uint64).copy()
+
+
+def dft_batch(m):
+    x = _copy(m)
+    lib().or_radix2dit_dft_batch(_ptr(x), x.shape[0], x.shape[1])
+    return x
+
+
+def idft_batch(m):
+    x = _copy(m)
+    lib().or_idft_batch(_ptr(x), x.shape[0], x.shape[1])
+    return x
+
+
+def coset_dft_batch(m, shift_limbs):
+    x = _copy(m)
+    lib().or_coset_dft_batch(_ptr(x), x.shape[0], x.shape[1], fr(shift_limbs))
+    return x
+
+
+def coset_idft_batch(m, shift_limbs):
+    x = _copy(m)
+    lib().or_coset_idft_batch(_ptr(x), x.shape[0], x.shape[1], fr(shift_limbs))
+    return x
+
+
+def coset_lde_batch(m, added_bits, shift_limbs):
+    x = np.ascontiguousarray(m, dtype=np.uint64)
+    out = np.empty((x.shape[0] << added_bits, x.shape[1], 4), dtype=np.uint64)
+    lib().or_coset_lde_batch(_ptr(x), _ptr(out), x.shape[0], x.shape[1], added_bits, fr(shift_limbs))
+    return out
+
+
+def r2dp_dft_batch(m):
+    """Radix2DitParallel::dft_batch storage (bit-reversed)."""
+    x = _copy(m)
+    lib().or_r2dp_dft_batch(_ptr(x), x.shape[0], x.shape[1])
+    return x
+
+
+def r2dp_coset_lde_batch(m, added_bits, shift_limbs):
+    """Radix2DitParallel::coset_lde_batch storage (bit-reversed)."""
+    x = np.ascontiguousarray(m, dtype=np.uint64)
+    out = np.empty((x.shape[0] << added_bits, x.shape[1], 4), dtype=np.uint64)
+    lib().or_r2dp_coset_lde_batch(_ptr(x), _ptr(out), x.shape[0], x.shape[1], added_bits, fr(shift_limbs))
+    return out
+
+
+def bit_reverse_rows(m):
+    x = _copy(m)
+    lib().or_reverse_matrix_index_bits(_ptr(x), x.shape[0], x.shape[1])
+    return x
+
+
+def eval_poly_col(coeffs, col: int, point_limbs):
+    """eval_poly (kzg/src/util.rs:63-68) of column `col` at a point (Montgomery limbs)."""
+    x = np.ascontiguousarray(coeffs, dtype=np.uint64)
+    r = lib().or_eval_poly_col(_ptr(x), x.shape[0], x.shape[1], col, fr(point_limbs))
+    return np.array([r.v[i] for i in range(4)], dtype=np.uint64)
+
+
+def kzg_evaluations_on_domain(coeffs, log_q: int, shift_limbs):
+    """KzgPcs::get_evaluations_on_domain (kzg/src/pcs.rs:267-287): Horner at every point."""
+    x = np.ascontiguousarray(coeffs, dtype=np.uint64)
+    out = np.empty((1 << log_q, x.shape[1], 4), dtype=np.uint64)
+    lib().or_kzg_evaluations_on_domain(_ptr(x), x.shape[0], x.shape[1], log_q, fr(shift_limbs), _ptr(out))
+    return out
+
+
+def fr_pow(base_limbs, e: int):
+    r = lib().or_fr_pow(fr(base_limbs), e)
+    return np.array([r.v[i] for i in range(4)], dtype=np.uint64)
+
+
+def fr_mul(a, b):
+    a = np.ascontiguousarray(a, dtype=np.uint64).reshape(1, 4)
+    b = np.ascontiguousarray(b, dtype=np.uint64).reshape(1, 4)
+    r = np.empty_like(a)
+    lib().or_fr_mul_batch(_ptr(a), _ptr(b), _ptr(r), 1)
+    return r[0]
+
+
+def two_adic_generator(bits: int):
+    r = lib().or_two_adic_generator(bits)
+    return np.array([r.v[i] for i in range(4)], dtype=np.uint64)
+
+
+def num_threads() -> int:
+    return lib().or_num_threads()
+
+
+def random_fr(seed: int, n: int) -> np.ndarray:
+    """n uniform canonical Montgomery residues (rejection sampling as bn254/src/field.rs:534-551),
+    numpy PCG64 stream -- deterministic test inputs."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    P = [0x43E1F593F0000001, 0x2833E84879B97091, 0xB85045B68181585D, 0x30644E72E131A029]
+    out = np.empty((0, 4), dtype=np.uint64)
+    while out.shape[0] < n:
+        c = rng.integers(0, 2**64, size=(2 * (n - out.shape[0]) + 16, 4), dtype=np.uint64)
+        c[:, 3] &= np.uint64((1 << 62) - 1)
+        # accept if c < P (compare limbs from the top)
+        lt = np.zeros(c.shape[0], dtype=bool)
+        eq = np.ones(c.shape[0], dtype=bool)
+        for i in (3, 2, 1, 0):
+            lt |= eq & (c[:, i] < np.uint64(P[i]))
+            eq &= c[:, i] == np.uint64(P[i])
+        out = np.concatenate([out, c[lt]])
+    return out[:n]

@@ -1,0 +1,481 @@
+/*
+ * eon_oracle.c -- CPU restatement of the reference's hot-path algorithms, in C (OpenMP).
+ *
+ * TEST INFRASTRUCTURE ONLY: the checker for parity tests and the `cpu_baseline` leg of bench.py
+ * (cpu_baseline.kind = "port").  Nothing in plonky3_eon_amd/ links or calls this.
+ *
+ * Restated (reference = Lolazyx/plonky3-eon; read as text, not compiled -- it is Rust with
+ * crates.io dependencies absent here):
+ *   - Fr arithmetic: bn254/src/helpers.rs:60-205 (wrapping add/sub, mul_small,
+ *     mul_small_and_acc, interleaved_monty_reduction with mu = p^-1 mod 2^64, monty_mul) and
+ *     bn254/src/field.rs:464-526 (add/sub/mul), :553-574 (two_adic_generator).
+ *   - Radix2Dit::dft_batch (dft/src/radix_2_dit.rs:61-122) and the trait defaults
+ *     idft/coset_dft/coset_idft/coset_lde (dft/src/traits.rs:83-249, dft/src/util.rs:15-36).
+ *   - Radix2DitParallel::dft_batch / coset_lde_batch with its two-half schedule
+ *     (dft/src/radix_2_dit_parallel.rs:53-553), OpenMP standing in for rayon's
+ *     par_row_chunks_exact_mut; reverse_matrix_index_bits (matrix/src/util.rs:36-57).
+ */
+#include "eon_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+
+static const uint64_t P[4] = {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull,
+                              0x30644e72e131a029ull};
+static const uint64_t MU = 0x3d1e0a6c10000001ull; /* P^-1 mod 2^64 (bn254/src/field.rs:40) */
+static const uint64_t R2[4] = {0x1bb8e645ae216da7ull, 0x53fe3ab1e35c59e3ull, 0x8c49833d53bb8085ull,
+                               0x0216d0b17f4e44a5ull};
+static const uint64_t ONE[4] = {0xac96341c4ffffffbull, 0x36fc76959f60cd29ull, 0x666ea36f7879462eull,
+                                0x0e0a77c19a07df2full};
+static const uint64_t TWO_ADIC_GEN[4] = {0x636e735580d13d9cull, 0xa22bf3742445ffd6ull,
+                                         0x56452ac01eb203d8ull, 0x1860ef942963f9e7ull};
+
+/* ---- Fr (bn254/src/helpers.rs, bn254/src/field.rs) ----------------------------------------- */
+static inline int wrapping_add4(const uint64_t* a, const uint64_t* b, uint64_t* o) {
+    u128 c = 0;
+    for (int i = 0; i < 4; i++) {
+        c += (u128)a[i] + b[i];
+        o[i] = (uint64_t)c;
+        c >>= 64;
+    }
+    return (int)c;
+}
+
+static inline int wrapping_sub4(const uint64_t* a, const uint64_t* b, uint64_t* o) {
+    int borrow = 0;
+    for (int i = 0; i < 4; i++) {
+        uint64_t d = a[i] - b[i];
+        int b1 = a[i] < b[i];
+        uint64_t e = d - (uint64_t)borrow;
+        int b2 = d < (uint64_t)borrow;
+        o[i] = e;
+        borrow = b1 | b2;
+    }
+    return borrow;
+}
+
+static inline uint64_t mul_small_and_acc(const uint64_t* lhs, uint64_t rhs, const uint64_t* add,
+                                         uint64_t* out) {
+    u128 acc = (u128)lhs[0] * rhs + (add ? add[0] : 0);
+    uint64_t out0 = (uint64_t)acc;
+    acc >>= 64;
+    for (int i = 1; i < 4; i++) {
+        acc += (u128)lhs[i] * rhs + (add ? add[i] : 0);
+        out[i - 1] = (uint64_t)acc;
+        acc >>= 64;
+    }
+    out[3] = (uint64_t)acc;
+    return out0;
+}
+
+static inline void interleaved_monty_reduction(uint64_t acc0, const uint64_t* acc, uint64_t* res) {
+    uint64_t t = acc0 * MU, u[4], sub[4];
+    (void)mul_small_and_acc(P, t, NULL, u);
+    if (wrapping_sub4(acc, u, sub)) {
+        wrapping_add4(sub, P, res);
+    } else {
+        memcpy(res, sub, 32);
+    }
+}
+
+void or_fr_mul(const fr_t* a, const fr_t* b, fr_t* r) {
+    /* monty_mul (bn254/src/helpers.rs:188-205) */
+    uint64_t acc[4], res[4];
+    uint64_t acc0 = mul_small_and_acc(a->v, b->v[0], NULL, acc);
+    interleaved_monty_reduction(acc0, acc, res);
+    for (int i = 1; i < 4; i++) {
+        acc0 = mul_small_and_acc(a->v, b->v[i], res, acc);
+        interleaved_monty_reduction(acc0, acc, res);
+    }
+    memcpy(r->v, res, 32);
+}
+
+void or_fr_add(const fr_t* a, const fr_t* b, fr_t* r) {
+    /* Fr::add (bn254/src/field.rs:464-489) */
+    uint64_t sum[4], corr[4];
+    wrapping_add4(a->v, b->v, sum);
+    if (wrapping_sub4(sum, P, corr))
+        memcpy(r->v, sum, 32);
+    else
+        memcpy(r->v, corr, 32);
+}
+
+void or_fr_sub(const fr_t* a, const fr_t* b, fr_t* r) {
+    /* Fr::sub (bn254/src/field.rs:491-508) */
+    uint64_t d[4];
+    if (wrapping_sub4(a->v, b->v, d)) wrapping_add4(d, P, d);
+    memcpy(r->v, d, 32);
+}
+
+static inline fr_t fmul(fr_t a, fr_t b) {
+    fr_t r;
+    or_fr_mul(&a, &b, &r);
+    return r;
+}
+static inline fr_t fadd(fr_t a, fr_t b) {
+    fr_t r;
+    or_fr_add(&a, &b, &r);
+    return r;
+}
+static inline fr_t fsub(fr_t a, fr_t b) {
+    fr_t r;
+    or_fr_sub(&a, &b, &r);
+    return r;
+}
+static inline fr_t fone(void) {
+    fr_t r;
+    memcpy(r.v, ONE, 32);
+    return r;
+}
+
+fr_t or_fr_from_u64(uint64_t x) {
+    /* Fr::new (bn254/src/field.rs:111-117): monty_mul(R^2, [x,0,0,0]) */
+    fr_t a = {{x, 0, 0, 0}}, r2;
+    memcpy(r2.v, R2, 32);
+    return fmul(r2, a);
+}
+
+fr_t or_fr_pow(fr_t b, uint64_t e) {
+    fr_t r = fone();
+    while (e) {
+        if (e & 1) r = fmul(r, b);
+        b = fmul(b, b);
+        e >>= 1;
+    }
+    return r;
+}
+
+fr_t or_fr_inverse(fr_t a) {
+    /* a^(p-2); the reference uses a gcd inversion (bn254/src/helpers.rs:417), same value */
+    uint64_t e[4];
+    const uint64_t two[4] = {2, 0, 0, 0};
+    wrapping_sub4(P, two, e);
+    fr_t r = fone();
+    for (int w = 3; w >= 0; w--)
+        for (int bit = 63; bit >= 0; bit--) {
+            r = fmul(r, r);
+            if ((e[w] >> bit) & 1) r = fmul(r, a);
+        }
+    return r;
+}
+
+fr_t or_two_adic_generator(uint32_t bits) {
+    fr_t w;
+    memcpy(w.v, TWO_ADIC_GEN, 32);
+    for (uint32_t i = bits; i < 28; i++) w = fmul(w, w);
+    return w;
+}
+
+static inline uint64_t rev_bits(uint64_t x, uint32_t bits) {
+    /* p3_util::reverse_bits_len (util/src/lib.rs:70-78) */
+    uint64_t r = 0;
+    for (uint32_t i = 0; i < bits; i++) {
+        r = (r << 1) | (x & 1);
+        x >>= 1;
+    }
+    return r;
+}
+
+static uint32_t log2_strict(uint64_t n) { return 63 - __builtin_clzll(n); }
+
+/* ---- matrix helpers ------------------------------------------------------------------------ */
+static void swap_rows(fr_t* m, uint64_t w, uint64_t i, uint64_t j) {
+    for (uint64_t c = 0; c < w; c++) {
+        fr_t t = m[i * w + c];
+        m[i * w + c] = m[j * w + c];
+        m[j * w + c] = t;
+    }
+}
+
+void or_reverse_matrix_index_bits(fr_t* m, uint64_t h, uint64_t w) {
+    /* matrix/src/util.rs:36-57 */
+    uint32_t lg = log2_strict(h);
+#pragma omp parallel for schedule(static)
+    for (uint64_t i = 0; i < h; i++) {
+        uint64_t j = rev_bits(i, lg);
+        if (i < j) swap_rows(m, w, i, j);
+    }
+}
+
+static void butterfly_rows(fr_t* lo, fr_t* hi, uint64_t w, fr_t t) {
+    /* DitButterfly (dft/src/butterflies.rs:177-185) */
+    for (uint64_t c = 0; c < w; c++) {
+        fr_t x2t = fmul(hi[c], t);
+        fr_t x1 = lo[c];
+        lo[c] = fadd(x1, x2t);
+        hi[c] = fsub(x1, x2t);
+    }
+}
+
+static void powers(fr_t base, fr_t start, uint64_t n, fr_t* out) {
+    fr_t cur = start;
+    for (uint64_t i = 0; i < n; i++) {
+        out[i] = cur;
+        cur = fmul(cur, base);
+    }
+}
+
+static void reverse_slice(fr_t* v, uint64_t n) {
+    if (n <= 1) return;
+    uint32_t lg = log2_strict(n);
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t j = rev_bits(i, lg);
+        if (i < j) {
+            fr_t t = v[i];
+            v[i] = v[j];
+            v[j] = t;
+        }
+    }
+}
+
+/* ---- Radix2Dit (dft/src/radix_2_dit.rs:61-122) --------------------------------------------- */
+void or_radix2dit_dft_batch(fr_t* m, uint64_t h, uint64_t w) {
+    uint32_t log_h = log2_strict(h);
+    fr_t* tw = (fr_t*)malloc(sizeof(fr_t) * (h ? h : 1));
+    powers(or_two_adic_generator(log_h), fone(), h, tw);
+    or_reverse_matrix_index_bits(m, h, w);
+    for (uint32_t layer = 0; layer < log_h; layer++) {
+        uint32_t layer_rev = log_h - 1 - layer;
+        uint64_t half = 1ull << layer, block = half * 2;
+#pragma omp parallel for schedule(static)
+        for (uint64_t b = 0; b < h / block; b++) {
+            for (uint64_t ind = 0; ind < half; ind++) {
+                fr_t* lo = m + (b * block + ind) * w;
+                fr_t* hi = m + (b * block + half + ind) * w;
+                if (ind == 0) {
+                    for (uint64_t c = 0; c < w; c++) { /* TwiddleFreeButterfly */
+                        fr_t x1 = lo[c], x2 = hi[c];
+                        lo[c] = fadd(x1, x2);
+                        hi[c] = fsub(x1, x2);
+                    }
+                } else {
+                    butterfly_rows(lo, hi, w, tw[ind << layer_rev]);
+                }
+            }
+        }
+    }
+    free(tw);
+}
+
+static void scale_all(fr_t* m, uint64_t n, fr_t s) {
+#pragma omp parallel for schedule(static)
+    for (uint64_t i = 0; i < n; i++) m[i] = fmul(m[i], s);
+}
+
+static void coset_shift_cols(fr_t* m, uint64_t h, uint64_t w, fr_t shift) {
+    /* dft/src/util.rs:28-36 */
+    fr_t* p = (fr_t*)malloc(sizeof(fr_t) * h);
+    powers(shift, fone(), h, p);
+#pragma omp parallel for schedule(static)
+    for (uint64_t r = 0; r < h; r++)
+        for (uint64_t c = 0; c < w; c++) m[r * w + c] = fmul(m[r * w + c], p[r]);
+    free(p);
+}
+
+void or_idft_batch(fr_t* m, uint64_t h, uint64_t w) {
+    /* dft/src/traits.rs:111-122 over Radix2Dit: dft, divide_by_height, swap rows r <-> h-r */
+    or_radix2dit_dft_batch(m, h, w);
+    scale_all(m, h * w, or_fr_inverse(or_fr_from_u64(h)));
+    for (uint64_t r = 1; r < h / 2; r++) swap_rows(m, w, r, h - r);
+}
+
+void or_coset_dft_batch(fr_t* m, uint64_t h, uint64_t w, fr_t shift) {
+    coset_shift_cols(m, h, w, shift); /* dft/src/traits.rs:83-91 */
+    or_radix2dit_dft_batch(m, h, w);
+}
+
+void or_coset_idft_batch(fr_t* m, uint64_t h, uint64_t w, fr_t shift) {
+    or_idft_batch(m, h, w); /* dft/src/traits.rs:144-153 */
+    coset_shift_cols(m, h, w, or_fr_inverse(shift));
+}
+
+void or_coset_lde_batch(const fr_t* in, fr_t* out, uint64_t h, uint64_t w, uint32_t added_bits,
+                        fr_t shift) {
+    /* dft/src/traits.rs:226-249 (default path, natural order) */
+    memcpy(out, in, sizeof(fr_t) * h * w);
+    or_idft_batch(out, h, w);
+    memset(out + h * w, 0, sizeof(fr_t) * ((h << added_bits) - h) * w);
+    or_coset_dft_batch(out, h << added_bits, w, shift);
+}
+
+/* ---- Radix2DitParallel (dft/src/radix_2_dit_parallel.rs) ----------------------------------- */
+/* dit_layer (:452-484): blocks of 2^(layer+1) rows, twiddle i = tw[i * tw_stride] */
+static void dit_layer(fr_t* sub, uint64_t rows, uint64_t w, uint32_t layer, const fr_t* tw,
+                      uint64_t tw_stride) {
+    uint64_t half = 1ull << layer, block = half * 2;
+    for (uint64_t b = 0; b < rows / block; b++)
+        for (uint64_t i = 0; i < half; i++)
+            butterfly_rows(sub + (b * block + i) * w, sub + (b * block + half + i) * w, w,
+                           tw[i * tw_stride]);
+}
+
+/* dit_layer_rev (:524-553): blocks of 2^(layer_rev+1) rows, block b uses twiddles_rev[b] */
+static void dit_layer_rev(fr_t* sub, uint64_t rows, uint64_t w, uint32_t log_h, uint32_t layer,
+                          const fr_t* tw_rev) {
+    uint32_t layer_rev = log_h - 1 - layer;
+    uint64_t half = 1ull << layer_rev, block = half * 2;
+    /* the whole half-block is one (lo, hi) pair of slices, one twiddle per block */
+    for (uint64_t b = 0; b < rows / block; b++)
+        butterfly_rows(sub + b * block * w, sub + (b * block + half) * w, half * w, tw_rev[b]);
+}
+
+/* first_half (:296-315) with uniform twiddles; per-layer twiddles when coset != NULL
+ * (first_half_general, :320-335) */
+static void first_half(fr_t* m, uint64_t h, uint64_t w, uint32_t mid, const fr_t* tw,
+                       fr_t* const* coset) {
+    uint32_t log_h = log2_strict(h);
+    uint64_t chunk = 1ull << mid;
+#pragma omp parallel for schedule(static)
+    for (uint64_t t = 0; t < h / chunk; t++) {
+        fr_t* sub = m + t * chunk * w;
+        for (uint32_t layer = 0; layer < mid; layer++) {
+            uint32_t layer_rev = log_h - 1 - layer;
+            if (coset)
+                dit_layer(sub, chunk, w, layer, coset[layer_rev], 1);
+            else
+                dit_layer(sub, chunk, w, layer, tw, 1ull << layer_rev);
+        }
+    }
+}
+
+/* second_half (:393-421, optional scale) / second_half_general (:426-449) */
+static void second_half(fr_t* m, uint64_t h, uint64_t w, uint32_t mid, const fr_t* tw_rev,
+                        fr_t* const* coset, const fr_t* scale) {
+    uint32_t log_h = log2_strict(h);
+    uint64_t chunk = 1ull << (log_h - mid);
+#pragma omp parallel for schedule(static)
+    for (uint64_t t = 0; t < h / chunk; t++) {
+        fr_t* sub = m + t * chunk * w;
+        if (scale)
+            for (uint64_t i = 0; i < chunk * w; i++) sub[i] = fmul(sub[i], *scale);
+        for (uint32_t layer = mid; layer < log_h; layer++) {
+            uint64_t first_block = t << (layer - mid);
+            uint32_t layer_rev = log_h - 1 - layer;
+            const fr_t* twr = coset ? coset[layer_rev] : tw_rev;
+            dit_layer_rev(sub, chunk, w, log_h, layer, twr + first_block);
+        }
+    }
+}
+
+/* get_or_compute_coset_twiddles (:80-115): layer l holds shift^(2^l) * (root^(2^l))^j for
+ * j < h >> (l+1), bit-reversed when log_h - 1 - l >= mid */
+static fr_t** coset_twiddles(uint32_t log_h, fr_t shift) {
+    uint32_t mid = (log_h + 1) / 2;
+    uint64_t h = 1ull << log_h;
+    fr_t root = or_two_adic_generator(log_h);
+    fr_t** tw = (fr_t**)calloc(log_h ? log_h : 1, sizeof(fr_t*));
+    fr_t shift_pow = shift, root_pow = root;
+    for (uint32_t layer = 0; layer < log_h; layer++) {
+        uint64_t n = h >> (layer + 1);
+        tw[layer] = (fr_t*)malloc(sizeof(fr_t) * n);
+        powers(root_pow, shift_pow, n, tw[layer]);
+        if (log_h - 1 - layer >= mid) reverse_slice(tw[layer], n);
+        shift_pow = fmul(shift_pow, shift_pow);
+        root_pow = fmul(root_pow, root_pow);
+    }
+    return tw;
+}
+
+static void free_twiddles(fr_t** tw, uint32_t log_h) {
+    for (uint32_t i = 0; i < log_h; i++) free(tw[i]);
+    free(tw);
+}
+
+/* coset_dft (:232-250), in place on a height-h block that holds bit-reversed coefficients */
+static void coset_dft_block(fr_t* m, uint64_t h, uint64_t w, fr_t shift) {
+    uint32_t log_h = log2_strict(h);
+    if (log_h == 0) return;
+    uint32_t mid = (log_h + 1) / 2;
+    fr_t** tw = coset_twiddles(log_h, shift);
+    first_half(m, h, w, mid, NULL, tw);
+    or_reverse_matrix_index_bits(m, h, w);
+    second_half(m, h, w, mid, NULL, tw, NULL);
+    free_twiddles(tw, log_h);
+}
+
+void or_r2dp_dft_batch(fr_t* m, uint64_t h, uint64_t w) {
+    /* dft_batch (:148-166): result storage is bit-reversed */
+    uint32_t log_h = log2_strict(h);
+    uint32_t mid = (log_h + 1) / 2;
+    uint64_t half_h = h >> 1;
+    fr_t* tw = (fr_t*)malloc(sizeof(fr_t) * (half_h ? half_h : 1));
+    powers(or_two_adic_generator(log_h), fone(), half_h, tw);
+    fr_t* twr = (fr_t*)malloc(sizeof(fr_t) * (half_h ? half_h : 1));
+    memcpy(twr, tw, sizeof(fr_t) * half_h);
+    reverse_slice(twr, half_h);
+    or_reverse_matrix_index_bits(m, h, w);
+    first_half(m, h, w, mid, tw, NULL);
+    or_reverse_matrix_index_bits(m, h, w);
+    second_half(m, h, w, mid, twr, NULL, NULL);
+    free(tw);
+    free(twr);
+}
+
+void or_r2dp_coset_lde_batch(const fr_t* in, fr_t* out, uint64_t h, uint64_t w, uint32_t added_bits,
+                             fr_t shift) {
+    /* coset_lde_batch (:169-228): `out` has (h << added_bits) rows; result storage bit-reversed */
+    uint32_t log_h = log2_strict(h);
+    uint32_t mid = (log_h + 1) / 2;
+    uint64_t half_h = h >> 1;
+    memcpy(out, in, sizeof(fr_t) * h * w);
+    fr_t* tw = (fr_t*)malloc(sizeof(fr_t) * (half_h ? half_h : 1));
+    powers(or_fr_inverse(or_two_adic_generator(log_h)), fone(), half_h, tw);
+    fr_t* twr = (fr_t*)malloc(sizeof(fr_t) * (half_h ? half_h : 1));
+    memcpy(twr, tw, sizeof(fr_t) * half_h);
+    reverse_slice(twr, half_h);
+    or_reverse_matrix_index_bits(out, h, w);
+    first_half(out, h, w, mid, tw, NULL);
+    or_reverse_matrix_index_bits(out, h, w);
+    fr_t scale = or_fr_inverse(or_fr_from_u64(h));
+    second_half(out, h, w, mid, twr, NULL, &scale);
+    free(tw);
+    free(twr);
+    /* coefficients are now bit-reversed in block 0 */
+    fr_t g_big = or_two_adic_generator(log_h + added_bits);
+    for (uint64_t coset_idx = 1; coset_idx < (1ull << added_bits); coset_idx++) {
+        fr_t total_shift = fmul(or_fr_pow(g_big, coset_idx), shift);
+        uint64_t dest = rev_bits(coset_idx, added_bits);
+        fr_t* dst = out + dest * h * w;
+        /* coset_dft_oop (:254-292) == copy + in-place coset_dft (same arithmetic) */
+        memcpy(dst, out, sizeof(fr_t) * h * w);
+        coset_dft_block(dst, h, w, total_shift);
+    }
+    coset_dft_block(out, h, w, shift);
+}
+
+/* ---- conversions for the Python side ------------------------------------------------------- */
+void or_fr_mul_batch(const fr_t* a, const fr_t* b, fr_t* r, uint64_t n) {
+#pragma omp parallel for schedule(static)
+    for (uint64_t i = 0; i < n; i++) or_fr_mul(&a[i], &b[i], &r[i]);
+}
+
+int or_num_threads(void) {
+#ifdef _OPENMP
+    extern int omp_get_max_threads(void);
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+/* ---- KzgPcs::get_evaluations_on_domain (kzg/src/pcs.rs:267-287) ----------------------------- */
+fr_t or_eval_poly_col(const fr_t* coeffs, uint64_t h, uint64_t w, uint64_t col, fr_t point) {
+    /* eval_poly (kzg/src/util.rs:63-68): Horner from the top coefficient */
+    fr_t acc = {{0, 0, 0, 0}};
+    for (uint64_t i = h; i-- > 0;) acc = fadd(fmul(acc, point), coeffs[i * w + col]);
+    return acc;
+}
+
+void or_kzg_evaluations_on_domain(const fr_t* coeffs, uint64_t h, uint64_t w, uint32_t log_q,
+                                  fr_t shift, fr_t* out) {
+    /* every column polynomial at every point shift * w_Q^i of the domain, row-major Q x w */
+    uint64_t q = 1ull << log_q;
+    fr_t g = or_two_adic_generator(log_q);
+#pragma omp parallel for schedule(dynamic, 16)
+    for (uint64_t i = 0; i < q; i++) {
+        fr_t pt = fmul(shift, or_fr_pow(g, i));
+        for (uint64_t c = 0; c < w; c++) out[i * w + c] = or_eval_poly_col(coeffs, h, w, c, pt);
+    }
+}

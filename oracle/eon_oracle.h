@@ -1,0 +1,41 @@
+/* eon_oracle.h -- CPU restatement of the reference hot path (TEST INFRASTRUCTURE ONLY; see
+ * eon_oracle.c).  fr_t is p3_bn254::Fr's layout: [u64;4] LE Montgomery, canonical. */
+#ifndef EON_ORACLE_H
+#define EON_ORACLE_H
+#include <stdint.h>
+
+typedef struct {
+    uint64_t v[4];
+} fr_t;
+
+void or_fr_mul(const fr_t* a, const fr_t* b, fr_t* r);
+void or_fr_add(const fr_t* a, const fr_t* b, fr_t* r);
+void or_fr_sub(const fr_t* a, const fr_t* b, fr_t* r);
+fr_t or_fr_from_u64(uint64_t x);
+fr_t or_fr_pow(fr_t b, uint64_t e);
+fr_t or_fr_inverse(fr_t a);
+fr_t or_two_adic_generator(uint32_t bits);
+void or_fr_mul_batch(const fr_t* a, const fr_t* b, fr_t* r, uint64_t n);
+void or_reverse_matrix_index_bits(fr_t* m, uint64_t h, uint64_t w);
+
+/* Radix2Dit + trait defaults: natural order, in place on m (h x w) */
+void or_radix2dit_dft_batch(fr_t* m, uint64_t h, uint64_t w);
+void or_idft_batch(fr_t* m, uint64_t h, uint64_t w);
+void or_coset_dft_batch(fr_t* m, uint64_t h, uint64_t w, fr_t shift);
+void or_coset_idft_batch(fr_t* m, uint64_t h, uint64_t w, fr_t shift);
+void or_coset_lde_batch(const fr_t* in, fr_t* out, uint64_t h, uint64_t w, uint32_t added_bits,
+                        fr_t shift);
+
+/* Radix2DitParallel: bit-reversed storage */
+void or_r2dp_dft_batch(fr_t* m, uint64_t h, uint64_t w);
+void or_r2dp_coset_lde_batch(const fr_t* in, fr_t* out, uint64_t h, uint64_t w, uint32_t added_bits,
+                             fr_t shift);
+
+int or_num_threads(void);
+
+/* KzgPcs::get_evaluations_on_domain's Horner evaluation (kzg/src/pcs.rs:267-287) */
+fr_t or_eval_poly_col(const fr_t* coeffs, uint64_t h, uint64_t w, uint64_t col, fr_t point);
+void or_kzg_evaluations_on_domain(const fr_t* coeffs, uint64_t h, uint64_t w, uint32_t log_q,
+                                  fr_t shift, fr_t* out);
+#endif
+

@@ -13,6 +13,7 @@
 //        bitrev:  inverse DIT (natural coefficients) then forward DIF on the zero-padded
 //                 vector, which lands directly in Radix2DitParallel's bit-reversed storage.
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 
 #include "context.h"
@@ -140,8 +141,8 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         }
         f.load_scale = table;
         a.max_stages_per_pass = f.max_stages_per_pass = ctx->ntt_max_stages;
-        EON_HIP(run_network(a, st));
-        EON_HIP(run_network(f, st));
+        EON_HIP(run_network(a, st, &ctx->prof));
+        EON_HIP(run_network(f, st, &ctx->prof));
         return Status::ok();
     }
 
@@ -178,7 +179,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         s.store_scale = table;
     }
     s.max_stages_per_pass = ctx->ntt_max_stages;
-    EON_HIP(run_network(s, st));
+    EON_HIP(run_network(s, st, &ctx->prof));
     return Status::ok();
 }
 
@@ -228,7 +229,8 @@ int eon_ctx_create(int device_ordinal, eon_ctx** out) {
     if (hipSetDevice(device_ordinal) != hipSuccess) return EON_E_DEVICE;
     eon_ctx* c = new eon_ctx();
     c->device = device_ordinal;
-    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    // blocking stream: host-API work stays ordered with null-stream work of other libraries
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault) != hipSuccess) {
         delete c;
         return EON_E_DEVICE;
     }
@@ -245,6 +247,11 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     ctx->tw_fwd.release();
     ctx->tw_inv.release();
     for (auto& kv : ctx->tables) kv.second.release();
+    for (auto& r : ctx->prof.recs) {
+        (void)hipEventDestroy(r.start);
+        (void)hipEventDestroy(r.stop);
+    }
+    for (auto e : ctx->prof.pool) (void)hipEventDestroy(e);
     ctx->scratch.release();
     ctx->stage_in.release();
     ctx->stage_out.release();
@@ -257,7 +264,8 @@ const char* eon_last_error(const eon_ctx* ctx) { return ctx ? ctx->last_error.c_
 int eon_ctx_set_stream(eon_ctx* ctx, void* hip_stream) {
     if (!ctx) return EON_E_ARG;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->stream = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+    // used verbatim: NULL is the HIP null (legacy default) stream, which is torch's default
+    ctx->stream = reinterpret_cast<hipStream_t>(hip_stream);
     return EON_OK;
 }
 
@@ -270,6 +278,53 @@ int eon_ctx_synchronize(eon_ctx* ctx) {
         ctx->last_error = hipGetErrorString(e);
         return EON_E_DEVICE;
     }
+    return EON_OK;
+}
+
+int eon_ctx_profile(eon_ctx* ctx, int enable) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& r : ctx->prof.recs) {
+        ctx->prof.pool.push_back(r.start);
+        ctx->prof.pool.push_back(r.stop);
+    }
+    ctx->prof.recs.clear();
+    ctx->prof.enabled = enable != 0;
+    return EON_OK;
+}
+
+int eon_ctx_profile_report(eon_ctx* ctx, char* buf, uint64_t len) {
+    // JSON: {"kernel name": {"launches": n, "total_ms": t, "alg_bytes": b}, ...}
+    if (!ctx || !buf || len == 0) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    (void)hipSetDevice(ctx->device);
+    struct Agg {
+        uint64_t n = 0, bytes = 0;
+        double ms = 0;
+    };
+    std::map<std::string, Agg> agg;
+    for (auto& r : ctx->prof.recs) {
+        if (hipEventSynchronize(r.stop) != hipSuccess) continue;
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, r.start, r.stop) != hipSuccess) continue;
+        Agg& a = agg[r.kernel];
+        a.n++;
+        a.ms += ms;
+        a.bytes += r.alg_bytes;
+    }
+    std::string out = "{";
+    char tmp[256];
+    for (auto& kv : agg) {
+        snprintf(tmp, sizeof tmp, "%s\"%s\": {\"launches\": %llu, \"total_ms\": %.6f, \"alg_bytes\": %llu}",
+                 out.size() > 1 ? ", " : "", kv.first.c_str(), (unsigned long long)kv.second.n,
+                 kv.second.ms, (unsigned long long)kv.second.bytes);
+        out += tmp;
+    }
+    out += "}";
+    if (out.size() + 1 > len) return EON_E_ARG;
+    memcpy(buf, out.c_str(), out.size() + 1);
     return EON_OK;
 }
 

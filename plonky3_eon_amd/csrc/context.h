@@ -7,6 +7,7 @@
 
 #include "../../include/eon.h"
 #include "field.h"
+#include "ntt.h"
 
 namespace eon {
 
@@ -77,6 +78,9 @@ struct eon_ctx {
 
     // EON_NTT_MAX_STAGES: cap on radix-2 stages per NTT pass (0 = tile limit); read at creation
     uint32_t ntt_max_stages = 0;
+
+    // per-launch HIP-event timing (eon_ctx_profile_*)
+    eon::Profiler prof;
 
     // scratch: NTT intermediates, host-API staging
     eon::DevBuf scratch, stage_in, stage_out;

@@ -1,5 +1,7 @@
 // Internal NTT launch API (not part of the C ABI; see include/eon.h).
 #pragma once
+#include <vector>
+
 #include "field.h"
 
 namespace eon {
@@ -35,7 +37,39 @@ struct NetworkSpec {
     uint32_t max_stages_per_pass = 0;  // 0 = tile limit; tests force multi-pass plans with it
 };
 
-hipError_t run_network(const NetworkSpec& s, hipStream_t st);
+// Optional per-launch timing (eon_ctx_profile_*): a launch is bracketed by two events.
+struct LaunchRecord {
+    const char* kernel;
+    uint64_t alg_bytes;  // algorithmic bytes of this launch (each element read + written once)
+    hipEvent_t start, stop;
+};
+struct Profiler {
+    bool enabled = false;
+    std::vector<LaunchRecord> recs;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    void begin(const char* kernel, uint64_t bytes, hipStream_t st) {
+        if (!enabled) return;
+        LaunchRecord r{kernel, bytes, get(), get()};
+        (void)hipEventRecord(r.start, st);
+        recs.push_back(r);
+    }
+    void end(hipStream_t st) {
+        if (!enabled || recs.empty()) return;
+        (void)hipEventRecord(recs.back().stop, st);
+    }
+};
+
+hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof = nullptr);
 hipError_t launch_powers(Fr* out, uint64_t n, const Fr& base, const Fr& scale, uint32_t rev_log,
                          hipStream_t st);
 hipError_t launch_twiddles(Fr* tw, uint32_t L, const Fr& root_L, hipStream_t st);

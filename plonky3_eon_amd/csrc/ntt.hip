@@ -248,7 +248,7 @@ static uint32_t pick_log_cb(uint64_t width) {
     return 0;
 }
 
-hipError_t run_network(const NetworkSpec& s, hipStream_t st) {
+hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
     const uint32_t log_cb = pick_log_cb(s.width);
     uint32_t kmax = 10 - log_cb;  // 1024 elements per tile (32 KiB of LDS)
     if (s.max_stages_per_pass && s.max_stages_per_pass < kmax) kmax = s.max_stages_per_pass;
@@ -286,7 +286,13 @@ hipError_t run_network(const NetworkSpec& s, hipStream_t st) {
         }
         a.store_scale = last ? s.store_scale : nullptr;
         const uint64_t groups = (1ull << s.log_m) >> a.k;
+        static const char* names[8] = {"k_ntt_pass<false, 0>", "k_ntt_pass<false, 1>",
+                                       "k_ntt_pass<false, 2>", "k_ntt_pass<false, 3>",
+                                       "k_ntt_pass<true, 0>",  "k_ntt_pass<true, 1>",
+                                       "k_ntt_pass<true, 2>",  "k_ntt_pass<true, 3>"};
+        if (prof) prof->begin(names[(s.dif ? 4 : 0) + log_cb], (64ull << s.log_m) * s.width, st);
         hipError_t e = launch_pass(s.dif, log_cb, a, groups, col_tiles, st);
+        if (prof) prof->end(st);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

@@ -53,6 +53,17 @@ class Context:
     def synchronize(self):
         self.check(self.lib.eon_ctx_synchronize(self._h))
 
+    def profile(self, enable: bool = True):
+        """Start (clearing) or stop per-launch HIP-event timing (eon_ctx_profile)."""
+        self.check(self.lib.eon_ctx_profile(self._h, 1 if enable else 0))
+
+    def profile_report(self) -> dict:
+        import json
+
+        buf = ctypes.create_string_buffer(1 << 16)
+        self.check(self.lib.eon_ctx_profile_report(self._h, buf, len(buf)))
+        return json.loads(buf.value.decode())
+
     def close(self):
         if getattr(self, "_h", None):
             self.lib.eon_ctx_destroy(self._h)

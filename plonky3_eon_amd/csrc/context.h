@@ -78,6 +78,9 @@ struct eon_ctx {
 
     // EON_NTT_MAX_STAGES: cap on radix-2 stages per NTT pass (0 = tile limit); read at creation
     uint32_t ntt_max_stages = 0;
+    // EON_NTT_TPB / EON_NTT_LOG_CB: tuning knobs (threads per block cap, columns per tile)
+    uint32_t ntt_tpb = 0;
+    int ntt_log_cb = -1;
 
     // per-launch HIP-event timing (eon_ctx_profile_*)
     eon::Profiler prof;

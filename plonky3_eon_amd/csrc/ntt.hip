@@ -65,7 +65,7 @@ __device__ __forceinline__ void gstore(Fr* p, const Fr& x) {
 }
 
 template <bool DIF, int LOG_CB>
-__global__ void __launch_bounds__(256) k_ntt_pass(PassArgs a) {
+__global__ void __launch_bounds__(512) k_ntt_pass(PassArgs a) {
     constexpr uint32_t CB = 1u << LOG_CB;
     extern __shared__ __attribute__((aligned(16))) uint4 lds[];
     const uint32_t k = a.k;
@@ -196,11 +196,13 @@ __global__ void k_tw_fill_lower(Fr* tw, uint32_t L) {
 }
 
 static hipError_t launch_pass(bool dif, uint32_t log_cb, const PassArgs& a, uint64_t groups,
-                              uint64_t col_tiles, hipStream_t st) {
+                              uint64_t col_tiles, uint32_t max_threads, hipStream_t st) {
     const uint32_t ne = (1u << log_cb) << a.k;
-    uint32_t threads = ne / 8;
+    // one butterfly per thread per stage: 512 threads per 1024-element (36 KiB) tile keeps the
+    // CU at 32 waves with 4 LDS-bound tiles resident
+    uint32_t threads = ne / 2;
+    if (threads > max_threads) threads = max_threads;
     if (threads < 64) threads = 64;
-    if (threads > 256) threads = 256;
     const size_t lds = (size_t)ne * 32 + ((size_t)1 << a.k) * 32;
     dim3 grid((unsigned)groups, (unsigned)col_tiles);
 #define EON_LAUNCH(D, C) \
@@ -249,7 +251,7 @@ static uint32_t pick_log_cb(uint64_t width) {
 }
 
 hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
-    const uint32_t log_cb = pick_log_cb(s.width);
+    const uint32_t log_cb = s.log_cb_override >= 0 ? (uint32_t)s.log_cb_override : pick_log_cb(s.width);
     uint32_t kmax = 10 - log_cb;  // 1024 elements per tile (32 KiB of LDS)
     if (s.max_stages_per_pass && s.max_stages_per_pass < kmax) kmax = s.max_stages_per_pass;
     const uint32_t lo_stage = s.first_stage;
@@ -291,7 +293,7 @@ hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
                                        "k_ntt_pass<true, 0>",  "k_ntt_pass<true, 1>",
                                        "k_ntt_pass<true, 2>",  "k_ntt_pass<true, 3>"};
         if (prof) prof->begin(names[(s.dif ? 4 : 0) + log_cb], (64ull << s.log_m) * s.width, st);
-        hipError_t e = launch_pass(s.dif, log_cb, a, groups, col_tiles, st);
+        hipError_t e = launch_pass(s.dif, log_cb, a, groups, col_tiles, s.max_threads ? s.max_threads : 512, st);
         if (prof) prof->end(st);
         if (e != hipSuccess) return e;
     }

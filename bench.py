@@ -78,15 +78,128 @@ def cpu_baseline_lde(log_n: int, width: int, b: int, sample_cols: int) -> dict:
     }
 
 
+def cpu_baseline_msm(bases_host: np.ndarray, scalars_host: np.ndarray) -> dict:
+    from oracle import coracle
+
+    coracle.build()
+    n = bases_host.shape[0]
+    t0 = time.perf_counter()
+    coracle.g1_msm(bases_host, scalars_host)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(dt * 1e3, 1),
+        "unit": "ms",
+        "cores": coracle.num_threads(),
+        "kind": "port",
+        "sample": f"full input: {n} points (C Pippenger restatement, unsigned windows, OpenMP over "
+        f"windows; halo2curves msm_best is not in the reference tree)",
+    }
+
+
+class LdeWorkload:
+    """configs[1]: coset_lde_batch 2^log_n x width, added_bits, shift 5."""
+
+    def __init__(self, args, ctx, dev, rank):
+        import torch
+
+        from plonky3_eon_amd import _lib as L
+        from plonky3_eon_amd.field import fr_to_abi
+
+        self.args, self.ctx = args, ctx
+        self.n, self.w, self.b = 1 << args.log_n, args.width, args.added_bits
+        self.order = L.EON_ORDER_NATURAL if args.order == "natural" else L.EON_ORDER_BITREV
+        self.x = torch.from_numpy(synthetic_fr(self.n, self.w, 1234 + rank).view(np.int64)).to(dev)
+        self.out = torch.empty((self.n << self.b, self.w, 4), dtype=torch.int64, device=dev)
+        self.shift = fr_to_abi(5)
+
+    def step(self):
+        import ctypes
+
+        c = self.ctx
+        c.check(c.lib.eon_coset_lde_batch_dev(c.handle, ctypes.c_void_p(self.x.data_ptr()),
+                                              ctypes.c_void_p(self.out.data_ptr()), self.n, self.w,
+                                              self.b, ctypes.byref(self.shift), self.order))
+
+    def describe(self, world):
+        a = self.args
+        return (f"configs[1]: batched LDE NTT, coset_lde_batch 2^{a.log_n} rows x {self.w} cols over "
+                f"BN254 Fr, added_bits={self.b}, shift=5, {a.order} output (per GPU; column-sharded)",
+                self.w * world, self.n, f"column-shard x{world}")
+
+    def throughput(self, world, ms):
+        n, w, b = self.n, self.w, self.b
+        lde_bytes = n * w * 32 + (n << b) * w * 32  # BASELINE.md section 3, C2
+        mulmods = lde_mulmods(self.args.log_n, w, b)
+        return {
+            "lde_elements_per_s": round(world * n * w / (ms * 1e-3), 1),
+            "alg_GBps_whole_lde": round(world * lde_bytes / (ms * 1e-3) / 1e9, 2),
+            "mulmod_per_s": round(world * mulmods / (ms * 1e-3), 1),
+        }, mulmods
+
+    def cpu_baseline(self):
+        a = self.args
+        return cpu_baseline_lde(a.log_n, self.w, self.b, min(a.cpu_sample_cols, self.w))
+
+
+class MsmWorkload:
+    """configs[2]: KZG commit MSM, 2^log_msm SRS points (alpha = 12345) x uniform Fr scalars."""
+
+    def __init__(self, args, ctx, dev, rank):
+        import ctypes
+
+        import torch
+
+        from plonky3_eon_amd import _lib as L
+        from plonky3_eon_amd.field import fr_to_abi
+
+        self.args, self.ctx = args, ctx
+        self.n = 1 << args.log_msm
+        self.bases_dev = torch.empty((self.n, 8), dtype=torch.int64, device=dev)
+        alpha = fr_to_abi(12345)
+        ctx.check(ctx.lib.eon_g1_srs_powers_dev(ctx.handle, ctypes.byref(alpha), self.n,
+                                                ctypes.c_void_p(self.bases_dev.data_ptr())))
+        h = ctypes.c_void_p()
+        ctx.check(ctx.lib.eon_msm_bases_create_dev(ctx.handle, ctypes.c_void_p(self.bases_dev.data_ptr()),
+                                                   self.n, L.EON_MSM_PRECOMPUTE, ctypes.byref(h)))
+        self.bases = h
+        self.scalars_host = synthetic_fr(self.n, 1, 3 + rank).reshape(self.n, 4)
+        self.scalars = torch.from_numpy(self.scalars_host.view(np.int64)).to(dev)
+        self.out = np.zeros(8, dtype=np.uint64)
+
+    def step(self):
+        import ctypes
+
+        c = self.ctx
+        c.check(c.lib.eon_msm_g1_dev(c.handle, self.bases, ctypes.c_void_p(self.scalars.data_ptr()),
+                                     self.n, self.out.ctypes.data_as(ctypes.c_void_p)))
+
+    def describe(self, world):
+        return (f"configs[2]: KZG commit MSM, 2^{self.args.log_msm} BN254 G1 SRS points (alpha=12345, "
+                f"fixed-base window table built untimed) x uniform Fr scalars (per GPU)",
+                world, self.n, f"msm-shard x{world}")
+
+    def throughput(self, world, ms):
+        # Pippenger mixed additions: n * ceil(255 / c) nonzero-digit pairs (c chosen by the library)
+        return {
+            "points_per_s": round(world * self.n / (ms * 1e-3), 1),
+            "alg_GBps": round(world * self.n * 96 / (ms * 1e-3) / 1e9, 3),  # BASELINE.md C3
+        }, None
+
+    def cpu_baseline(self):
+        return cpu_baseline_msm(self.bases_dev.cpu().numpy().view(np.uint64), self.scalars_host)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=["lde", "msm"], default="lde")
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--width", type=int, default=64)
     ap.add_argument("--added-bits", type=int, default=1)
     ap.add_argument("--order", choices=["natural", "bitrev"], default="natural")
+    ap.add_argument("--log-msm", type=int, default=20)
     ap.add_argument("--cpu-sample-cols", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -105,28 +218,13 @@ def main() -> int:
         dist.init_process_group("nccl", device_id=dev)
 
     from plonky3_eon_amd import Context
-    from plonky3_eon_amd import _lib as L
-    from plonky3_eon_amd.field import fr_to_abi
-    import ctypes
 
     ctx = Context(local_rank)
-    stream = torch.cuda.current_stream(dev)
-    ctx.set_stream(stream.cuda_stream)
-
-    n, w, b = 1 << args.log_n, args.width, args.added_bits
-    order = L.EON_ORDER_NATURAL if args.order == "natural" else L.EON_ORDER_BITREV
-    x_host = synthetic_fr(n, w, 1234 + rank)
-    x = torch.from_numpy(x_host.view(np.int64)).to(dev)
-    out = torch.empty((n << b, w, 4), dtype=torch.int64, device=dev)
-    shift = fr_to_abi(5)
-
-    def step():
-        ctx.check(ctx.lib.eon_coset_lde_batch_dev(ctx.handle, ctypes.c_void_p(x.data_ptr()),
-                                                  ctypes.c_void_p(out.data_ptr()), n, w, b,
-                                                  ctypes.byref(shift), order))
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    wl = (LdeWorkload if args.workload == "lde" else MsmWorkload)(args, ctx, dev, rank)
 
     for _ in range(args.warmup):
-        step()
+        wl.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -134,7 +232,7 @@ def main() -> int:
     ctx.profile(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        wl.step()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -148,15 +246,33 @@ def main() -> int:
         elapsed = float(t.item())
 
     ms_per_step = elapsed * 1e3 / args.steps
-    # dominant kernel: largest total time
     kname, kst = max(prof.items(), key=lambda kv: kv[1]["total_ms"])
     avg_ms = kst["total_ms"] / kst["launches"]
     bytes_per_launch = kst["alg_bytes"] / kst["launches"]
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    lde_bytes = n * w * 32 + (n << b) * w * 32
-    mulmods = lde_mulmods(args.log_n, w, b)
     gpu_total_ms = sum(v["total_ms"] for v in prof.values()) / args.steps
+    workload, gbatch, seq, par = wl.describe(world)
+    thr, mulmods = wl.throughput(world, ms_per_step)
 
+    roof = {
+        "bound": "hbm",
+        "kernel": kname,
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 4),
+        "traffic": None,
+        "avg_launch_ms": round(avg_ms, 4),
+        "alg_bytes_per_launch": int(bytes_per_launch),
+        "kernels": prof,
+    }
+    if mulmods is not None:
+        roof["valu"] = {
+            "binding": True,
+            "achieved_mulmod_per_s": round(mulmods / (gpu_total_ms * 1e-3), 1),
+            "peak_mulmod_per_s": MULMOD_PEAK_PER_S,
+            "frac": round(mulmods / (gpu_total_ms * 1e-3) / MULMOD_PEAK_PER_S, 4),
+        }
     result = {
         "metric": METRIC,
         "value": round(ms_per_step, 3),
@@ -170,49 +286,22 @@ def main() -> int:
         "vs_baseline": None,
         "dtype": "bn254-fr (u32x8 Montgomery)",
         "data": "synthetic uniform Fr, resident in HBM",
-        "config": {
-            "workload": f"configs[1]: batched LDE NTT, coset_lde_batch 2^{args.log_n} rows x {w} cols over "
-            f"BN254 Fr, added_bits={b}, shift=5, {args.order} output (per GPU; column-sharded)",
-            "global_batch": w * world,
-            "seq_len": n,
-            "parallelism": f"column-shard x{world}",
-        },
-        "throughput": {
-            "lde_elements_per_s": round(world * n * w / (ms_per_step * 1e-3), 1),
-            "alg_GBps_whole_lde": round(world * lde_bytes / (ms_per_step * 1e-3) / 1e9, 2),
-            "mulmod_per_s": round(world * mulmods / (ms_per_step * 1e-3), 1),
-        },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": kname,
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": None,
-            "avg_launch_ms": round(avg_ms, 4),
-            "alg_bytes_per_launch": int(bytes_per_launch),
-            "valu": {
-                "binding": True,
-                "achieved_mulmod_per_s": round(mulmods / (gpu_total_ms * 1e-3), 1),
-                "peak_mulmod_per_s": MULMOD_PEAK_PER_S,
-                "frac": round(mulmods / (gpu_total_ms * 1e-3) / MULMOD_PEAK_PER_S, 4),
-            },
-            "kernels": prof,
-        },
+        "config": {"workload": workload, "global_batch": gbatch, "seq_len": seq, "parallelism": par},
+        "throughput": thr,
+        "roofline": roof,
         "cpu_baseline": None,
     }
-    traffic_file = ROOT / "profiles" / "traffic_lde.json"
+    traffic_file = ROOT / "profiles" / f"traffic_{args.workload}.json"
     if traffic_file.exists():
         try:
             tf = json.loads(traffic_file.read_text())
-            if tf.get("kernel") == kname and tf.get("workload") == result["config"]["workload"]:
-                result["roofline"]["traffic"] = tf.get("bytes_per_launch")
+            if tf.get("kernel") == kname and tf.get("workload") == workload:
+                roof["traffic"] = tf.get("bytes_per_launch")
         except Exception:
             pass
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline_lde(args.log_n, w, b, min(args.cpu_sample_cols, w))
+        result["cpu_baseline"] = wl.cpu_baseline()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

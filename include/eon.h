@@ -112,6 +112,39 @@ int eon_coset_lde_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_
                             uint32_t width, uint32_t added_bits, const eon_fr* shift,
                             int out_order);
 
+/* ---- BN254 G1 multi-scalar multiplication -------------------------------------------------
+ * Value of G1::multi_exp (bn254/src/curve.rs:158-179, halo2curves msm_best): sum_i s_i * P_i,
+ * returned in affine form ((0,0) = identity; empty input -> identity).  Bases are uploaded
+ * once into an eon_msm_bases handle and reused, as the KZG SRS g1_powers is
+ * (kzg/src/params.rs:57-139, commit_column kzg/src/util.rs:37-40). */
+enum {
+    EON_MSM_PRECOMPUTE = 1 /* fixed-base mode: store 2^(c*w) * P_i for every window (SRS bases) */
+};
+/* `bases`: host array of n affine points with canonical coordinates. */
+int eon_msm_bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32_t flags,
+                         eon_msm_bases** out);
+void eon_msm_bases_destroy(eon_msm_bases* bases);
+uint64_t eon_msm_bases_len(const eon_msm_bases* bases);
+/* MSM over the first n bases; `scalars` host (eon_msm_g1) or device (eon_msm_g1_dev) Fr array;
+ * `out` is a host pointer; both calls return when the result is in *out.  n > len(bases) is
+ * EON_E_SHAPE (the reference asserts equal lengths, curve.rs:159-162). */
+int eon_msm_g1(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* scalars, uint64_t n,
+               eon_g1_affine* out);
+int eon_msm_g1_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* scalars, uint64_t n,
+                   eon_g1_affine* out);
+/* As eon_msm_bases_create with `bases` a DEVICE pointer (coordinates are not re-validated). */
+int eon_msm_bases_create_dev(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32_t flags,
+                             eon_msm_bases** out);
+/* One-shot G1::multi_exp(points, scalars) on host arrays (bases uploaded for this call only). */
+int eon_g1_multi_exp(eon_ctx* ctx, const eon_g1_affine* points, const eon_fr* scalars, uint64_t n,
+                     eon_g1_affine* out);
+
+/* ---- test SRS (setup, not prove time) --------------------------------------------------------
+ * init_srs_unsafe's g1_powers (kzg/src/params.rs:123-139): out[i] = alpha^i * G1::generator(),
+ * affine, i < n.  `alpha` is a host pointer; `out` host (eon_g1_srs_powers) or device (_dev). */
+int eon_g1_srs_powers(eon_ctx* ctx, const eon_fr* alpha, uint64_t n, eon_g1_affine* out);
+int eon_g1_srs_powers_dev(eon_ctx* ctx, const eon_fr* alpha, uint64_t n, eon_g1_affine* out);
+
 #ifdef __cplusplus
 }
 #endif

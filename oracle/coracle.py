@@ -60,6 +60,12 @@ def lib():
         l.or_eval_poly_col.restype = fr_t
         l.or_kzg_evaluations_on_domain.argtypes = [P, U64, U64, U32, fr_t, P]
         l.or_kzg_evaluations_on_domain.restype = None
+        for k, a in {"or_g1_generator": [P], "or_g1_mul": [P, P, P], "or_g1_add": [P, P, P],
+                     "or_g1_srs": [U64, P, P], "or_g1_msm": [P, P, U64, P]}.items():
+            getattr(l, k).argtypes = a
+            getattr(l, k).restype = None
+        l.or_g1_on_curve.argtypes = [P]
+        l.or_g1_on_curve.restype = ctypes.c_int
         _lib = l
     return _lib
 
@@ -167,6 +173,50 @@ def fr_mul(a, b):
 def two_adic_generator(bits: int):
     r = lib().or_two_adic_generator(bits)
     return np.array([r.v[i] for i in range(4)], dtype=np.uint64)
+
+
+# --- G1 (points: numpy uint64 (..., 8) = x[4], y[4] Fq Montgomery; identity = zeros) ---------
+def g1_generator():
+    out = np.zeros(8, dtype=np.uint64)
+    lib().or_g1_generator(_ptr(out))
+    return out
+
+
+def g1_mul(p, scalar_limbs):
+    p = np.ascontiguousarray(p, dtype=np.uint64)
+    s = np.ascontiguousarray(scalar_limbs, dtype=np.uint64)
+    out = np.zeros(8, dtype=np.uint64)
+    lib().or_g1_mul(_ptr(p), _ptr(s), _ptr(out))
+    return out
+
+
+def g1_add(a, b):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    out = np.zeros(8, dtype=np.uint64)
+    lib().or_g1_add(_ptr(a), _ptr(b), _ptr(out))
+    return out
+
+
+def g1_on_curve(p) -> bool:
+    return bool(lib().or_g1_on_curve(_ptr(np.ascontiguousarray(p, dtype=np.uint64))))
+
+
+def g1_srs(n: int, alpha_limbs):
+    """init_srs_unsafe g1_powers (kzg/src/params.rs:123-139), affine."""
+    out = np.zeros((n, 8), dtype=np.uint64)
+    a = np.ascontiguousarray(alpha_limbs, dtype=np.uint64)
+    lib().or_g1_srs(n, _ptr(a), _ptr(out))
+    return out
+
+
+def g1_msm(points, scalars):
+    """Value of G1::multi_exp (Pippenger restatement)."""
+    p = np.ascontiguousarray(points, dtype=np.uint64)
+    s = np.ascontiguousarray(scalars, dtype=np.uint64)
+    out = np.zeros(8, dtype=np.uint64)
+    lib().or_g1_msm(_ptr(p), _ptr(s), p.shape[0], _ptr(out))
+    return out
 
 
 def num_threads() -> int:

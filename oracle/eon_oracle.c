@@ -479,3 +479,254 @@ void or_kzg_evaluations_on_domain(const fr_t* coeffs, uint64_t h, uint64_t w, ui
         for (uint64_t c = 0; c < w; c++) out[i * w + c] = or_eval_poly_col(coeffs, h, w, c, pt);
     }
 }
+
+/* ---- BN254 G1 over Fq (halo2curves 0.9 is not in the reference tree; the group law and the MSM
+ * value are restated directly: y^2 = x^3 + 3, generator (1, 2)) ----------------------------- */
+static const uint64_t FQ_P[4] = {0x3c208c16d87cfd47ull, 0x97816a916871ca8dull, 0xb85045b68181585dull,
+                                 0x30644e72e131a029ull};
+static const uint64_t FQ_MU = 0x782df87d1b799c77ull; /* q^-1 mod 2^64 */
+static const uint64_t FQ_R2[4] = {0xf32cfc5b538afa89ull, 0xb5e71911d44501fbull, 0x47ab1eff0a417ff6ull,
+                                  0x06d89f71cab8351full};
+static const uint64_t FQ_ONE[4] = {0xd35d438dc58f0d9dull, 0x0a78eb28f5c70b3dull, 0x666ea36f7879462cull,
+                                   0x0e0a77c19a07df2full};
+
+typedef struct {
+    uint64_t v[4];
+} fq_t;
+
+static inline void fq_reduce_step(uint64_t acc0, const uint64_t* acc, uint64_t* res) {
+    uint64_t t = acc0 * FQ_MU, u[4], sub[4];
+    (void)mul_small_and_acc(FQ_P, t, NULL, u);
+    if (wrapping_sub4(acc, u, sub))
+        wrapping_add4(sub, FQ_P, res);
+    else
+        memcpy(res, sub, 32);
+}
+
+static inline fq_t qmul(fq_t a, fq_t b) {
+    /* the same interleaved Montgomery product as Fr (bn254/src/helpers.rs:188-205), modulus q */
+    uint64_t acc[4], res[4];
+    uint64_t acc0 = mul_small_and_acc(a.v, b.v[0], NULL, acc);
+    fq_reduce_step(acc0, acc, res);
+    for (int i = 1; i < 4; i++) {
+        acc0 = mul_small_and_acc(a.v, b.v[i], res, acc);
+        fq_reduce_step(acc0, acc, res);
+    }
+    fq_t r;
+    memcpy(r.v, res, 32);
+    return r;
+}
+static inline fq_t qadd(fq_t a, fq_t b) {
+    fq_t r;
+    uint64_t s[4], c[4];
+    wrapping_add4(a.v, b.v, s);
+    if (wrapping_sub4(s, FQ_P, c))
+        memcpy(r.v, s, 32);
+    else
+        memcpy(r.v, c, 32);
+    return r;
+}
+static inline fq_t qsub(fq_t a, fq_t b) {
+    fq_t r;
+    if (wrapping_sub4(a.v, b.v, r.v)) wrapping_add4(r.v, FQ_P, r.v);
+    return r;
+}
+static inline int qzero(fq_t a) { return (a.v[0] | a.v[1] | a.v[2] | a.v[3]) == 0; }
+static inline int qeq(fq_t a, fq_t b) { return !memcmp(a.v, b.v, 32); }
+static inline fq_t qone(void) {
+    fq_t r;
+    memcpy(r.v, FQ_ONE, 32);
+    return r;
+}
+static inline fq_t qfrom_u64(uint64_t x) {
+    fq_t a = {{x, 0, 0, 0}}, r2;
+    memcpy(r2.v, FQ_R2, 32);
+    return qmul(r2, a);
+}
+static fq_t qinv(fq_t a) {
+    uint64_t e[4];
+    const uint64_t two[4] = {2, 0, 0, 0};
+    wrapping_sub4(FQ_P, two, e);
+    fq_t r = qone();
+    for (int w = 3; w >= 0; w--)
+        for (int bit = 63; bit >= 0; bit--) {
+            r = qmul(r, r);
+            if ((e[w] >> bit) & 1) r = qmul(r, a);
+        }
+    return r;
+}
+
+typedef struct {
+    fq_t X, Y, Z; /* Jacobian; Z = 0 is the point at infinity */
+} g1j_t;
+
+static g1j_t jinf(void) {
+    g1j_t r;
+    r.X = qone();
+    r.Y = qone();
+    memset(r.Z.v, 0, 32);
+    return r;
+}
+
+static g1j_t jfrom_affine(const g1_affine_t* a) {
+    g1j_t r;
+    if (qzero(*(const fq_t*)a->x) && qzero(*(const fq_t*)a->y)) return jinf();
+    memcpy(r.X.v, a->x, 32);
+    memcpy(r.Y.v, a->y, 32);
+    r.Z = qone();
+    return r;
+}
+
+static g1j_t jdbl(g1j_t p) {
+    /* dbl-2009-l */
+    if (qzero(p.Z)) return p;
+    fq_t A = qmul(p.X, p.X), B = qmul(p.Y, p.Y), C = qmul(B, B);
+    fq_t t = qadd(p.X, B);
+    fq_t D = qsub(qsub(qmul(t, t), A), C);
+    D = qadd(D, D);
+    fq_t E = qadd(qadd(A, A), A), F = qmul(E, E);
+    g1j_t r;
+    r.X = qsub(F, qadd(D, D));
+    fq_t C8 = qadd(C, C);
+    C8 = qadd(C8, C8);
+    C8 = qadd(C8, C8);
+    r.Y = qsub(qmul(E, qsub(D, r.X)), C8);
+    fq_t yz = qmul(p.Y, p.Z);
+    r.Z = qadd(yz, yz);
+    return r;
+}
+
+static g1j_t jadd(g1j_t p, g1j_t q) {
+    /* add-2007-bl with the doubling / inverse cases */
+    if (qzero(p.Z)) return q;
+    if (qzero(q.Z)) return p;
+    fq_t Z1Z1 = qmul(p.Z, p.Z), Z2Z2 = qmul(q.Z, q.Z);
+    fq_t U1 = qmul(p.X, Z2Z2), U2 = qmul(q.X, Z1Z1);
+    fq_t S1 = qmul(qmul(p.Y, q.Z), Z2Z2), S2 = qmul(qmul(q.Y, p.Z), Z1Z1);
+    fq_t H = qsub(U2, U1), rr = qsub(S2, S1);
+    if (qzero(H)) {
+        if (qzero(rr)) return jdbl(p);
+        return jinf();
+    }
+    fq_t H2 = qadd(H, H), I = qmul(H2, H2), J = qmul(H, I);
+    rr = qadd(rr, rr);
+    fq_t V = qmul(U1, I);
+    g1j_t r;
+    r.X = qsub(qsub(qmul(rr, rr), J), qadd(V, V));
+    fq_t s1j = qmul(S1, J);
+    r.Y = qsub(qmul(rr, qsub(V, r.X)), qadd(s1j, s1j));
+    fq_t zs = qadd(p.Z, q.Z);
+    r.Z = qmul(qsub(qsub(qmul(zs, zs), Z1Z1), Z2Z2), H);
+    return r;
+}
+
+static void jto_affine(g1j_t p, g1_affine_t* out) {
+    if (qzero(p.Z)) {
+        memset(out, 0, sizeof *out);
+        return;
+    }
+    fq_t zi = qinv(p.Z), zi2 = qmul(zi, zi), zi3 = qmul(zi2, zi);
+    fq_t x = qmul(p.X, zi2), y = qmul(p.Y, zi3);
+    memcpy(out->x, x.v, 32);
+    memcpy(out->y, y.v, 32);
+}
+
+static void fr_canonical(const fr_t* s, uint64_t* out) {
+    fr_t one_int = {{1, 0, 0, 0}}, r;
+    or_fr_mul(s, &one_int, &r); /* as_canonical_biguint (bn254/src/field.rs:456-461) */
+    memcpy(out, r.v, 32);
+}
+
+static g1j_t jmul(g1j_t p, const uint64_t* k) {
+    g1j_t acc = jinf();
+    for (int w = 3; w >= 0; w--)
+        for (int b = 63; b >= 0; b--) {
+            acc = jdbl(acc);
+            if ((k[w] >> b) & 1) acc = jadd(acc, p);
+        }
+    return acc;
+}
+
+void or_g1_generator(g1_affine_t* out) {
+    fq_t x = qfrom_u64(1), y = qfrom_u64(2);
+    memcpy(out->x, x.v, 32);
+    memcpy(out->y, y.v, 32);
+}
+
+void or_g1_mul(const g1_affine_t* p, const fr_t* scalar, g1_affine_t* out) {
+    uint64_t k[4];
+    fr_canonical(scalar, k);
+    jto_affine(jmul(jfrom_affine(p), k), out);
+}
+
+void or_g1_add(const g1_affine_t* a, const g1_affine_t* b, g1_affine_t* out) {
+    jto_affine(jadd(jfrom_affine(a), jfrom_affine(b)), out);
+}
+
+int or_g1_on_curve(const g1_affine_t* a) {
+    fq_t x, y;
+    memcpy(x.v, a->x, 32);
+    memcpy(y.v, a->y, 32);
+    if (qzero(x) && qzero(y)) return 1;
+    fq_t rhs = qadd(qmul(qmul(x, x), x), qfrom_u64(3));
+    return qeq(qmul(y, y), rhs);
+}
+
+void or_g1_srs(uint64_t n, const fr_t* alpha, g1_affine_t* out) {
+    /* init_srs_unsafe g1_powers (kzg/src/params.rs:123-139): g1_powers[i] = alpha^i * G */
+    g1_affine_t g;
+    or_g1_generator(&g);
+    g1j_t gj = jfrom_affine(&g);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (uint64_t i = 0; i < n; i++) {
+        fr_t s = or_fr_pow(*alpha, i);
+        uint64_t k[4];
+        fr_canonical(&s, k);
+        jto_affine(jmul(gj, k), &out[i]);
+    }
+}
+
+void or_g1_msm(const g1_affine_t* pts, const fr_t* scalars, uint64_t n, g1_affine_t* out) {
+    /* Pippenger (bucket method), unsigned c-bit windows, OpenMP over windows; the value of
+     * G1::multi_exp (bn254/src/curve.rs:158-179).  Empty input -> identity. */
+    if (n == 0) {
+        memset(out, 0, sizeof *out);
+        return;
+    }
+    uint32_t lg = 0;
+    while ((1ull << (lg + 1)) <= n) lg++;
+    uint32_t c = lg > 3 ? lg - 2 : 2;
+    if (c > 16) c = 16;
+    uint32_t nw = (254 + c - 1) / c;
+    uint64_t* ks = (uint64_t*)malloc(sizeof(uint64_t) * 4 * n);
+    for (uint64_t i = 0; i < n; i++) fr_canonical(&scalars[i], ks + 4 * i);
+    g1j_t* wsum = (g1j_t*)malloc(sizeof(g1j_t) * nw);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (uint32_t w = 0; w < nw; w++) {
+        uint64_t nb = (1ull << c) - 1;
+        g1j_t* buckets = (g1j_t*)malloc(sizeof(g1j_t) * nb);
+        for (uint64_t b = 0; b < nb; b++) buckets[b] = jinf();
+        for (uint64_t i = 0; i < n; i++) {
+            uint32_t pos = w * c, li = pos / 64, off = pos % 64;
+            unsigned __int128 v = ks[4 * i + li];
+            if (li + 1 < 4) v |= (unsigned __int128)ks[4 * i + li + 1] << 64;
+            uint64_t d = (uint64_t)(v >> off) & ((1ull << c) - 1);
+            if (d) buckets[d - 1] = jadd(buckets[d - 1], jfrom_affine(&pts[i]));
+        }
+        g1j_t run = jinf(), acc = jinf();
+        for (uint64_t b = nb; b-- > 0;) {
+            run = jadd(run, buckets[b]);
+            acc = jadd(acc, run);
+        }
+        wsum[w] = acc;
+        free(buckets);
+    }
+    g1j_t acc = wsum[nw - 1];
+    for (int w = (int)nw - 2; w >= 0; w--) {
+        for (uint32_t k = 0; k < c; k++) acc = jdbl(acc);
+        acc = jadd(acc, wsum[w]);
+    }
+    jto_affine(acc, out);
+    free(wsum);
+    free(ks);
+}

@@ -33,6 +33,18 @@ void or_r2dp_coset_lde_batch(const fr_t* in, fr_t* out, uint64_t h, uint64_t w, 
 
 int or_num_threads(void);
 
+/* BN254 G1: affine x, y as Fq Montgomery [u64;4] LE; identity = (0, 0) (the C-ABI layout) */
+typedef struct {
+    uint64_t x[4];
+    uint64_t y[4];
+} g1_affine_t;
+void or_g1_generator(g1_affine_t* out);
+void or_g1_mul(const g1_affine_t* p, const fr_t* scalar, g1_affine_t* out);
+void or_g1_add(const g1_affine_t* a, const g1_affine_t* b, g1_affine_t* out);
+int or_g1_on_curve(const g1_affine_t* a);
+void or_g1_srs(uint64_t n, const fr_t* alpha, g1_affine_t* out);
+void or_g1_msm(const g1_affine_t* pts, const fr_t* scalars, uint64_t n, g1_affine_t* out);
+
 /* KzgPcs::get_evaluations_on_domain's Horner evaluation (kzg/src/pcs.rs:267-287) */
 fr_t or_eval_poly_col(const fr_t* coeffs, uint64_t h, uint64_t w, uint64_t col, fr_t point);
 void or_kzg_evaluations_on_domain(const fr_t* coeffs, uint64_t h, uint64_t w, uint32_t log_q,

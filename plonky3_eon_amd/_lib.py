@@ -20,6 +20,7 @@ EON_E_OOM = -4
 EON_E_ARG = -5
 EON_ORDER_NATURAL = 0
 EON_ORDER_BITREV = 1
+EON_MSM_PRECOMPUTE = 1
 
 _ERRNAMES = {
     EON_E_SHAPE: "EON_E_SHAPE",
@@ -71,6 +72,15 @@ SIGNATURES = {
     "eon_coset_dft_batch_dev": (_INT, [_P, _P, _P, _U64, _U32, _P, _INT]),
     "eon_coset_idft_batch_dev": (_INT, [_P, _P, _P, _U64, _U32, _P]),
     "eon_coset_lde_batch_dev": (_INT, [_P, _P, _P, _U64, _U32, _U32, _P, _INT]),
+    "eon_msm_bases_create": (_INT, [_P, _P, _U64, _U32, ctypes.POINTER(_P)]),
+    "eon_msm_bases_destroy": (None, [_P]),
+    "eon_msm_bases_len": (_U64, [_P]),
+    "eon_msm_g1": (_INT, [_P, _P, _P, _U64, _P]),
+    "eon_msm_g1_dev": (_INT, [_P, _P, _P, _U64, _P]),
+    "eon_g1_multi_exp": (_INT, [_P, _P, _P, _U64, _P]),
+    "eon_msm_bases_create_dev": (_INT, [_P, _P, _U64, _U32, ctypes.POINTER(_P)]),
+    "eon_g1_srs_powers": (_INT, [_P, _P, _U64, _P]),
+    "eon_g1_srs_powers_dev": (_INT, [_P, _P, _U64, _P]),
 }
 
 _lib = None

@@ -258,6 +258,7 @@ void eon_ctx_destroy(eon_ctx* ctx) {
         (void)hipEventDestroy(r.stop);
     }
     for (auto e : ctx->prof.pool) (void)hipEventDestroy(e);
+    ctx->msm.release();
     ctx->scratch.release();
     ctx->stage_in.release();
     ctx->stage_out.release();

@@ -46,6 +46,17 @@ struct Status {
     bool bad() const { return code != EON_OK; }
 };
 
+// device workspace of one MSM pipeline run (msm.hip); grows on demand, reused across calls
+struct MsmWork {
+    DevBuf keys, vals, keys2, vals2, start, count, piece_off, off2, owner, piece_sums,
+        piece_sums2, bucket_sums, red_a, red_b, temp;
+    void release() {
+        for (DevBuf* b : {&keys, &vals, &keys2, &vals2, &start, &count, &piece_off, &off2, &owner,
+                          &piece_sums, &piece_sums2, &bucket_sums, &red_a, &red_b, &temp})
+            b->release();
+    }
+};
+
 #define EON_HIP(call)                                                                     \
     do {                                                                                  \
         hipError_t _e = (call);                                                           \
@@ -84,6 +95,9 @@ struct eon_ctx {
 
     // per-launch HIP-event timing (eon_ctx_profile_*)
     eon::Profiler prof;
+
+    // MSM pipeline workspace
+    eon::MsmWork msm;
 
     // scratch: NTT intermediates, host-API staging
     eon::DevBuf scratch, stage_in, stage_out;

@@ -1,0 +1,46 @@
+"""Turns two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) into per-launch HBM traffic of one
+kernel, corrected as MI355X_MICROARCH.md prescribes: counters are in KB (x1024), and on gfx950
+FETCH_SIZE reports half the bytes of a wide coalesced streaming read (x2).
+
+usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <kernel-substring> <workload> <out.json>
+"""
+
+import csv
+import glob
+import json
+import sys
+
+
+def per_dispatch(d, counter, kernel):
+    vals = {}
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") == counter and kernel in r.get("Kernel_Name", ""):
+                key = r.get("Dispatch_Id")
+                vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
+    return vals
+
+
+def main():
+    fdir, wdir, kernel, workload, out = sys.argv[1:6]
+    fetch = per_dispatch(fdir, "FETCH_SIZE", kernel)
+    write = per_dispatch(wdir, "WRITE_SIZE", kernel)
+    if not fetch or not write:
+        raise SystemExit(f"no counter rows for {kernel}: fetch={len(fetch)} write={len(write)}")
+    f_kb = sum(fetch.values()) / len(fetch)
+    w_kb = sum(write.values()) / len(write)
+    res = {
+        "kernel": kernel,
+        "workload": workload,
+        "dispatches": {"fetch": len(fetch), "write": len(write)},
+        "fetch_size_kb_per_launch": f_kb,
+        "write_size_kb_per_launch": w_kb,
+        "bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024),
+        "correction": "bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (gfx950 FETCH_SIZE halves wide reads)",
+    }
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -139,6 +139,45 @@ int eon_msm_bases_create_dev(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t 
 int eon_g1_multi_exp(eon_ctx* ctx, const eon_g1_affine* points, const eon_fr* scalars, uint64_t n,
                      eon_g1_affine* out);
 
+/* ---- eon-uni-stark quotient on the Poseidon2-AIR --------------------------------------------
+ * selectors_on_coset (commit/src/domain.rs:252-292): for the trace domain H (shift 1, 2^log_n) on
+ * the coset shift * K (2^log_q), writes 4 x 2^log_q Fr to device `out`: is_first_row,
+ * is_last_row, is_transition, inv_vanishing.  shift (host) must not be ONE (domain.rs:254). */
+int eon_selectors_on_coset_dev(eon_ctx* ctx, uint32_t log_n, uint32_t log_q, const eon_fr* shift,
+                               eon_fr* out);
+
+/* Poseidon2-AIR over BN254 Fr (poseidon2-air/src/air.rs): WIDTH 3, SBOX_DEGREE 5,
+ * SBOX_REGISTERS 1, external layer mds_light, internal layer [2,1,1;1,2,1;1,1,3]
+ * (bn254/src/poseidon2.rs:55-63); VECTOR_LEN permutations per row (vectorized.rs).  Constants
+ * are host arrays: beginning/ending half_full_rounds x 3, partial partial_rounds
+ * (RoundConstants, poseidon2-air/src/constants.rs:17-31). */
+typedef struct {
+    uint32_t half_full_rounds;
+    uint32_t partial_rounds;
+    const eon_fr* beginning;
+    const eon_fr* partial;
+    const eon_fr* ending;
+} eon_poseidon2_constants;
+typedef struct eon_p2air eon_p2air;
+/* Poseidon2Air::new / VectorizedPoseidon2Air::new (vector_len: power of two <= 32) */
+int eon_p2air_create(eon_ctx* ctx, const eon_poseidon2_constants* constants, uint32_t vector_len,
+                     eon_p2air** out);
+void eon_p2air_destroy(eon_p2air* air);
+/* trace width: (4 + 12 * half_full_rounds + 2 * partial_rounds) * vector_len (164 * vector_len) */
+uint32_t eon_p2air_width(const eon_p2air* air);
+/* generate_vectorized_trace_rows (poseidon2-air/src/generation.rs:14-72): inputs n_perms x 3 Fr
+ * (device), trace (n_perms / vector_len) x width (device); n_perms = vector_len * 2^k. */
+int eon_p2air_generate_trace_dev(eon_ctx* ctx, const eon_p2air* air, const eon_fr* inputs,
+                                 uint64_t n_perms, eon_fr* trace);
+/* quotient_values (eon-uni-stark/src/prover.rs:539-709) with the ProverConstraintFolder
+ * accumulator (folder.rs:81-85): `lde` is the trace on the quotient domain GENERATOR * K,
+ * |K| = 2^(log_n + log_qd), natural order (KzgPcs::get_evaluations_on_domain), device;
+ * out[i] = sum_k alpha^(K-1-k) C_k(row i) * inv_vanishing[i], device, 2^(log_n+log_qd) Fr.
+ * `alpha` is a host pointer. */
+int eon_p2air_quotient_values_dev(eon_ctx* ctx, const eon_p2air* air, const eon_fr* lde,
+                                  uint32_t log_n, uint32_t log_qd, const eon_fr* alpha,
+                                  eon_fr* out);
+
 /* ---- test SRS (setup, not prove time) --------------------------------------------------------
  * init_srs_unsafe's g1_powers (kzg/src/params.rs:123-139): out[i] = alpha^i * G1::generator(),
  * affine, i < n.  `alpha` is a host pointer; `out` host (eon_g1_srs_powers) or device (_dev). */

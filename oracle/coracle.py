@@ -64,6 +64,14 @@ def lib():
                      "or_g1_srs": [U64, P, P], "or_g1_msm": [P, P, U64, P]}.items():
             getattr(l, k).argtypes = a
             getattr(l, k).restype = None
+        for k, a in {"or_p2_generate_trace": [P, U64, U32, U32, U32, P, P, P, P],
+                     "or_selectors_on_coset": [U32, U32, fr_t, P, P, P, P],
+                     "or_p2_quotient_values": [P, U32, U32, U32, U32, U32, P, P, P, fr_t, P],
+                     "or_quotient_and_eval": [P, U64, U64, fr_t, P, P]}.items():
+            getattr(l, k).argtypes = a
+            getattr(l, k).restype = None
+        l.or_p2_num_cols.argtypes = [U32, U32]
+        l.or_p2_num_cols.restype = U32
         l.or_g1_on_curve.argtypes = [P]
         l.or_g1_on_curve.restype = ctypes.c_int
         _lib = l
@@ -217,6 +225,55 @@ def g1_msm(points, scalars):
     out = np.zeros(8, dtype=np.uint64)
     lib().or_g1_msm(_ptr(p), _ptr(s), p.shape[0], _ptr(out))
     return out
+
+
+# --- Poseidon2-AIR / quotient / open ----------------------------------------------------------
+class P2Constants:
+    """Round constants as Montgomery limb arrays: begin (hf, 3, 4), partial (pr, 4), end (hf, 3, 4)."""
+
+    def __init__(self, begin, partial, end):
+        self.begin = np.ascontiguousarray(begin, dtype=np.uint64).reshape(-1, 3, 4)
+        self.partial = np.ascontiguousarray(partial, dtype=np.uint64).reshape(-1, 4)
+        self.end = np.ascontiguousarray(end, dtype=np.uint64).reshape(-1, 3, 4)
+        self.hf = self.begin.shape[0]
+        self.pr = self.partial.shape[0]
+
+    @property
+    def num_cols(self):
+        return 1 + 3 + 12 * self.hf + 2 * self.pr
+
+
+def p2_generate_trace(inputs, vl: int, k: P2Constants):
+    x = np.ascontiguousarray(inputs, dtype=np.uint64).reshape(-1, 3, 4)
+    n = x.shape[0]
+    out = np.zeros((n // vl, k.num_cols * vl, 4), dtype=np.uint64)
+    lib().or_p2_generate_trace(_ptr(x), n, vl, k.hf, k.pr, _ptr(k.begin), _ptr(k.partial), _ptr(k.end), _ptr(out))
+    return out
+
+
+def selectors_on_coset(log_n: int, log_q: int, shift_limbs):
+    q = 1 << log_q
+    out = np.zeros((4, q, 4), dtype=np.uint64)
+    lib().or_selectors_on_coset(log_n, log_q, fr(shift_limbs), _ptr(out[0]), _ptr(out[1]), _ptr(out[2]), _ptr(out[3]))
+    return out
+
+
+def p2_quotient_values(lde, log_n: int, log_qd: int, vl: int, k: P2Constants, alpha_limbs):
+    x = np.ascontiguousarray(lde, dtype=np.uint64)
+    out = np.zeros((1 << (log_n + log_qd), 4), dtype=np.uint64)
+    lib().or_p2_quotient_values(_ptr(x), log_n, log_qd, vl, k.hf, k.pr, _ptr(k.begin), _ptr(k.partial),
+                                _ptr(k.end), fr(alpha_limbs), _ptr(out))
+    return out
+
+
+def quotient_and_eval(coeffs_col, point_limbs):
+    """quotient_and_eval (kzg/src/util.rs:100-111) on one coefficient column."""
+    c = np.ascontiguousarray(coeffs_col, dtype=np.uint64).reshape(-1, 4)
+    n = c.shape[0]
+    q = np.zeros((max(n - 1, 0), 4), dtype=np.uint64)
+    v = np.zeros(4, dtype=np.uint64)
+    lib().or_quotient_and_eval(_ptr(c), n, 1, fr(point_limbs), _ptr(q) if n > 1 else None, _ptr(v))
+    return q, v
 
 
 def num_threads() -> int:

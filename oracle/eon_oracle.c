@@ -730,3 +730,176 @@ void or_g1_msm(const g1_affine_t* pts, const fr_t* scalars, uint64_t n, g1_affin
     free(wsum);
     free(ks);
 }
+
+/* ---- Poseidon2-AIR over BN254 Fr: WIDTH 3, SBOX_DEGREE 5, SBOX_REGISTERS 1 ----
+ * poseidon2-air/src/{air.rs:108-288, columns.rs:12-71, generation.rs:76-288, vectorized.rs};
+ * linear layers: external = mds_light width 3 (poseidon2/src/external.rs:128-133),
+ * internal = [2,1,1;1,2,1;1,1,3] (bn254/src/poseidon2.rs:55-63).
+ * Columns per permutation: export, inputs[3], HF x (sbox x3[3], post[3]), PR x (x3, post_sbox),
+ * HF x (x3[3], post[3]).  Permutation j of a VECTOR_LEN-wide trace sits at row j / VL,
+ * columns [(j % VL) * cols, ...). */
+static void p2_ext(fr_t* s) {
+    fr_t sum = fadd(fadd(s[0], s[1]), s[2]);
+    s[0] = fadd(s[0], sum);
+    s[1] = fadd(s[1], sum);
+    s[2] = fadd(s[2], sum);
+}
+static void p2_int(fr_t* s) {
+    fr_t sum = fadd(s[0], fadd(s[1], s[2]));
+    s[0] = fadd(s[0], sum);
+    s[1] = fadd(s[1], sum);
+    s[2] = fadd(fadd(s[2], s[2]), sum);
+}
+
+uint32_t or_p2_num_cols(uint32_t hf, uint32_t pr) { return 1 + 3 + 2 * hf * 6 + pr * 2; }
+
+void or_p2_generate_trace(const fr_t* inputs, uint64_t n_perms, uint32_t vl, uint32_t hf, uint32_t pr,
+                          const fr_t* rc_begin, const fr_t* rc_partial, const fr_t* rc_end,
+                          fr_t* trace) {
+    /* generate_trace_rows_for_perm (poseidon2-air/src/generation.rs:130-288) */
+    uint32_t nc = or_p2_num_cols(hf, pr);
+#pragma omp parallel for schedule(static)
+    for (uint64_t j = 0; j < n_perms; j++) {
+        fr_t* c = trace + (j / vl) * (uint64_t)nc * vl + (j % vl) * nc;
+        fr_t s[3] = {inputs[3 * j], inputs[3 * j + 1], inputs[3 * j + 2]};
+        uint32_t k = 0;
+        c[k++] = fone(); /* export */
+        for (int i = 0; i < 3; i++) c[k++] = s[i];
+        p2_ext(s);
+        for (uint32_t half = 0; half < 2; half++) {
+            if (half == 1) {
+                for (uint32_t r = 0; r < pr; r++) {
+                    s[0] = fadd(s[0], rc_partial[r]);
+                    fr_t x2 = fmul(s[0], s[0]), x3 = fmul(x2, s[0]);
+                    c[k++] = x3;
+                    s[0] = fmul(x3, x2);
+                    c[k++] = s[0];
+                    p2_int(s);
+                }
+            }
+            const fr_t* rc = half == 0 ? rc_begin : rc_end;
+            for (uint32_t r = 0; r < hf; r++) {
+                for (int i = 0; i < 3; i++) {
+                    s[i] = fadd(s[i], rc[3 * r + i]);
+                    fr_t x2 = fmul(s[i], s[i]), x3 = fmul(x2, s[i]);
+                    c[k++] = x3;
+                    s[i] = fmul(x3, x2);
+                }
+                p2_ext(s);
+                for (int i = 0; i < 3; i++) c[k++] = s[i];
+            }
+        }
+    }
+}
+
+/* Constraint folding of one permutation row (air.rs:108-288 in assert order), accumulated as the
+ * ProverConstraintFolder does: acc += alpha^(K-1-k) * C_k (folder.rs:81-85), i.e. Horner
+ * acc = acc * alpha + C_k over the global constraint index k. */
+static fr_t p2_fold(const fr_t* c, fr_t acc, fr_t alpha, uint32_t hf, uint32_t pr, const fr_t* rc_begin,
+                    const fr_t* rc_partial, const fr_t* rc_end) {
+    fr_t s[3] = {c[1], c[2], c[3]};
+    uint32_t k = 4;
+    p2_ext(s);
+    for (uint32_t half = 0; half < 2; half++) {
+        if (half == 1) {
+            for (uint32_t r = 0; r < pr; r++) {
+                s[0] = fadd(s[0], rc_partial[r]);
+                fr_t x3 = c[k], post = c[k + 1];
+                k += 2;
+                fr_t x2 = fmul(s[0], s[0]);
+                acc = fadd(fmul(acc, alpha), fsub(x3, fmul(x2, s[0]))); /* assert_eq(x3, x2 * x) */
+                s[0] = fmul(x3, x2);
+                acc = fadd(fmul(acc, alpha), fsub(s[0], post)); /* assert_eq(state0, post_sbox) */
+                s[0] = post;
+                p2_int(s);
+            }
+        }
+        const fr_t* rc = half == 0 ? rc_begin : rc_end;
+        for (uint32_t r = 0; r < hf; r++) {
+            for (int i = 0; i < 3; i++) {
+                s[i] = fadd(s[i], rc[3 * r + i]);
+                fr_t x3 = c[k + i];
+                fr_t x2 = fmul(s[i], s[i]);
+                acc = fadd(fmul(acc, alpha), fsub(x3, fmul(x2, s[i])));
+                s[i] = fmul(x3, x2);
+            }
+            p2_ext(s);
+            for (int i = 0; i < 3; i++) {
+                acc = fadd(fmul(acc, alpha), fsub(s[i], c[k + 3 + i])); /* assert_eq(state_i, post_i) */
+                s[i] = c[k + 3 + i];
+            }
+            k += 6;
+        }
+    }
+    return acc;
+}
+
+/* selectors_on_coset (commit/src/domain.rs:252-292) for trace domain H (shift 1, size 2^log_n) on
+ * the coset shift * K (size 2^log_q); four Q-long vectors */
+void or_selectors_on_coset(uint32_t log_n, uint32_t log_q, fr_t shift, fr_t* is_first, fr_t* is_last,
+                           fr_t* is_transition, fr_t* inv_vanishing) {
+    uint64_t q = 1ull << log_q, n = 1ull << log_n;
+    uint32_t rate = log_q - log_n;
+    fr_t s_pow_n = shift;
+    for (uint32_t i = 0; i < log_n; i++) s_pow_n = fmul(s_pow_n, s_pow_n);
+    fr_t g_rate = or_two_adic_generator(rate), g_q = or_two_adic_generator(log_q);
+    fr_t h_inv = or_fr_inverse(or_two_adic_generator(log_n));
+    uint64_t nr = 1ull << rate;
+    fr_t* zh = (fr_t*)malloc(sizeof(fr_t) * nr);
+    fr_t* zh_inv = (fr_t*)malloc(sizeof(fr_t) * nr);
+    fr_t one = fone(), pw = one;
+    for (uint64_t j = 0; j < nr; j++) {
+        zh[j] = fsub(fmul(s_pow_n, pw), one);
+        zh_inv[j] = or_fr_inverse(zh[j]);
+        pw = fmul(pw, g_rate);
+    }
+    (void)n;
+#pragma omp parallel for schedule(static)
+    for (uint64_t i = 0; i < q; i++) {
+        fr_t x = fmul(shift, or_fr_pow(g_q, i));
+        fr_t z = zh[i % nr];
+        is_first[i] = fmul(z, or_fr_inverse(fsub(x, one)));
+        is_last[i] = fmul(z, or_fr_inverse(fsub(x, h_inv)));
+        is_transition[i] = fsub(x, h_inv);
+        inv_vanishing[i] = zh_inv[i % nr];
+    }
+    free(zh);
+    free(zh_inv);
+}
+
+void or_p2_quotient_values(const fr_t* lde, uint32_t log_n, uint32_t log_qd, uint32_t vl, uint32_t hf,
+                           uint32_t pr, const fr_t* rc_begin, const fr_t* rc_partial, const fr_t* rc_end,
+                           fr_t alpha, fr_t* out) {
+    /* quotient_values (eon-uni-stark/src/prover.rs:539-709) for the (vectorized) Poseidon2-AIR on
+     * the quotient domain 5 * K, |K| = 2^(log_n + log_qd): out[i] = acc(row i) * inv_vanishing[i]
+     * (the AIR reads no selectors and no next row) */
+    uint32_t log_q = log_n + log_qd;
+    uint64_t q = 1ull << log_q;
+    uint32_t nc = or_p2_num_cols(hf, pr);
+    fr_t* f = (fr_t*)malloc(sizeof(fr_t) * q * 4);
+    or_selectors_on_coset(log_n, log_q, or_fr_from_u64(5), f, f + q, f + 2 * q, f + 3 * q);
+#pragma omp parallel for schedule(static)
+    for (uint64_t i = 0; i < q; i++) {
+        fr_t acc = {{0, 0, 0, 0}};
+        for (uint32_t v = 0; v < vl; v++)
+            acc = p2_fold(lde + i * (uint64_t)nc * vl + (uint64_t)v * nc, acc, alpha, hf, pr, rc_begin,
+                          rc_partial, rc_end);
+        out[i] = fmul(acc, f[3 * q + i]);
+    }
+    free(f);
+}
+
+/* quotient_and_eval (kzg/src/util.rs:100-111) */
+void or_quotient_and_eval(const fr_t* coeffs, uint64_t n, uint64_t stride, fr_t point, fr_t* quotient,
+                          fr_t* value) {
+    if (n == 0) {
+        memset(value, 0, sizeof *value);
+        return;
+    }
+    fr_t carry = coeffs[(n - 1) * stride];
+    for (uint64_t i = n - 1; i-- > 0;) {
+        quotient[i] = carry;
+        carry = fadd(coeffs[i * stride], fmul(carry, point));
+    }
+    *value = carry;
+}

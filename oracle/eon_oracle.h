@@ -49,5 +49,17 @@ void or_g1_msm(const g1_affine_t* pts, const fr_t* scalars, uint64_t n, g1_affin
 fr_t or_eval_poly_col(const fr_t* coeffs, uint64_t h, uint64_t w, uint64_t col, fr_t point);
 void or_kzg_evaluations_on_domain(const fr_t* coeffs, uint64_t h, uint64_t w, uint32_t log_q,
                                   fr_t shift, fr_t* out);
+
+/* Poseidon2-AIR over BN254 (width 3, x^5 with one register) and the eon quotient */
+uint32_t or_p2_num_cols(uint32_t hf, uint32_t pr);
+void or_p2_generate_trace(const fr_t* inputs, uint64_t n_perms, uint32_t vl, uint32_t hf, uint32_t pr,
+                          const fr_t* rc_begin, const fr_t* rc_partial, const fr_t* rc_end, fr_t* trace);
+void or_selectors_on_coset(uint32_t log_n, uint32_t log_q, fr_t shift, fr_t* is_first, fr_t* is_last,
+                           fr_t* is_transition, fr_t* inv_vanishing);
+void or_p2_quotient_values(const fr_t* lde, uint32_t log_n, uint32_t log_qd, uint32_t vl, uint32_t hf,
+                           uint32_t pr, const fr_t* rc_begin, const fr_t* rc_partial, const fr_t* rc_end,
+                           fr_t alpha, fr_t* out);
+void or_quotient_and_eval(const fr_t* coeffs, uint64_t n, uint64_t stride, fr_t point, fr_t* quotient,
+                          fr_t* value);
 #endif
 

@@ -336,3 +336,136 @@ if __name__ == "__main__":  # quick self-check
     assert to_mont(1) == limbs_to_int((0xAC96341C4FFFFFFB, 0x36FC76959F60CD29, 0x666EA36F7879462E, 0x0E0A77C19A07DF2F))
     assert pow(two_adic_generator(28), 1 << 27, P) == P - 1
     print("ok")
+
+
+# --- Poseidon2-AIR over BN254 (poseidon2-air/src/air.rs:108-288) ---------------
+P2_WIDTH = 3
+
+
+def p2_ext(s):
+    """external layer: mds_light width 3 (poseidon2/src/external.rs:128-133)."""
+    t = sum(s) % P
+    return [(x + t) % P for x in s]
+
+
+def p2_int(s):
+    """internal layer [2,1,1;1,2,1;1,1,3] (bn254/src/poseidon2.rs:55-63)."""
+    t = sum(s) % P
+    return [(s[0] + t) % P, (s[1] + t) % P, (2 * s[2] + t) % P]
+
+
+def p2_num_cols(hf, pr):
+    return 1 + 3 + 2 * hf * 6 + 2 * pr
+
+
+def p2_constants(seed, hf=4, pr=56):
+    """Deterministic round constants (the reference draws them from rand's SmallRng,
+    poseidon2-air/src/constants.rs:37-46, whose stream cannot be reproduced offline)."""
+    rng = SplitMix64(seed)
+    f = lambda: from_mont(rng.fr_mont())  # noqa: E731
+    begin = [[f() for _ in range(3)] for _ in range(hf)]
+    partial = [f() for _ in range(pr)]
+    end = [[f() for _ in range(3)] for _ in range(hf)]
+    return begin, partial, end
+
+
+def p2_trace_row(inp, consts):
+    """generate_trace_rows_for_perm (poseidon2-air/src/generation.rs:130-288)."""
+    begin, partial, end = consts
+    row = [1] + list(inp)
+    s = p2_ext(list(inp))
+
+    def full(s, rc):
+        x3s = []
+        for i in range(3):
+            x = (s[i] + rc[i]) % P
+            x3 = pow(x, 3, P)
+            x3s.append(x3)
+            s[i] = x3 * x * x % P
+        s = p2_ext(s)
+        return s, x3s + list(s)
+
+    for rc in begin:
+        s, cols = full(s, rc)
+        row += cols
+    for rc in partial:
+        x = (s[0] + rc) % P
+        x3 = pow(x, 3, P)
+        s[0] = x3 * x * x % P
+        row += [x3, s[0]]
+        s = p2_int(s)
+    for rc in end:
+        s, cols = full(s, rc)
+        row += cols
+    return row
+
+
+def p2_constraints(row, consts):
+    """Every assert_zero of eval (air.rs:108-288) in order; assert_eq(x, y) = x - y
+    (air/src/air.rs:158-160)."""
+    begin, partial, end = consts
+    out = []
+    s = p2_ext([row[1], row[2], row[3]])
+    k = 4
+
+    def full(s, rc, k):
+        for i in range(3):
+            x = (s[i] + rc[i]) % P
+            x3 = row[k + i]
+            out.append((x3 - x * x * x) % P)
+            s[i] = x3 * x * x % P
+        s = p2_ext(s)
+        for i in range(3):
+            out.append((s[i] - row[k + 3 + i]) % P)
+            s[i] = row[k + 3 + i]
+        return s, k + 6
+
+    for rc in begin:
+        s, k = full(s, rc, k)
+    for rc in partial:
+        x = (s[0] + rc) % P
+        x3 = row[k]
+        out.append((x3 - x * x * x) % P)
+        s[0] = x3 * x * x % P
+        out.append((s[0] - row[k + 1]) % P)
+        s[0] = row[k + 1]
+        s = p2_int(s)
+        k += 2
+    for rc in end:
+        s, k = full(s, rc, k)
+    return out
+
+
+def selectors_on_coset(log_n, log_q, shift):
+    """commit/src/domain.rs:252-292."""
+    n, q = 1 << log_n, 1 << log_q
+    rate = log_q - log_n
+    h = two_adic_generator(log_n)
+    h_inv = pow(h, -1, P)
+    gq = two_adic_generator(log_q)
+    s_pow_n = pow(shift, n, P)
+    gr = two_adic_generator(rate)
+    zh = [(s_pow_n * pow(gr, j, P) - 1) % P for j in range(1 << rate)]
+    xs = [shift * pow(gq, i, P) % P for i in range(q)]
+    first = [zh[i % len(zh)] * pow(xs[i] - 1, -1, P) % P for i in range(q)]
+    last = [zh[i % len(zh)] * pow(xs[i] - h_inv, -1, P) % P for i in range(q)]
+    trans = [(x - h_inv) % P for x in xs]
+    inv_van = [pow(zh[i % len(zh)], -1, P) for i in range(q)]
+    return first, last, trans, inv_van
+
+
+def p2_quotient_values(lde_rows, log_n, log_qd, vl, consts, alpha):
+    """quotient_values (eon-uni-stark/src/prover.rs:539-709): sum_k alpha^(K-1-k) C_k(row) /
+    Z_H(x_i); alpha powers reversed as prover.rs:578-579."""
+    nc = p2_num_cols(len(consts[0]), len(consts[1]))
+    _, _, _, inv_van = selectors_on_coset(log_n, log_n + log_qd, GENERATOR)
+    K = 160 * vl if (len(consts[0]), len(consts[1])) == (4, 56) else None
+    out = []
+    for i, row in enumerate(lde_rows):
+        cs = []
+        for v in range(vl):
+            cs += p2_constraints(row[v * nc:(v + 1) * nc], consts)
+        K = len(cs)
+        acc = sum(pow(alpha, K - 1 - k, P) * c for k, c in enumerate(cs)) % P
+        out.append(acc * inv_van[i] % P)
+    return out

@@ -43,6 +43,11 @@ class eon_fr(ctypes.Structure):
     _fields_ = [("l", ctypes.c_uint64 * 4)]
 
 
+class eon_poseidon2_constants(ctypes.Structure):
+    _fields_ = [("half_full_rounds", ctypes.c_uint32), ("partial_rounds", ctypes.c_uint32),
+                ("beginning", ctypes.c_void_p), ("partial", ctypes.c_void_p), ("ending", ctypes.c_void_p)]
+
+
 class eon_g1_affine(ctypes.Structure):
     _fields_ = [("x", ctypes.c_uint64 * 4), ("y", ctypes.c_uint64 * 4)]
 
@@ -81,6 +86,12 @@ SIGNATURES = {
     "eon_msm_bases_create_dev": (_INT, [_P, _P, _U64, _U32, ctypes.POINTER(_P)]),
     "eon_g1_srs_powers": (_INT, [_P, _P, _U64, _P]),
     "eon_g1_srs_powers_dev": (_INT, [_P, _P, _U64, _P]),
+    "eon_selectors_on_coset_dev": (_INT, [_P, _U32, _U32, _P, _P]),
+    "eon_p2air_create": (_INT, [_P, _P, _U32, ctypes.POINTER(_P)]),
+    "eon_p2air_destroy": (None, [_P]),
+    "eon_p2air_width": (_U32, [_P]),
+    "eon_p2air_generate_trace_dev": (_INT, [_P, _P, _P, _U64, _P]),
+    "eon_p2air_quotient_values_dev": (_INT, [_P, _P, _P, _U32, _U32, _P, _P]),
 }
 
 _lib = None

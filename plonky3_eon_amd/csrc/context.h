@@ -99,6 +99,9 @@ struct eon_ctx {
     // MSM pipeline workspace
     eon::MsmWork msm;
 
+    // quotient: vanishing-polynomial table
+    eon::DevBuf sel_tab;
+
     // scratch: NTT intermediates, host-API staging
     eon::DevBuf scratch, stage_in, stage_out;
 };

@@ -132,6 +132,14 @@ int eon_msm_g1(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* scalars, 
                eon_g1_affine* out);
 int eon_msm_g1_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* scalars, uint64_t n,
                    eon_g1_affine* out);
+/* One MSM per column of a row-major rows x width Fr matrix over bases[0..rows): out[j] =
+ * sum_i mat[i][j] * P_i (width affine points, host) -- the per-column commit_column loop of
+ * KzgPcs::commit (kzg/src/pcs.rs:244-251) and of open's witnesses (pcs.rs:310-316).  `mat` is
+ * host (eon_msm_g1_columns) or device (eon_msm_g1_columns_dev). */
+int eon_msm_g1_columns(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* mat, uint64_t rows,
+                       uint32_t width, eon_g1_affine* out);
+int eon_msm_g1_columns_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* mat,
+                           uint64_t rows, uint32_t width, eon_g1_affine* out);
 /* As eon_msm_bases_create with `bases` a DEVICE pointer (coordinates are not re-validated). */
 int eon_msm_bases_create_dev(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32_t flags,
                              eon_msm_bases** out);

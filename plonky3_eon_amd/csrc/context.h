@@ -49,10 +49,11 @@ struct Status {
 // device workspace of one MSM pipeline run (msm.hip); grows on demand, reused across calls
 struct MsmWork {
     DevBuf keys, vals, keys2, vals2, start, count, piece_off, off2, owner, piece_sums,
-        piece_sums2, bucket_sums, red_a, red_b, temp;
+        piece_sums2, bucket_sums, red_a, red_b, temp, results;
     void release() {
         for (DevBuf* b : {&keys, &vals, &keys2, &vals2, &start, &count, &piece_off, &off2, &owner,
-                          &piece_sums, &piece_sums2, &bucket_sums, &red_a, &red_b, &temp})
+                          &piece_sums, &piece_sums2, &bucket_sums, &red_a, &red_b, &temp,
+                          &results})
             b->release();
     }
 };

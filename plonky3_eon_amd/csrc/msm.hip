@@ -16,7 +16,11 @@
 //                       (log-depth under any skew, e.g. all-equal scalars), k_bucket_final.
 //   7. k_segment_sum /  sum_d d * B_d per group: segments of SEG buckets by running sums, the
 //      k_tree_sum       segment offset applied by a short double-and-add, then LDS tree sums.
-//   8. host             (groups > 1 only) Horner over the per-window sums, then affine.
+//   8. k_window_horner  (per-window buckets only) sum_w 2^(c*w) G_w per MSM; batched affine.
+//
+// Batched mode (eon_msm_g1_columns*): one pipeline run handles many MSMs at once -- the columns
+// of a row-major coefficient matrix, as KzgPcs::commit commits every column against the same
+// SRS prefix (kzg/src/pcs.rs:244-251) -- with the column index in the high bits of the key.
 //
 // Fixed-base mode (eon_msm_bases_create with EON_MSM_PRECOMPUTE; the KZG SRS): the bases object
 // stores 2^(c*w) * P_i in affine for every window w, so every window's digits land in ONE bucket
@@ -60,13 +64,18 @@ __device__ __forceinline__ uint32_t window_bits(const uint32_t* s, uint32_t pos,
     return (uint32_t)v & ((1u << c) - 1);
 }
 
-__global__ void k_msm_digits(const Fr* scalars, uint64_t n, uint32_t c, uint32_t windows,
-                             uint32_t precomputed, uint32_t* keys, uint32_t* vals) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const Fr s = to_canonical(scalars[i]);
+// One thread per (row i, MSM column col): the scalar is scalars[i * ld + col] (a row-major
+// matrix column; ld = 1, cols = 1 for a single MSM).  Group of a digit: the column (fixed-base
+// mode: every window shares the column's bucket set) or (column, window).
+__global__ void k_msm_digits(const Fr* scalars, uint64_t n, uint64_t ld, uint32_t cols, uint32_t c,
+                             uint32_t windows, uint32_t precomputed, uint32_t* keys, uint32_t* vals) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * cols) return;
+    const uint32_t col = (uint32_t)(t % cols);
+    const uint64_t i = t / cols;
+    const Fr s = to_canonical(scalars[i * ld + col]);
     const uint32_t B = 1u << (c - 1);
-    const uint32_t sentinel = precomputed ? B : windows * B;
+    const uint32_t sentinel = (precomputed ? cols : cols * windows) * B;
     uint32_t carry = 0;
     for (uint32_t w = 0; w < windows; w++) {
         const uint32_t raw = window_bits(s.v, w * c, c) + carry;
@@ -81,16 +90,31 @@ __global__ void k_msm_digits(const Fr* scalars, uint64_t n, uint32_t c, uint32_t
             neg = 0;
             carry = 0;
         }
-        const uint64_t e = (uint64_t)w * n + i;
+        const uint64_t e = ((uint64_t)w * n + i) * cols + col;
         if (mag == 0) {
             keys[e] = sentinel;
             vals[e] = 0;
         } else {
-            keys[e] = (precomputed ? 0u : w * B) + mag - 1;
+            const uint32_t g = precomputed ? col : col * windows + w;
+            keys[e] = g * B + mag - 1;
             const uint32_t ref = precomputed ? (uint32_t)(i * windows + w) : (uint32_t)i;
             vals[e] = ref | (neg << 31);
         }
     }
+}
+
+// per-window sums -> per-column result: sum_w 2^(c*w) * G[col*W + w] (one thread per column)
+__global__ void k_window_horner(const G1Xyzz* gs, uint32_t cols, uint32_t W, uint32_t c,
+                                G1Xyzz* out) {
+    const uint32_t col = blockIdx.x * blockDim.x + threadIdx.x;
+    if (col >= cols) return;
+    const G1Xyzz* g = gs + (uint64_t)col * W;
+    G1Xyzz acc = g[W - 1];
+    for (int w = (int)W - 2; w >= 0; w--) {
+        for (uint32_t k = 0; k < c; k++) acc = xyzz_dbl(acc);
+        acc = xyzz_add(acc, g[w]);
+    }
+    out[col] = acc;
 }
 
 // start[b] = index of the first sorted pair with key >= b, for b in [0, nb]
@@ -348,23 +372,18 @@ Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32
     return Status::ok();
 }
 
-// The device pipeline; `scalars` is a device pointer to n Fr.  Writes the result to *result.
-Status msm_run(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, uint64_t n,
-               G1Affine* result) {
-    if (n > b->n) return Status::err(EON_E_SHAPE, "more scalars than bases");
-    if (n == 0) {  // G1::multi_exp returns the identity for empty input (curve.rs:163-165)
-        result->x = Fq::zero();
-        result->y = Fq::zero();
-        return Status::ok();
-    }
+// One batch of `cols` MSMs of length n over bases[0..n): MSM j uses scalars[i * ld + j].
+// Results (affine) are written to the device array `out_dev` (cols entries).
+static Status msm_batch(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, uint64_t n,
+                        uint64_t ld, uint32_t cols, G1Affine* out_dev) {
     hipStream_t st = ctx->stream;
     MsmWork& wk = ctx->msm;
     const uint32_t c = b->precomputed ? b->c : choose_c(n, false);
     const uint32_t W = b->precomputed ? b->windows : (255 + c - 1) / c;
     const uint32_t B = 1u << (c - 1);
-    const uint32_t groups = b->precomputed ? 1 : W;
+    const uint32_t groups = b->precomputed ? cols : cols * W;
     const uint32_t nb = groups * B;
-    const uint64_t E = n * W;
+    const uint64_t E = n * W * cols;
     if (E >= (1ull << 32)) return Status::err(EON_E_SHAPE, "MSM too large for 32-bit pair indices");
     uint32_t key_bits = 1;
     while ((1ull << key_bits) <= nb) key_bits++;
@@ -385,9 +404,10 @@ Status msm_run(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, uint64_t
     EON_HIP(wk.temp.ensure(std::max(sort_bytes, scan_bytes)));
 
     Profiler* prof = &ctx->prof;
-    prof->begin("k_msm_digits", n * 32 + E * 8, st);
-    hipLaunchKernelGGL(k_msm_digits, dim3(blocks_for(n, 256)), dim3(256), 0, st, scalars, n, c, W,
-                       (uint32_t)b->precomputed, wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>());
+    prof->begin("k_msm_digits", n * cols * 32 + E * 8, st);
+    hipLaunchKernelGGL(k_msm_digits, dim3(blocks_for(n * cols, 256)), dim3(256), 0, st, scalars, n,
+                       ld, cols, c, W, (uint32_t)b->precomputed, wk.keys.as<uint32_t>(),
+                       wk.vals.as<uint32_t>());
     prof->end(st);
     EON_HIP(hipGetLastError());
     prof->begin("radix_sort_pairs", E * 16, st);
@@ -473,17 +493,50 @@ Status msm_run(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, uint64_t
         len = blk;
     }
     EON_HIP(hipGetLastError());
-    std::vector<G1Xyzz> gs(groups);
-    EON_HIP(hipMemcpyAsync(gs.data(), cur, groups * sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
-    EON_HIP(hipStreamSynchronize(st));
-    // Horner over windows (groups > 1): sum_w 2^(c*w) * G_w
-    G1Xyzz acc = gs[groups - 1];
-    for (int w = (int)groups - 2; w >= 0; w--) {
-        for (uint32_t k = 0; k < c; k++) acc = xyzz_dbl(acc);
-        acc = xyzz_add(acc, gs[w]);
+    // `cur` holds one point per group; per column: the group itself (fixed base) or the
+    // Horner combination of its windows; then batched XYZZ -> affine on device
+    G1Xyzz* per_col = cur;
+    if (!b->precomputed) {
+        hipLaunchKernelGGL(k_window_horner, dim3(blocks_for(cols, 64)), dim3(64), 0, st, cur, cols, W,
+                           c, nxt);
+        per_col = nxt;
     }
-    *result = xyzz_to_affine(acc);
+    EON_HIP(launch_batch_to_affine(per_col, cols, out_dev, st));
     return Status::ok();
+}
+
+Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, uint64_t n,
+                       uint32_t width, G1Affine* out_host) {
+    if (n > b->n) return Status::err(EON_E_SHAPE, "more scalars than bases");
+    if (width == 0) return Status::ok();
+    if (n == 0) {  // G1::multi_exp returns the identity for empty input (curve.rs:163-165)
+        for (uint32_t j = 0; j < width; j++) {
+            out_host[j].x = Fq::zero();
+            out_host[j].y = Fq::zero();
+        }
+        return Status::ok();
+    }
+    const uint32_t c = b->precomputed ? b->c : choose_c(n, false);
+    const uint64_t W = (255 + c - 1) / c;
+    // columns per batch: keep the digit pairs of one batch at <= 2^28 (4 GiB of sort buffers)
+    uint64_t cpb = (1ull << 28) / (n * W);
+    if (cpb < 1) cpb = 1;
+    const uint64_t max_groups = b->precomputed ? cpb : cpb * W;
+    if (max_groups > 65535) cpb = b->precomputed ? 65535 : 65535 / W;
+    EON_HIP(ctx->msm.results.ensure(width * sizeof(G1Affine)));
+    G1Affine* res = ctx->msm.results.as<G1Affine>();
+    for (uint32_t j0 = 0; j0 < width; j0 += (uint32_t)cpb) {
+        const uint32_t cols = (uint32_t)std::min<uint64_t>(cpb, width - j0);
+        EON_TRY(msm_batch(ctx, b, scalars + j0, n, width, cols, res + j0));
+    }
+    EON_HIP(hipMemcpyAsync(out_host, res, width * sizeof(G1Affine), hipMemcpyDeviceToHost, ctx->stream));
+    EON_HIP(hipStreamSynchronize(ctx->stream));
+    return Status::ok();
+}
+
+Status msm_run(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, uint64_t n,
+               G1Affine* result) {
+    return msm_run_columns(ctx, b, scalars, n, 1, result);
 }
 
 }  // namespace eon
@@ -560,6 +613,38 @@ int eon_msm_g1_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* scala
     G1Affine r;
     Status s = msm_run(ctx, bases, reinterpret_cast<const Fr*>(scalars), n, &r);
     if (!s.bad()) *out = g1_to_abi(r);
+    return finish(ctx, s);
+}
+
+int eon_msm_g1_columns_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* mat,
+                           uint64_t rows, uint32_t width, eon_g1_affine* out) {
+    if (!ctx) return EON_E_ARG;
+    if (!bases || (width && !out) || (rows && width && !mat)) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    std::vector<G1Affine> r(width);
+    Status s = msm_run_columns(ctx, bases, reinterpret_cast<const Fr*>(mat), rows, width, r.data());
+    if (!s.bad())
+        for (uint32_t j = 0; j < width; j++) out[j] = g1_to_abi(r[j]);
+    return finish(ctx, s);
+}
+
+int eon_msm_g1_columns(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* mat, uint64_t rows,
+                       uint32_t width, eon_g1_affine* out) {
+    if (!ctx) return EON_E_ARG;
+    if (!bases || (width && !out) || (rows && width && !mat)) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    std::vector<G1Affine> r(width);
+    Status s = [&]() -> Status {
+        if (rows > bases->n) return Status::err(EON_E_SHAPE, "more rows than bases");
+        const size_t bytes = (size_t)rows * width * sizeof(Fr);
+        EON_HIP(ctx->stage_in.ensure(bytes ? bytes : 32));
+        if (bytes) EON_HIP(hipMemcpyAsync(ctx->stage_in.p, mat, bytes, hipMemcpyHostToDevice, ctx->stream));
+        return msm_run_columns(ctx, bases, ctx->stage_in.as<Fr>(), rows, width, r.data());
+    }();
+    if (!s.bad())
+        for (uint32_t j = 0; j < width; j++) out[j] = g1_to_abi(r[j]);
     return finish(ctx, s);
 }
 

@@ -50,6 +50,23 @@ class MsmBases:
             ctx.check(lib.eon_msm_g1(ctx.handle, self._h, _p(s), s.shape[0], _p(out)))
         return out
 
+    def msm_columns(self, mat) -> np.ndarray:
+        """One MSM per column of a (rows, width, 4) Fr matrix -> (width, 8) affine points."""
+        lib, ctx = self.ctx.lib, self.ctx
+        rows, width = int(mat.shape[0]), int(mat.shape[1])
+        out = np.zeros((width, 8), dtype=np.uint64)
+        if _is_torch(mat):
+            import torch
+
+            m = mat.contiguous()
+            ctx.set_stream(torch.cuda.current_stream(m.device).cuda_stream)
+            ctx.check(lib.eon_msm_g1_columns_dev(ctx.handle, self._h, ctypes.c_void_p(m.data_ptr()), rows, width,
+                                                 _p(out)))
+        else:
+            m = np.ascontiguousarray(mat, dtype=np.uint64)
+            ctx.check(lib.eon_msm_g1_columns(ctx.handle, self._h, _p(m), rows, width, _p(out)))
+        return out
+
     def close(self):
         if getattr(self, "_h", None):
             self.ctx.lib.eon_msm_bases_destroy(self._h)

@@ -121,3 +121,34 @@ def test_kzg_identity_full_size(gpu_ctx):
     st = torch.from_numpy(s.view(np.int64)).to("cuda:0")
     np.testing.assert_array_equal(bases.msm(st), want)
     np.testing.assert_array_equal(MsmBases(pts, gpu_ctx, precompute=False).msm(s), want)
+
+
+@pytest.mark.parametrize("precompute", [True, False])
+def test_msm_columns_vs_c(gpu_ctx, precompute):
+    """KzgPcs::commit's per-column commit_column loop (kzg/src/pcs.rs:244-251) as one batched call."""
+    rows, width = 200, 7
+    pts = srs_powers(256, 12345, gpu_ctx)
+    mat = C.random_fr(31, rows * width).reshape(rows, width, 4)
+    mat[:, 3] = 0  # an all-zero column commits to the identity
+    got = MsmBases(pts, gpu_ctx, precompute=precompute).msm_columns(mat)
+    for j in range(width):
+        np.testing.assert_array_equal(got[j], C.g1_msm(pts[:rows], mat[:, j]))
+    assert not got[3].any()
+
+
+@pytest.mark.slow
+def test_msm_columns_batched_kzg_identity(gpu_ctx):
+    """300 columns x 2^16 rows (split into 2 internal batches), device-resident: every column
+    satisfies sum_i m[i][j] alpha^i G = [f_j(alpha)] G."""
+    import torch
+
+    rows, width = 1 << 16, 300
+    alpha = C.fr_from_u64(12345)
+    pts = srs_powers(rows, 12345, gpu_ctx)
+    mat = C.random_fr(32, rows * width).reshape(rows, width, 4)
+    bases = MsmBases(pts, gpu_ctx, precompute=True)
+    got = bases.msm_columns(torch.from_numpy(mat.view(np.int64)).to("cuda:0"))
+    g = C.g1_generator()
+    for j in list(range(0, width, 13)) + [width - 1]:
+        f_alpha = C.eval_poly_col(mat, j, alpha)
+        np.testing.assert_array_equal(got[j], C.g1_mul(g, f_alpha), err_msg=f"column {j}")

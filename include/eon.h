@@ -140,6 +140,13 @@ int eon_msm_g1_columns(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* m
                        uint32_t width, eon_g1_affine* out);
 int eon_msm_g1_columns_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* mat,
                            uint64_t rows, uint32_t width, eon_g1_affine* out);
+/* quotient_and_eval (kzg/src/util.rs:100-111) for every column of a row-major rows x width
+ * coefficient matrix (device) at `point` (host): quotient (device) receives the (rows-1) x width
+ * synthetic-division quotients, values (device) the width evaluations f_j(point), as
+ * KzgPcs::open computes per (matrix, point, column) (kzg/src/pcs.rs:297-330). */
+int eon_quotient_and_eval_columns_dev(eon_ctx* ctx, const eon_fr* coeffs, uint64_t rows,
+                                      uint32_t width, const eon_fr* point, eon_fr* quotient,
+                                      eon_fr* values);
 /* As eon_msm_bases_create with `bases` a DEVICE pointer (coordinates are not re-validated). */
 int eon_msm_bases_create_dev(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32_t flags,
                              eon_msm_bases** out);

@@ -1,0 +1,60 @@
+"""CPU restatement of eon_uni_stark::prove for the Poseidon2-AIR with KzgPcs, assembled from the
+C restatement oracle.  TEST INFRASTRUCTURE ONLY.
+
+Follows prove_with_preprocessed (eon-uni-stark/src/prover.rs:28-534) with the reference's own
+algorithms where they differ from the GPU path: get_evaluations_on_domain is the Horner loop of
+kzg/src/pcs.rs:267-287, openings run quotient_and_eval per column (kzg/src/util.rs:100-111),
+every commitment is commit_column = G1::multi_exp (kzg/src/util.rs:37-40).  alpha and zeta are
+inputs (the Fiat-Shamir transcript is out of scope, see plonky3_eon_amd/prover.py).
+"""
+
+import numpy as np
+
+from . import coracle as C
+from . import pyoracle as O
+
+
+def _lim(x):
+    return np.array(O.int_to_limbs(O.to_mont(x % O.P)), dtype=np.uint64)
+
+
+def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1):
+    n, w = trace.shape[0], trace.shape[1]
+    log_n = n.bit_length() - 1
+    alpha = _lim(alpha_int)
+    coeffs = C.idft_batch(trace)  # coset_idft_batch(evals, shift 1) (kzg/src/pcs.rs:242)
+    trace_commit = np.stack([C.g1_msm(srs[:n], coeffs[:, j]) for j in range(w)])
+    lde = C.kzg_evaluations_on_domain(coeffs, log_n + log_qd, _lim(O.GENERATOR))
+    qv = C.p2_quotient_values(lde, log_n, log_qd, vl, consts, alpha)
+    chunks = 1 << log_qd
+    g_q = O.two_adic_generator(log_n + log_qd)
+    q_coeffs, quotient_commit = [], []
+    for c in range(chunks):
+        ev = np.ascontiguousarray(qv.reshape(n, chunks, 4)[:, c:c + 1, :])
+        shift = O.GENERATOR * pow(g_q, c, O.P) % O.P
+        cc = C.coset_idft_batch(ev, _lim(shift))
+        q_coeffs.append(cc)
+        quotient_commit.append(C.g1_msm(srs[:n], cc[:, 0]))
+    zeta_next = zeta_int * O.two_adic_generator(log_n) % O.P
+
+    def open_matrix(cf, points):
+        vals, wits = [], []
+        for z in points:
+            v, wt = [], []
+            for j in range(cf.shape[1]):
+                q, val = C.quotient_and_eval(cf[:, j], _lim(z))
+                v.append(val)
+                wt.append(C.g1_msm(srs[:n - 1], q) if n > 1 else np.zeros(8, np.uint64))
+            vals.append(np.stack(v))
+            wits.append(np.stack(wt))
+        return vals, wits
+
+    trace_open = open_matrix(coeffs, [zeta_int, zeta_next])
+    quot_open = [open_matrix(cc, [zeta_int]) for cc in q_coeffs]
+    return {
+        "trace_commit": trace_commit,
+        "quotient_commit": np.stack(quotient_commit),
+        "trace_open": trace_open,
+        "quotient_open": quot_open,
+        "quotient_values": qv,
+    }

@@ -85,6 +85,7 @@ SIGNATURES = {
     "eon_g1_multi_exp": (_INT, [_P, _P, _P, _U64, _P]),
     "eon_msm_g1_columns": (_INT, [_P, _P, _P, _U64, _U32, _P]),
     "eon_msm_g1_columns_dev": (_INT, [_P, _P, _P, _U64, _U32, _P]),
+    "eon_quotient_and_eval_columns_dev": (_INT, [_P, _P, _U64, _U32, _P, _P, _P]),
     "eon_msm_bases_create_dev": (_INT, [_P, _P, _U64, _U32, ctypes.POINTER(_P)]),
     "eon_g1_srs_powers": (_INT, [_P, _P, _U64, _P]),
     "eon_g1_srs_powers_dev": (_INT, [_P, _P, _U64, _P]),

@@ -260,6 +260,7 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     for (auto e : ctx->prof.pool) (void)hipEventDestroy(e);
     ctx->msm.release();
     ctx->sel_tab.release();
+    ctx->kzg_tmp.release();
     ctx->scratch.release();
     ctx->stage_in.release();
     ctx->stage_out.release();

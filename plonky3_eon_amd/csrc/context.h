@@ -100,8 +100,8 @@ struct eon_ctx {
     // MSM pipeline workspace
     eon::MsmWork msm;
 
-    // quotient: vanishing-polynomial table
-    eon::DevBuf sel_tab;
+    // quotient: vanishing-polynomial table; KZG opening scan workspace
+    eon::DevBuf sel_tab, kzg_tmp;
 
     // scratch: NTT intermediates, host-API staging
     eon::DevBuf scratch, stage_in, stage_out;

@@ -1,0 +1,158 @@
+"""Host-side mirror of p3-kzg's KzgPcs over the C ABI, with every matrix device-resident.
+
+Reference: ``KzgPcs`` (kzg/src/pcs.rs:143-402) implementing ``Pcs<Fr, Challenger>``
+(commit/src/pcs.rs:21-187) over ``TwoAdicMultiplicativeCoset`` domains (commit/src/domain.rs).
+
+* ``commit``                     -- coset_idft_batch of each matrix (pcs.rs:242) and one KZG
+                                    commitment (MSM over the SRS g1_powers) per column
+                                    (pcs.rs:244-251), as one batched device MSM.
+* ``get_evaluations_on_domain``  -- pcs.rs:267-287 evaluates every column at every point by
+                                    Horner; the same values come from one coset LDE.
+* ``commit_quotient``            -- commit/src/pcs.rs:82-101: split_evals / split_domains
+                                    (domain.rs:174-221), then commit.
+* ``open``                       -- pcs.rs:289-335: per (matrix, point) the synthetic-division
+                                    quotients of every column and their commitments.
+
+Commitments / witnesses are (width, 8) u64 arrays of affine G1 points (x, y Fq Montgomery).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from .dft import Context, Radix2Dit, default_context
+from .field import FR_MODULUS, fr_mont, fr_to_abi, fr_unmont
+from .msm import MsmBases, srs_powers
+
+GENERATOR = 5
+_TWO_ADIC_GENERATOR_MONT = (0x636E735580D13D9C, 0xA22BF3742445FFD6, 0x56452AC01EB203D8, 0x1860EF942963F9E7)
+
+
+def two_adic_generator(bits: int) -> int:
+    """bn254/src/field.rs:567-573 (host-side domain bookkeeping)."""
+    g = fr_unmont(sum(x << (64 * i) for i, x in enumerate(_TWO_ADIC_GENERATOR_MONT)))
+    for _ in range(bits, 28):
+        g = g * g % FR_MODULUS
+    return g
+
+
+@dataclass(frozen=True)
+class Domain:
+    """TwoAdicMultiplicativeCoset (field/src/coset.rs): shift * <w_(2^log_size)>."""
+
+    shift: int
+    log_size: int
+
+    @property
+    def size(self):
+        return 1 << self.log_size
+
+    def generator(self):
+        return two_adic_generator(self.log_size)
+
+    def next_point(self, x: int) -> int:
+        """commit/src/domain.rs:115-117."""
+        return x * self.generator() % FR_MODULUS
+
+    def create_disjoint_domain(self, min_size: int) -> "Domain":
+        """commit/src/domain.rs:155-168."""
+        return Domain(self.shift * GENERATOR % FR_MODULUS, max(0, (min_size - 1).bit_length()))
+
+    def split_domains(self, num_chunks: int):
+        """commit/src/domain.rs:174-186."""
+        lc = num_chunks.bit_length() - 1
+        g = self.generator()
+        return [Domain(self.shift * pow(g, i, FR_MODULUS) % FR_MODULUS, self.log_size - lc) for i in range(num_chunks)]
+
+
+@dataclass
+class MatrixProverData:
+    """kzg/src/pcs.rs:46-63: the committed evaluations and their coefficients (device)."""
+
+    domain: Domain
+    evals: object
+    coeffs: object
+
+
+@dataclass
+class Opened:
+    values: list = field(default_factory=list)     # [matrix][point] -> (width, 4) u64 Fr
+    witnesses: list = field(default_factory=list)  # [matrix][point] -> (width, 8) u64 G1
+
+
+class GpuKzgPcs:
+    def __init__(self, max_degree: int, alpha: int, ctx: Context | None = None):
+        """KzgPcs::new(max_degree, alpha) with the test SRS init_srs_unsafe
+        (kzg/src/params.rs:123-139); the g1_powers stay on device as fixed-base MSM bases."""
+        self.ctx = ctx or default_context(0)
+        self.max_degree = max_degree
+        self.bases = MsmBases(srs_powers(max_degree + 1, alpha, self.ctx), self.ctx, precompute=True)
+        self.dft = Radix2Dit(self.ctx)
+
+    # -- Pcs surface -----------------------------------------------------------------------------
+    def natural_domain_for_degree(self, degree: int) -> Domain:
+        return Domain(1, (degree - 1).bit_length() if degree > 1 else 0)
+
+    def ensure_supported(self, degree: int):
+        """kzg/src/params.rs:164-173 (KzgError::DegreeTooLarge)."""
+        if degree > self.max_degree:
+            raise _lib.EonError(_lib.EON_E_DEGREE_TOO_LARGE, f"degree {degree} > max {self.max_degree}")
+
+    def commit(self, evaluations):
+        commitments, data = [], []
+        for domain, evals in evaluations:
+            h = int(evals.shape[0])
+            if h != domain.size:
+                raise _lib.EonError(_lib.EON_E_SHAPE, "evaluation height must match domain size")
+            self.ensure_supported(max(h - 1, 0))
+            coeffs = self.dft.coset_idft_batch(evals, domain.shift)
+            commitments.append(self.bases.msm_columns(coeffs))
+            data.append(MatrixProverData(domain, evals, coeffs))
+        return commitments, data
+
+    def get_evaluations_on_domain(self, prover_data, idx: int, domain: Domain):
+        m = prover_data[idx]
+        if m.domain == domain:
+            return m.evals
+        if domain.log_size < m.domain.log_size:
+            raise _lib.EonError(_lib.EON_E_SHAPE, "evaluation domain smaller than the committed domain")
+        # f(domain.shift * w^k) = coset LDE of the evals on m.domain with shift domain.shift / m.domain.shift
+        rel = domain.shift * pow(m.domain.shift, -1, FR_MODULUS) % FR_MODULUS
+        return self.dft.coset_lde_batch(m.evals, domain.log_size - m.domain.log_size, rel)
+
+    def commit_quotient(self, quotient_domain: Domain, quotient_evals, num_chunks: int):
+        """commit/src/pcs.rs:82-101; chunk c holds rows {i * num_chunks + c} (domain.rs:188-221)."""
+        q = quotient_evals.reshape(quotient_domain.size // num_chunks, num_chunks, 4)
+        chunks = [q[:, c:c + 1, :].contiguous() for c in range(num_chunks)]
+        return self.commit(list(zip(quotient_domain.split_domains(num_chunks), chunks)))
+
+    def open(self, rounds):
+        """rounds: [(prover_data, points_per_matrix)] -> (opened values, witnesses) per round."""
+        import torch
+
+        out = []
+        for prover_data, points_per_matrix in rounds:
+            if len(prover_data) != len(points_per_matrix):
+                raise _lib.EonError(_lib.EON_E_SHAPE, "one point list per matrix")
+            r = Opened()
+            for m, points in zip(prover_data, points_per_matrix):
+                n, w = int(m.coeffs.shape[0]), int(m.coeffs.shape[1])
+                vals, wits = [], []
+                for z in points:
+                    quo = torch.empty((max(n - 1, 1), w, 4), dtype=torch.int64, device=m.coeffs.device)
+                    v = torch.empty((w, 4), dtype=torch.int64, device=m.coeffs.device)
+                    pz = fr_to_abi(z)
+                    self.ctx.set_stream(torch.cuda.current_stream(m.coeffs.device).cuda_stream)
+                    self.ctx.check(self.ctx.lib.eon_quotient_and_eval_columns_dev(
+                        self.ctx.handle, ctypes.c_void_p(m.coeffs.data_ptr()), n, w, ctypes.byref(pz),
+                        ctypes.c_void_p(quo.data_ptr()), ctypes.c_void_p(v.data_ptr())))
+                    wits.append(self.bases.msm_columns(quo[:n - 1]))
+                    vals.append(v.cpu().numpy().view(np.uint64))
+                r.values.append(vals)
+                r.witnesses.append(wits)
+            out.append(r)
+        return out

@@ -1,0 +1,75 @@
+"""End-to-end GPU prove of the (vectorized) Poseidon2-AIR with the KZG PCS against the CPU
+restatement (oracle/prove_oracle.py, which uses the reference's Horner
+get_evaluations_on_domain and per-column quotient_and_eval), every output bit-exact."""
+
+import numpy as np
+import pytest
+
+from oracle import coracle as C
+from oracle import prove_oracle
+from oracle import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+HF, PR = 4, 56
+
+
+def lim(x):
+    return np.array(O.int_to_limbs(O.to_mont(x)), dtype=np.uint64)
+
+
+@pytest.fixture(scope="module")
+def consts():
+    py = O.p2_constants(2024, HF, PR)
+    return C.P2Constants([[lim(x) for x in r] for r in py[0]], [lim(x) for x in py[1]],
+                         [[lim(x) for x in r] for r in py[2]])
+
+
+def test_open_kernel_vs_oracle(gpu_ctx):
+    import torch
+
+    from plonky3_eon_amd.kzg import GpuKzgPcs, MatrixProverData, Domain
+
+    pcs = GpuKzgPcs(600, 12345, gpu_ctx)
+    for rows, w in [(1, 2), (2, 3), (257, 5), (600, 3)]:
+        cf = C.random_fr(rows + w, rows * w).reshape(rows, w, 4)
+        dev = torch.from_numpy(cf.view(np.int64)).to("cuda:0")
+        data = [MatrixProverData(Domain(1, 0), None, dev)]
+        z = 0xABCDEF123456789
+        r = pcs.open([(data, [[z, 0]])])[0]
+        for pi, pt in enumerate((z, 0)):
+            for j in range(w):
+                q, v = C.quotient_and_eval(cf[:, j], lim(pt))
+                np.testing.assert_array_equal(r.values[0][pi][j], v)
+                want = C.g1_msm(C.g1_srs(rows - 1, C.fr_from_u64(12345)), q) if rows > 1 else np.zeros(8, np.uint64)
+                np.testing.assert_array_equal(r.witnesses[0][pi][j], want)
+
+
+@pytest.mark.parametrize("log_n,vl", [(3, 1), (4, 2), (5, 8)])
+def test_prove_vs_oracle(gpu_ctx, consts, log_n, vl):
+    import torch
+
+    from plonky3_eon_amd.air import Poseidon2Air
+    from plonky3_eon_amd.kzg import GpuKzgPcs
+    from plonky3_eon_amd.prover import prove
+
+    n = 1 << log_n
+    alpha_srs = 12345
+    pcs = GpuKzgPcs(n, alpha_srs, gpu_ctx)
+    air = Poseidon2Air(consts.begin, consts.partial, consts.end, vl, gpu_ctx)
+    inputs = C.random_fr(log_n * 3 + vl, n * vl * 3).reshape(n * vl, 3, 4)
+    trace = air.generate_trace(torch.from_numpy(inputs.view(np.int64)).to("cuda:0"))
+    alpha, zeta = 0x1234567890ABCDEF1234, 0xFEDCBA0987654321
+    proof = prove(air, pcs, trace, alpha, zeta)
+
+    srs = C.g1_srs(n + 1, C.fr_from_u64(alpha_srs))
+    want = prove_oracle.prove(C.p2_generate_trace(inputs, vl, consts), srs, consts, vl, alpha, zeta)
+    np.testing.assert_array_equal(proof.trace_commit[0], want["trace_commit"])
+    np.testing.assert_array_equal(np.stack([c[0] for c in proof.quotient_commit]), want["quotient_commit"])
+    tr = proof.opened[0]
+    for p in range(2):
+        np.testing.assert_array_equal(tr.values[0][p], want["trace_open"][0][p])
+        np.testing.assert_array_equal(tr.witnesses[0][p], want["trace_open"][1][p])
+    qo = proof.opened[1]
+    for c in range(2):
+        np.testing.assert_array_equal(qo.values[c][0], want["quotient_open"][c][0][0])
+        np.testing.assert_array_equal(qo.witnesses[c][0], want["quotient_open"][c][1][0])

@@ -189,12 +189,124 @@ class MsmWorkload:
         return cpu_baseline_msm(self.bases_dev.cpu().numpy().view(np.uint64), self.scalars_host)
 
 
+def p2_constants_limbs(seed: int, hf: int = 4, pr: int = 56):
+    """Deterministic Poseidon2 round constants as Montgomery limbs (synthetic; the reference draws
+    them from SmallRng, poseidon2-air/src/constants.rs:37-46)."""
+    x = synthetic_fr(6 * hf + pr, 1, seed).reshape(-1, 4)
+    return x[:3 * hf].reshape(hf, 3, 4), x[3 * hf:3 * hf + pr], x[3 * hf + pr:].reshape(hf, 3, 4)
+
+
+def cpu_baseline_prove(log_n: int, vl: int, consts) -> dict:
+    """Projected reference-algorithm prove time on this host from full-size component samples
+    (a full CPU run is infeasible: get_evaluations_on_domain's Horner is ~4.5e13 mulmods)."""
+    from oracle import coracle as C
+
+    C.build()
+    n = 1 << log_n
+    w = 164 * vl
+    q = 2 * n
+    alpha = C.fr_from_u64(12345)
+    comp = {}
+    # trace coset_idft (Radix2Dit in KzgPcs): 16 sample columns, linear in width
+    x = synthetic_fr(n, 16, 11)
+    t0 = time.perf_counter(); C.idft_batch(x); dt = time.perf_counter() - t0
+    comp["trace idft"] = dt * w / 16
+    # one MSM of n points; prove runs w (trace) + 2 (quotient) + 2w + 2 (open) of them
+    pts = C.g1_srs(1 << 12, alpha)
+    pts = np.concatenate([pts] * (n >> 12))
+    s = synthetic_fr(n, 1, 12).reshape(n, 4)
+    t0 = time.perf_counter(); C.g1_msm(pts, s); dt = time.perf_counter() - t0
+    n_msm = 3 * w + 4
+    comp["msm x%d" % n_msm] = dt * n_msm
+    # get_evaluations_on_domain by Horner (kzg/src/pcs.rs:267-287): Q * w evaluations of degree n
+    coeffs = synthetic_fr(n, 1, 13)
+    t0 = time.perf_counter()
+    for k in range(16):
+        C.eval_poly_col(coeffs, 0, C.fr_from_u64(k + 7))
+    dt = (time.perf_counter() - t0) / 16
+    comp["lde horner (reference)"] = dt * q * w / C.num_threads()
+    # the same values by coset LDE (C restatement), 16 sample columns
+    t0 = time.perf_counter(); C.coset_lde_batch(x, 1, C.fr_from_u64(5)); dt = time.perf_counter() - t0
+    lde_fft = dt * w / 16
+    # quotient_values on 4096 sample rows
+    k = C.P2Constants(*consts)
+    lde_s = synthetic_fr(1 << 12, w, 14)
+    t0 = time.perf_counter(); C.p2_quotient_values(lde_s, 11, 1, vl, k, alpha); dt = time.perf_counter() - t0
+    comp["quotient_values"] = dt * q / 4096
+    total = sum(comp.values())
+    alt = total - comp["lde horner (reference)"] + lde_fft
+    return {
+        "value": round(total * 1e3, 1),
+        "unit": "ms",
+        "cores": C.num_threads(),
+        "kind": "port",
+        "projected": True,
+        "sample": "projected = sum of full-size component samples of the C restatement (trace idft 16/%d "
+                  "cols, one 2^%d MSM x %d, Horner LDE 16 points, quotient 4096 rows); reference "
+                  "algorithms incl. the Horner get_evaluations_on_domain" % (w, log_n, n_msm),
+        "components_ms": {k2: round(v * 1e3, 1) for k2, v in comp.items()},
+        "with_coset_lde_ms": round(alt * 1e3, 1),
+    }
+
+
+class ProveWorkload:
+    """configs[3]: eon-uni-stark prove of the vectorized Poseidon2-AIR (VECTOR_LEN 8, 2^(log_n+3)
+    permutations, log-trace-length log_n) with KzgPcs over BN254 (SRS max_degree 2^log_n,
+    alpha 12345); alpha / zeta fixed (transcript out of scope)."""
+
+    def __init__(self, args, ctx, dev, rank):
+        import torch
+
+        from plonky3_eon_amd.air import Poseidon2Air
+        from plonky3_eon_amd.kzg import GpuKzgPcs
+
+        self.args, self.ctx = args, ctx
+        self.log_n, self.vl = args.log_trace, args.vector_len
+        n = 1 << self.log_n
+        self.consts = p2_constants_limbs(99)
+        self.air = Poseidon2Air(*self.consts, self.vl, ctx)
+        self.pcs = GpuKzgPcs(n, 12345, ctx)
+        inputs = torch.from_numpy(synthetic_fr(n * self.vl, 3, 5 + rank).view(np.int64)).to(dev)
+        self.trace = self.air.generate_trace(inputs)
+        del inputs
+        self.alpha, self.zeta = 0x1234567890ABCDEF1234567 + rank, 0xFEDCBA09876543210FEDCBA + rank
+        self.timings = []
+
+    def step(self):
+        from plonky3_eon_amd.prover import prove
+
+        p = prove(self.air, self.pcs, self.trace, self.alpha, self.zeta)
+        self.timings.append(p.timings_ms)
+
+    def describe(self, world):
+        w = 164 * self.vl
+        return (f"configs[3]: eon-uni-stark prove, Poseidon2-AIR (VECTOR_LEN {self.vl}, width {w}) "
+                f"log-trace-length {self.log_n} (2^{self.log_n + (self.vl.bit_length() - 1)} permutations), "
+                f"KzgPcs over BN254 (per GPU)", world, 1 << self.log_n, f"instance-shard x{world}")
+
+    def throughput(self, world, ms):
+        n = 1 << self.log_n
+        st = {}
+        for k in self.timings[-self.args.steps:]:
+            for a, b in k.items():
+                st[a] = st.get(a, 0.0) + b / self.args.steps
+        return {
+            "permutations_per_s": round(world * n * self.vl / (ms * 1e-3), 1),
+            "stage_ms": {a: round(b, 2) for a, b in st.items()},
+        }, None
+
+    def cpu_baseline(self):
+        return cpu_baseline_prove(self.log_n, self.vl, self.consts)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["lde", "msm"], default="lde")
+    ap.add_argument("--steps", type=int, default=None, help="default: 3 (prove), 10 (lde, msm)")
+    ap.add_argument("--warmup", type=int, default=None, help="default: 1 (prove), 3 (lde, msm)")
+    ap.add_argument("--workload", choices=["prove", "lde", "msm"], default="prove")
+    ap.add_argument("--log-trace", type=int, default=17)
+    ap.add_argument("--vector-len", type=int, default=8)
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--width", type=int, default=64)
     ap.add_argument("--added-bits", type=int, default=1)
@@ -203,6 +315,10 @@ def main() -> int:
     ap.add_argument("--cpu-sample-cols", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 3 if args.workload == "prove" else 10
+    if args.warmup is None:
+        args.warmup = 1 if args.workload == "prove" else 3
 
     import torch
     import torch.distributed as dist
@@ -221,7 +337,7 @@ def main() -> int:
 
     ctx = Context(local_rank)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    wl = (LdeWorkload if args.workload == "lde" else MsmWorkload)(args, ctx, dev, rank)
+    wl = {"lde": LdeWorkload, "msm": MsmWorkload, "prove": ProveWorkload}[args.workload](args, ctx, dev, rank)
 
     for _ in range(args.warmup):
         wl.step()

@@ -193,6 +193,12 @@ int eon_p2air_quotient_values_dev(eon_ctx* ctx, const eon_p2air* air, const eon_
                                   uint32_t log_n, uint32_t log_qd, const eon_fr* alpha,
                                   eon_fr* out);
 
+/* out[i] = sum_{j<k} coeffs[j] * in[j * rows + i] (device in/out, host coeffs, 1 <= k <= 64):
+ * the combine step of the lane-sharded quotient -- every rank all-gathers the
+ * shards' partial quotients and weights shard g by alpha^(K_lane * (VECTOR_LEN - lane_end_g)). */
+int eon_fr_lincomb_dev(eon_ctx* ctx, const eon_fr* in, uint32_t k, uint64_t rows,
+                       const eon_fr* coeffs, eon_fr* out);
+
 /* ---- test SRS (setup, not prove time) --------------------------------------------------------
  * init_srs_unsafe's g1_powers (kzg/src/params.rs:123-139): out[i] = alpha^i * G1::generator(),
  * affine, i < n.  `alpha` is a host pointer; `out` host (eon_g1_srs_powers) or device (_dev). */

@@ -165,6 +165,21 @@ __global__ void __launch_bounds__(256) k_p2_quotient(const Fr* lde, uint64_t q, 
     }
 }
 
+constexpr uint32_t MAX_LINCOMB = 64;
+struct LincombCoeffs {
+    Fr c[MAX_LINCOMB];
+};
+
+// out[i] = sum_j c_j * in[j * rows + i]: combines per-shard partial quotients (mod-p sums are not
+// an RCCL reduction, so shards all-gather their partials and every rank combines them here).
+__global__ void k_fr_lincomb(const Fr* in, uint32_t k, uint64_t rows, LincombCoeffs c, Fr* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows) return;
+    Fr acc = mul(ldg(in + i), c.c[0]);
+    for (uint32_t j = 1; j < k; j++) acc = add(acc, mul(ldg(in + (uint64_t)j * rows + i), c.c[j]));
+    stg(out + i, acc);
+}
+
 // Z_H(x_i) = s^n * w_rate^j - 1 and its inverse for j < 2^rate (one thread each)
 __global__ void k_vanishing_table(Fr s_pow_n, Fr g_rate, uint32_t nr, Fr* zh, Fr* zh_inv) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -386,6 +401,30 @@ int eon_p2air_quotient_values_dev(eon_ctx* ctx, const eon_p2air* air, const eon_
                            ctx->stream, reinterpret_cast<const Fr*>(lde), q, a, al, lp, zh_inv,
                            (1u << log_qd) - 1,
                            reinterpret_cast<Fr*>(out));
+        ctx->prof.end(ctx->stream);
+        EON_HIP(hipGetLastError());
+        return Status::ok();
+    }();
+    return finish(ctx, s);
+}
+
+int eon_fr_lincomb_dev(eon_ctx* ctx, const eon_fr* in, uint32_t k, uint64_t rows,
+                       const eon_fr* coeffs, eon_fr* out) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    Status s = [&]() -> Status {
+        if (rows == 0) return Status::ok();
+        if (!in || !coeffs || !out) return Status::err(EON_E_ARG, "null argument");
+        if (k == 0 || k > MAX_LINCOMB) return Status::err(EON_E_SHAPE, "1 <= k <= 64 vectors");
+        LincombCoeffs c;
+        for (uint32_t j = 0; j < k; j++) {
+            c.c[j] = fr_from_abi(&coeffs[j]);
+            if (!fr_is_canonical(c.c[j])) return Status::err(EON_E_ARG, "coefficient is not a canonical Fr");
+        }
+        ctx->prof.begin("k_fr_lincomb", (k + 1) * rows * 32, ctx->stream);
+        hipLaunchKernelGGL(k_fr_lincomb, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, ctx->stream,
+                           reinterpret_cast<const Fr*>(in), k, rows, c, reinterpret_cast<Fr*>(out));
         ctx->prof.end(ctx->stream);
         EON_HIP(hipGetLastError());
         return Status::ok();

@@ -1,0 +1,132 @@
+"""Lane-sharded eon-uni-stark prove across ranks: one process per GPU, torch.distributed
+(backend "nccl" = RCCL over xGMI on the MI355X node; "gloo" for the CPU tests and for several
+ranks sharing one GPU).
+
+The sharding is SURVEY.md 8(e)'s preferred scheme for the vectorized Poseidon2-AIR.  The AIR
+evaluates its VECTOR_LEN lanes one after another (poseidon2-air/src/vectorized.rs:259-274), so
+lane v owns trace columns [164 v, 164 v + 164) and constraints [160 v, 160 v + 160).  Rank g
+owns a contiguous lane range [l0, l1):
+
+* trace commit  -- coset_idft + column MSMs of its own columns (kzg/src/pcs.rs:223-265); no
+                   exchange.
+* quotient      -- its LDE columns (pcs.rs:267-287) and the partial folder accumulator over its
+                   lanes (prover.rs:539-709).  The folder's running sum
+                   sum_k alpha^(K-1-k) C_k (folder.rs:81-85) splits by lane: lane v's block is
+                   weighted alpha^(K_lane (VL-1-v)).  A VectorizedPoseidon2Air over the rank's
+                   l1 - l0 lanes weights its local lane v' by alpha^(K_lane (l1-l0-1-v')), so the
+                   rank's partial times alpha^(K_lane (VL - l1)) is its exact share.  Every rank
+                   all-gathers the partials (Q x 32 B each), the only data-path collective, and
+                   combines them on device (eon_fr_lincomb_dev): mod-p sums are not an RCCL
+                   reduction.  inv_vanishing is applied per partial and distributes over the sum.
+* quotient commit and its opening -- 2 chunks x 1 column, replicated on every rank (identical
+                   inputs, identical results).
+* trace open    -- its columns at [zeta, zeta h] (pcs.rs:289-335); no exchange.
+* assembly      -- one all-gather of the per-column results (commitment, 2 values,
+                   2 witnesses): 32 u64 per column.
+
+Every rank ends with the same Proof, equal to the single-GPU prove's.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .field import FR_MODULUS, fr_to_abi
+
+
+@dataclass(frozen=True)
+class Shard:
+    """This rank's lanes of a VectorizedPoseidon2Air with `vector_len` lanes."""
+
+    rank: int
+    world: int
+    vector_len: int
+    group: object = None
+
+    @property
+    def lanes(self):
+        return lane_range(self.rank, self.world, self.vector_len)
+
+    def columns(self, cols_per_lane: int):
+        l0, l1 = self.lanes
+        return l0 * cols_per_lane, l1 * cols_per_lane
+
+
+def lane_range(rank: int, world: int, vector_len: int):
+    """Contiguous lane block of `rank`; every rank gets vector_len / world lanes."""
+    if world < 1 or not 0 <= rank < world:
+        raise _lib.EonError(_lib.EON_E_ARG, f"rank {rank} outside world {world}")
+    if vector_len % world:
+        raise _lib.EonError(_lib.EON_E_SHAPE, f"VECTOR_LEN {vector_len} does not split over {world} ranks")
+    per = vector_len // world
+    return rank * per, (rank + 1) * per
+
+
+def lane_weights(alpha: int, vector_len: int, world: int, constraints_per_lane: int):
+    """alpha^(K_lane (VL - l1_g)) for every rank g: the factor turning rank g's local folder
+    accumulator into its share of the full one."""
+    a = alpha % FR_MODULUS
+    return [pow(a, constraints_per_lane * (vector_len - lane_range(g, world, vector_len)[1]), FR_MODULUS)
+            for g in range(world)]
+
+
+def all_gather_rows(t, group=None):
+    """Stack `t` from every rank in rank order -> (world, *t.shape), on t's device.
+
+    nccl (RCCL) gathers device buffers directly; other backends (gloo) stage through host
+    memory, which is how the CPU tests and a several-ranks-per-GPU run exchange."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    t = t.contiguous()
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=group)
+        return out
+    h = t.cpu()
+    parts = [torch.empty_like(h) for _ in range(world)]
+    dist.all_gather(parts, h, group=group)
+    return torch.stack(parts).to(t.device)
+
+
+def combine_partials(ctx, parts, weights):
+    """sum_g weights[g] * parts[g] over Fr on device: parts (G, Q, 4) int64 -> (Q, 4)."""
+    import torch
+
+    g, q = int(parts.shape[0]), int(parts.shape[1])
+    if len(weights) != g:
+        raise _lib.EonError(_lib.EON_E_SHAPE, "one weight per partial")
+    out = torch.empty((q, 4), dtype=torch.int64, device=parts.device)
+    coeffs = (_lib.eon_fr * g)(*[fr_to_abi(w) for w in weights])
+    p = parts.contiguous()
+    ctx.set_stream(torch.cuda.current_stream(p.device).cuda_stream)
+    ctx.check(ctx.lib.eon_fr_lincomb_dev(ctx.handle, ctypes.c_void_p(p.data_ptr()), g, q, coeffs,
+                                         ctypes.c_void_p(out.data_ptr())))
+    return out
+
+
+# per-column record exchanged at assembly: commitment (8) | value at zeta (4) | value at zeta h (4)
+# | witness at zeta (8) | witness at zeta h (8)
+COLUMN_RECORD = 32
+
+
+def pack_columns(commit, values, witnesses) -> np.ndarray:
+    return np.concatenate([commit, values[0], values[1], witnesses[0], witnesses[1]], axis=1).astype(np.uint64)
+
+
+def unpack_columns(rec: np.ndarray):
+    rec = rec.reshape(-1, COLUMN_RECORD)
+    return rec[:, 0:8], [rec[:, 8:12], rec[:, 12:16]], [rec[:, 16:24], rec[:, 24:32]]
+
+
+def gather_columns(local: np.ndarray, device, group=None) -> np.ndarray:
+    """All-gather the (w_local, 32) per-column records -> (W, 32) in global column order."""
+    import torch
+
+    t = torch.from_numpy(np.ascontiguousarray(local).view(np.int64)).to(device)
+    return all_gather_rows(t, group).cpu().numpy().view(np.uint64).reshape(-1, COLUMN_RECORD)

@@ -40,9 +40,16 @@ def log_quotient_degree(max_constraint_degree: int) -> int:
 
 
 def prove(air, pcs: GpuKzgPcs, trace, alpha: int, zeta: int, max_constraint_degree: int = 3,
-          sync=None) -> Proof:
-    """trace: (N, width, 4) device tensor.  The Poseidon2-AIR's constraints have degree 3."""
+          shard=None) -> Proof:
+    """trace: (N, width, 4) device tensor.  The Poseidon2-AIR's constraints have degree 3.
+
+    shard: a distributed.Shard when the prove is split by vector lane over several ranks; `air`
+    and `trace` are then this rank's lanes (a VectorizedPoseidon2Air of shard.lanes' length and
+    its trace columns), and every rank returns the full proof (plonky3_eon_amd/distributed.py).
+    """
     import torch
+
+    from . import distributed as D
 
     def tick():
         torch.cuda.synchronize(trace.device)
@@ -54,6 +61,12 @@ def prove(air, pcs: GpuKzgPcs, trace, alpha: int, zeta: int, max_constraint_degr
     log_qd = log_quotient_degree(max_constraint_degree)
     num_chunks = 1 << log_qd
     trace_domain = pcs.natural_domain_for_degree(n)
+    if shard is not None and shard.world > 1:
+        l0, l1 = shard.lanes
+        if air.vector_len != l1 - l0:
+            raise ValueError(f"rank {shard.rank} owns lanes [{l0}, {l1}) but the AIR has {air.vector_len}")
+    else:
+        shard = None
 
     t0 = tick()
     trace_commit, trace_data = pcs.commit([(trace_domain, trace)])  # prover.rs:186-187
@@ -64,19 +77,35 @@ def prove(air, pcs: GpuKzgPcs, trace, alpha: int, zeta: int, max_constraint_degr
     qv = air.quotient_values(lde, log_n, log_qd, alpha)  # prover.rs:328-342
     del lde
     t3 = tick()
+    if shard is not None:
+        parts = D.all_gather_rows(qv, shard.group)
+        weights = D.lane_weights(alpha, shard.vector_len, shard.world, air.constraints_per_perm)
+        qv = D.combine_partials(pcs.ctx, parts, weights)
+        del parts
+    t3x = tick()
     quotient_commit, quotient_data = pcs.commit_quotient(quotient_domain, qv, num_chunks)  # :371-372
     t4 = tick()
     zeta_next = trace_domain.next_point(zeta)  # prover.rs:416-419
     opened = pcs.open([(trace_data, [[zeta, zeta_next]]),
                        (quotient_data, [[zeta]] * num_chunks)])  # prover.rs:424-442
     t5 = tick()
+    if shard is not None:
+        tr = opened[0]
+        rec = D.pack_columns(trace_commit[0], tr.values[0], tr.witnesses[0])
+        commit_all, values_all, wits_all = D.unpack_columns(D.gather_columns(rec, trace.device, shard.group))
+        trace_commit = [commit_all]
+        tr.values[0], tr.witnesses[0] = values_all, wits_all
+    t6 = tick()
     t.update({
         "commit to trace data": (t1 - t0) * 1e3,
         "trace LDE (get_evaluations_on_domain)": (t2 - t1) * 1e3,
         "quotient_values": (t3 - t2) * 1e3,
-        "commit to quotient poly chunks": (t4 - t3) * 1e3,
+        "commit to quotient poly chunks": (t4 - t3x) * 1e3,
         "open": (t5 - t4) * 1e3,
     })
+    if shard is not None:
+        t["exchange partial quotients"] = (t3x - t3) * 1e3
+        t["assemble columns"] = (t6 - t5) * 1e3
     return Proof(trace_commit, quotient_commit, opened, log_n, t)
 
 

@@ -1,0 +1,150 @@
+"""One rank of the lane-sharded prove tests (launched by test_distributed_*.py as a subprocess,
+RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment, backend gloo).
+
+  cpu  -- the sharding arithmetic and exchange with the C restatement oracle as the per-rank
+          compute: per-lane trace slices, partial quotients, all_gather_rows, lane weights and
+          gather_columns must reproduce the single-process oracle quotient.
+  gpu  -- the product path (plonky3_eon_amd.prover.prove with a Shard) on cuda:0 for every rank;
+          rank 0 also runs the unsharded prove and every proof field must match bit for bit.
+
+Writes {"ok": true} or {"ok": false, "why": ...} as JSON to argv[2].
+"""
+
+import json
+import os
+import sys
+import traceback
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+
+from oracle import coracle as C  # noqa: E402
+from oracle import pyoracle as O  # noqa: E402
+
+HF, PR, CPP = 4, 56, 164
+
+
+def lim(x):
+    return np.array(O.int_to_limbs(O.to_mont(x % O.P)), dtype=np.uint64)
+
+
+def val(limbs):
+    return O.from_mont(O.limbs_to_int([int(x) for x in limbs]))
+
+
+def consts():
+    py = O.p2_constants(2024, HF, PR)
+    return C.P2Constants([[lim(x) for x in r] for r in py[0]], [lim(x) for x in py[1]],
+                         [[lim(x) for x in r] for r in py[2]])
+
+
+def lane_inputs(inputs, n, vl, l0, l1):
+    """Permutation j sits at row j / VECTOR_LEN, lane j % VECTOR_LEN (generation.rs:14-72)."""
+    return np.ascontiguousarray(inputs.reshape(n, vl, 3, 4)[:, l0:l1]).reshape(-1, 3, 4)
+
+
+def run_cpu(rank, world, group):
+    import torch
+
+    from plonky3_eon_amd import distributed as D
+
+    log_n, vl, log_qd = 3, 4, 1
+    n = 1 << log_n
+    k = consts()
+    alpha = 0x1234567890ABCDEF1234
+    inputs = C.random_fr(77, n * vl * 3).reshape(n * vl, 3, 4)
+    full = C.p2_generate_trace(inputs, vl, k)
+    l0, l1 = D.lane_range(rank, world, vl)
+    c0, c1 = D.Shard(rank, world, vl).columns(CPP)
+    local = C.p2_generate_trace(lane_inputs(inputs, n, vl, l0, l1), l1 - l0, k)
+    if not np.array_equal(local, full[:, c0:c1]):
+        return "lane trace != column slice of the full trace"
+
+    def quotient(tr, lanes):
+        lde = C.kzg_evaluations_on_domain(C.idft_batch(tr), log_n + log_qd, lim(O.GENERATOR))
+        return C.p2_quotient_values(lde, log_n, log_qd, lanes, k, lim(alpha))
+
+    part = quotient(local, l1 - l0)
+    parts = D.all_gather_rows(torch.from_numpy(part.view(np.int64)), group).numpy().view(np.uint64)
+    w = D.lane_weights(alpha, vl, world, 12 * HF + 2 * PR)
+    got = [sum(w[g] * val(parts[g, i]) for g in range(world)) % O.P for i in range(parts.shape[1])]
+    want = quotient(full, vl)
+    if got != [val(x) for x in want]:
+        return "combined partial quotients != full quotient"
+    # assembly order: each rank's records land at its global columns
+    rec = np.zeros((c1 - c0, D.COLUMN_RECORD), dtype=np.uint64)
+    rec[:, 0] = np.arange(c0, c1)
+    rec[:, 31] = rank
+    allrec = D.gather_columns(rec, "cpu", group)
+    if not (np.array_equal(allrec[:, 0], np.arange(vl * CPP))
+            and np.array_equal(allrec[:, 31], np.repeat(np.arange(world), (vl // world) * CPP))):
+        return "gather_columns order"
+    return None
+
+
+def run_gpu(rank, world, group):
+    import torch
+
+    from plonky3_eon_amd import Context
+    from plonky3_eon_amd import distributed as D
+    from plonky3_eon_amd.air import Poseidon2Air
+    from plonky3_eon_amd.kzg import GpuKzgPcs
+    from plonky3_eon_amd.prover import prove
+
+    log_n, vl = int(os.environ.get("EON_T_LOG_N", "5")), int(os.environ.get("EON_T_VL", "4"))
+    n = 1 << log_n
+    k = consts()
+    ctx = Context(0)
+    dev = torch.device("cuda:0")
+    inputs = C.random_fr(99, n * vl * 3).reshape(n * vl, 3, 4)
+    alpha, zeta = 0x1234567890ABCDEF1234, 0xFEDCBA0987654321
+    pcs = GpuKzgPcs(n, 12345, ctx)
+    shard = D.Shard(rank, world, vl, group)
+    l0, l1 = shard.lanes
+    air = Poseidon2Air(k.begin, k.partial, k.end, l1 - l0, ctx)
+    trace = air.generate_trace(torch.from_numpy(lane_inputs(inputs, n, vl, l0, l1).view(np.int64)).to(dev))
+    p = prove(air, pcs, trace, alpha, zeta, shard=shard)
+    if rank != 0:
+        return None
+    full_air = Poseidon2Air(k.begin, k.partial, k.end, vl, ctx)
+    full = full_air.generate_trace(torch.from_numpy(inputs.view(np.int64)).to(dev))
+    q = prove(full_air, pcs, full, alpha, zeta)
+    checks = [("trace_commit", p.trace_commit[0], q.trace_commit[0])]
+    checks += [(f"quotient_commit[{c}]", p.quotient_commit[c], q.quotient_commit[c]) for c in range(2)]
+    for r in range(2):
+        for m in range(len(q.opened[r].values)):
+            for pt in range(len(q.opened[r].values[m])):
+                checks.append((f"opened[{r}].values[{m}][{pt}]", p.opened[r].values[m][pt], q.opened[r].values[m][pt]))
+                checks.append((f"opened[{r}].witnesses[{m}][{pt}]", p.opened[r].witnesses[m][pt],
+                               q.opened[r].witnesses[m][pt]))
+    for name, a, b in checks:
+        if not np.array_equal(np.asarray(a), np.asarray(b)):
+            return f"{name} differs from the unsharded prove"
+    return None
+
+
+def main():
+    import torch.distributed as dist
+
+    mode, out = sys.argv[1], sys.argv[2]
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        why = (run_cpu if mode == "cpu" else run_gpu)(rank, world, None)
+    except Exception:
+        why = traceback.format_exc()
+    finally:
+        try:
+            dist.barrier()
+        except Exception:
+            pass
+        dist.destroy_process_group()
+    Path(out).write_text(json.dumps({"ok": why is None, "why": why}))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

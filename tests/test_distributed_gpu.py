@@ -1,0 +1,14 @@
+"""Lane-sharded prove through the product path (HIP kernels) with two gloo ranks sharing cuda:0:
+every rank's proof must equal the unsharded prove bit for bit."""
+
+import pytest
+
+from _launch import run_world
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("world,log_n,vl", [(2, 5, 4), (4, 4, 8)])
+def test_sharded_prove_matches_single(world, log_n, vl):
+    res = run_world("gpu", world, timeout=900, extra_env={"EON_T_LOG_N": str(log_n), "EON_T_VL": str(vl)})
+    assert all(r["ok"] for r in res), [r["why"] for r in res]

@@ -161,4 +161,41 @@ EON_HD G1Affine xyzz_to_affine(const G1Xyzz& p) {
     return xyzz_to_affine_with_inv(p, inverse(p.ZZZ));
 }
 
+// Pinned point loads / vector stores (see ld_pinned in field.h)
+__device__ __forceinline__ void pin(G1Xyzz& a) {
+    pin(a.X);
+    pin(a.Y);
+    pin(a.ZZ);
+    pin(a.ZZZ);
+}
+
+__device__ __forceinline__ G1Xyzz ld_xyzz(const G1Xyzz* p) {
+    G1Xyzz r;
+    r.X = ld_pinned(&p->X);
+    r.Y = ld_pinned(&p->Y);
+    r.ZZ = ld_pinned(&p->ZZ);
+    r.ZZZ = ld_pinned(&p->ZZZ);
+    return r;
+}
+
+__device__ __forceinline__ void st_xyzz(G1Xyzz* p, const G1Xyzz& a) {
+    st_vec(&p->X, a.X);
+    st_vec(&p->Y, a.Y);
+    st_vec(&p->ZZ, a.ZZ);
+    st_vec(&p->ZZZ, a.ZZZ);
+}
+
+__device__ __forceinline__ G1Affine ld_affine(const G1Affine* p) {
+    G1Affine r;
+    r.x = ld_pinned(&p->x);
+    r.y = ld_pinned(&p->y);
+    return r;
+}
+
+__device__ __forceinline__ void st_affine(G1Affine* p, const G1Affine& a) {
+    st_vec(&p->x, a.x);
+    st_vec(&p->y, a.y);
+}
+
 }  // namespace eon
+

@@ -173,15 +173,15 @@ struct Acc96 {
 
 __device__ __forceinline__ void mac(Acc96& acc, uint32_t x, uint32_t y) {
     uint64_t cc;
-    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc.lo), "=s"(cc) : "v"(x), "v"(y));
-    asm volatile("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(acc.ov), "=s"(cc) : "s"(cc));
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc.lo), "=s"(cc) : "v"(x), "v"(y));
+    asm("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(acc.ov), "=s"(cc) : "s"(cc));
 }
 
 // Same, with a wave-uniform (modulus-limb) multiplier held in an SGPR.
 __device__ __forceinline__ void mac_s(Acc96& acc, uint32_t x, uint32_t y) {
     uint64_t cc;
-    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc.lo), "=s"(cc) : "v"(x), "s"(y));
-    asm volatile("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(acc.ov), "=s"(cc) : "s"(cc));
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc.lo), "=s"(cc) : "v"(x), "s"(y));
+    asm("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(acc.ov), "=s"(cc) : "s"(cc));
 }
 
 template <class M>
@@ -291,4 +291,33 @@ EON_HD uint32_t reverse_bits_len(uint32_t x, uint32_t bits) {
     return bits == 0 ? 0u : (__builtin_bitreverse32(x) >> (32 - bits));
 }
 
+// Register-pinned element loads.  A field element read through a pointer and then used by
+// inlined multiplies can be "rematerialised" by the compiler -- re-loaded from memory at every use
+// instead of kept in VGPRs -- which turned one 128-byte point read into ~360 L2 requests in the
+// MSM combine kernels.  The empty asm makes every limb an opaque register value.
+template <class M>
+__device__ __forceinline__ void pin(Fe<M>& x) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) asm volatile("" : "+v"(x.v[i]));
+}
+
+template <class M>
+__device__ __forceinline__ Fe<M> ld_pinned(const Fe<M>* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 a = q[0], b = q[1];
+    Fe<M> x;
+    x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
+    x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+    pin(x);
+    return x;
+}
+
+template <class M>
+__device__ __forceinline__ void st_vec(Fe<M>* p, const Fe<M>& x) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+    q[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+}
+
 }  // namespace eon
+

@@ -28,6 +28,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "context.h"
@@ -73,7 +75,8 @@ __global__ void k_msm_digits(const Fr* scalars, uint64_t n, uint64_t ld, uint32_
     if (t >= n * cols) return;
     const uint32_t col = (uint32_t)(t % cols);
     const uint64_t i = t / cols;
-    const Fr s = to_canonical(scalars[i * ld + col]);
+    Fr s = to_canonical(ld_pinned(scalars + i * ld + col));
+    pin(s);
     const uint32_t B = 1u << (c - 1);
     const uint32_t sentinel = (precomputed ? cols : cols * windows) * B;
     uint32_t carry = 0;
@@ -109,12 +112,12 @@ __global__ void k_window_horner(const G1Xyzz* gs, uint32_t cols, uint32_t W, uin
     const uint32_t col = blockIdx.x * blockDim.x + threadIdx.x;
     if (col >= cols) return;
     const G1Xyzz* g = gs + (uint64_t)col * W;
-    G1Xyzz acc = g[W - 1];
+    G1Xyzz acc = ld_xyzz(g + W - 1);
     for (int w = (int)W - 2; w >= 0; w--) {
         for (uint32_t k = 0; k < c; k++) acc = xyzz_dbl(acc);
-        acc = xyzz_add(acc, g[w]);
+        acc = xyzz_add(acc, ld_xyzz(g + w));
     }
-    out[col] = acc;
+    st_xyzz(out + col, acc);
 }
 
 // start[b] = index of the first sorted pair with key >= b, for b in [0, nb]
@@ -132,17 +135,6 @@ __global__ void k_piece_owner(const uint32_t* piece_off, uint32_t nb, uint32_t* 
     for (uint32_t p = piece_off[b]; p < piece_off[b + 1]; p++) owner[p] = b;
 }
 
-__device__ __forceinline__ G1Affine load_affine(const G1Affine* t, uint32_t idx) {
-    const uint4* q = reinterpret_cast<const uint4*>(t + idx);
-    G1Affine a;
-    uint4 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3];
-    a.x.v[0] = v0.x; a.x.v[1] = v0.y; a.x.v[2] = v0.z; a.x.v[3] = v0.w;
-    a.x.v[4] = v1.x; a.x.v[5] = v1.y; a.x.v[6] = v1.z; a.x.v[7] = v1.w;
-    a.y.v[0] = v2.x; a.y.v[1] = v2.y; a.y.v[2] = v2.z; a.y.v[3] = v2.w;
-    a.y.v[4] = v3.x; a.y.v[5] = v3.y; a.y.v[6] = v3.z; a.y.v[7] = v3.w;
-    return a;
-}
-
 __global__ void k_piece_sum(const uint32_t* vals, const uint32_t* start, const uint32_t* piece_off,
                             const uint32_t* owner, uint32_t n_pieces, const G1Affine* pts,
                             G1Xyzz* piece_sums) {
@@ -155,11 +147,11 @@ __global__ void k_piece_sum(const uint32_t* vals, const uint32_t* start, const u
     G1Xyzz acc = xyzz_inf();
     for (uint32_t e = e0; e < e1; e++) {
         const uint32_t v = vals[e];
-        G1Affine a = load_affine(pts, v & 0x7fffffffu);
+        G1Affine a = ld_affine(pts + (v & 0x7fffffffu));
         if (v >> 31) a = affine_neg(a);
         acc = xyzz_add_affine(acc, a);
     }
-    piece_sums[p] = acc;
+    st_xyzz(piece_sums + p, acc);
 }
 
 // One combine level: new partial p of bucket b sums old partials
@@ -173,9 +165,9 @@ __global__ void k_partial_combine(const uint32_t* off_old, const uint32_t* off_n
     const uint32_t j = p - off_new[b];
     const uint32_t e0 = off_old[b] + j * PIECE;
     const uint32_t e1 = min(e0 + PIECE, off_old[b + 1]);
-    G1Xyzz acc = in[e0];
-    for (uint32_t e = e0 + 1; e < e1; e++) acc = xyzz_add(acc, in[e]);
-    out[p] = acc;
+    G1Xyzz acc = ld_xyzz(in + e0);
+    for (uint32_t e = e0 + 1; e < e1; e++) acc = xyzz_add(acc, ld_xyzz(in + e));
+    st_xyzz(out + p, acc);
 }
 
 // count[b] = ceil((off[b+1] - off[b]) / PIECE) (0 for the terminator)
@@ -190,7 +182,7 @@ __global__ void k_bucket_final(const uint32_t* off, uint32_t nb, const G1Xyzz* p
                                G1Xyzz* bucket_sums) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
-    bucket_sums[b] = off[b + 1] > off[b] ? partials[off[b]] : xyzz_inf();
+    st_xyzz(bucket_sums + b, off[b + 1] > off[b] ? ld_xyzz(partials + off[b]) : xyzz_inf());
 }
 
 // Segment s of group g covers buckets [lo, lo + SEG) (bucket b holds digit b + 1):
@@ -205,11 +197,11 @@ __global__ void k_segment_sum(const G1Xyzz* bucket_sums, uint32_t B, uint32_t gr
     const G1Xyzz* sb = bucket_sums + (uint64_t)g * B + lo;
     G1Xyzz run = xyzz_inf(), acc = xyzz_inf();
     for (int k = SEG - 1; k >= 0; k--) {
-        run = xyzz_add(run, sb[k]);
+        run = xyzz_add(run, ld_xyzz(sb + k));
         acc = xyzz_add(acc, run);
     }
     if (lo) acc = xyzz_add(acc, xyzz_mul_small(run, lo));
-    seg_out[t] = acc;
+    st_xyzz(seg_out + t, acc);
 }
 
 // out[g * gridDim.x + blk] = sum of in[g * n + blk * TREE .. + TREE)
@@ -217,13 +209,19 @@ __global__ void __launch_bounds__(TREE) k_tree_sum(const G1Xyzz* in, uint32_t n,
     __shared__ G1Xyzz sh[TREE];
     const uint32_t g = blockIdx.y;
     const uint32_t i = blockIdx.x * TREE + threadIdx.x;
-    sh[threadIdx.x] = i < n ? in[(uint64_t)g * n + i] : xyzz_inf();
+    G1Xyzz acc = i < n ? ld_xyzz(in + (uint64_t)g * n + i) : xyzz_inf();
+    sh[threadIdx.x] = acc;
     __syncthreads();
     for (uint32_t w = TREE / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + w]);
+        if (threadIdx.x < w) {
+            G1Xyzz o = sh[threadIdx.x + w];
+            pin(o);
+            acc = xyzz_add(acc, o);
+            sh[threadIdx.x] = acc;
+        }
         __syncthreads();
     }
-    if (threadIdx.x == 0) out[(uint64_t)g * gridDim.x + blockIdx.x] = sh[0];
+    if (threadIdx.x == 0) st_xyzz(out + (uint64_t)g * gridDim.x + blockIdx.x, acc);
 }
 
 // --- fixed-base precomputation ------------------------------------------------------------
@@ -232,36 +230,36 @@ __global__ void k_precompute_windows(const G1Affine* pts, uint64_t n, uint32_t c
                                      G1Xyzz* tmp) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    G1Xyzz p = xyzz_from_affine(pts[i]);
+    G1Xyzz p = xyzz_from_affine(ld_affine(pts + i));
     for (uint32_t w = 0; w < W; w++) {
-        tmp[i * W + w] = p;
+        st_xyzz(tmp + i * W + w, p);
         if (w + 1 < W)
             for (uint32_t k = 0; k < c; k++) p = xyzz_dbl(p);
     }
 }
 
-// XYZZ -> affine with Montgomery's batch inversion over chunks of BATCH consecutive points
+// XYZZ -> affine with Montgomery's batch inversion over chunks of BATCH consecutive points; the
+// prefix products are parked in the outputs' x coordinates (no per-lane array, no scratch)
 __global__ void k_batch_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t i0 = t * BATCH;
     if (i0 >= m) return;
     const uint64_t i1 = min(i0 + BATCH, m);
-    Fq prefix[BATCH];
     Fq acc = Fq::one();
     for (uint64_t i = i0; i < i1; i++) {
-        prefix[i - i0] = acc;
-        if (!is_inf(in[i])) acc = mul(acc, in[i].ZZZ);
+        st_vec(&out[i].x, acc);
+        if (!ld_pinned(&in[i].ZZ).is_zero()) acc = mul(acc, ld_pinned(&in[i].ZZZ));
     }
     Fq inv = inverse(acc);
     for (uint64_t i = i1; i-- > i0;) {
-        const G1Xyzz p = in[i];
+        const G1Xyzz p = ld_xyzz(in + i);
         if (is_inf(p)) {
-            out[i] = xyzz_to_affine_with_inv(p, Fq::zero());
+            st_affine(out + i, xyzz_to_affine_with_inv(p, Fq::zero()));
             continue;
         }
-        const Fq inv_zzz = mul(inv, prefix[i - i0]);
+        const Fq inv_zzz = mul(inv, ld_pinned(&out[i].x));
         inv = mul(inv, p.ZZZ);
-        out[i] = xyzz_to_affine_with_inv(p, inv_zzz);
+        st_affine(out + i, xyzz_to_affine_with_inv(p, inv_zzz));
     }
 }
 
@@ -435,6 +433,10 @@ static Status msm_batch(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars,
     EON_HIP(hipStreamSynchronize(st));
     uint32_t n_pieces = counts[0];
     const uint32_t n_pairs = counts[1];
+    static const bool debug = getenv("EON_MSM_DEBUG") != nullptr;
+    if (debug)
+        fprintf(stderr, "msm_batch n=%llu cols=%u c=%u W=%u nb=%u E=%llu pairs=%u pieces=%u\n",
+                (unsigned long long)n, cols, c, W, nb, (unsigned long long)E, n_pairs, n_pieces);
     const G1Affine* pts = b->precomputed ? b->table.as<G1Affine>() : b->points.as<G1Affine>();
     // algorithmic bytes: every nonzero digit reads its 4-byte reference and a 64-byte affine
     // base; every piece writes one 128-byte XYZZ partial
@@ -460,6 +462,7 @@ static Status msm_batch(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars,
         uint32_t n_new = 0;
         EON_HIP(hipMemcpyAsync(&n_new, off_nxt + nb, 4, hipMemcpyDeviceToHost, st));
         EON_HIP(hipStreamSynchronize(st));
+        if (debug) fprintf(stderr, "  level %d: %u -> %u partials\n", level, n_pieces, n_new);
         if (n_new == n_pieces) break;  // every bucket already holds at most one partial
         hipLaunchKernelGGL(k_piece_owner, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_nxt, nb,
                            wk.owner.as<uint32_t>());

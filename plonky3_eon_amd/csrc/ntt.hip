@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(512) k_ntt_pass(PassArgs a) {
             }
             if (present) {
                 x = gload(a.src + r * width + col);
-                if (a.load_scale) x = mul(x, gload(a.load_scale + r));
+                if (a.load_scale) x = mul(x, ld_pinned(a.load_scale + r));
                 if (a.has_load_const) x = mul(x, a.load_const);
             }
         }
@@ -135,14 +135,18 @@ __global__ void __launch_bounds__(512) k_ntt_pass(PassArgs a) {
             Fr u, v;
             if (!DIF) {
                 // DitButterfly (dft/src/butterflies.rs:177-185): (x + w*y, x - w*y)
-                const Fr t = unit ? y : mul(y, twl[half + r]);
+                Fr w = twl[half + r];
+                pin(w);
+                const Fr t = unit ? y : mul(y, w);
                 u = add(x, t);
                 v = sub(x, t);
             } else {
                 // DIF butterfly: (x + y, (x - y) * w)
                 u = add(x, y);
                 const Fr d = sub(x, y);
-                v = unit ? d : mul(d, twl[half + r]);
+                Fr w = twl[half + r];
+                pin(w);
+                v = unit ? d : mul(d, w);
             }
             lds_put(lo, hi, i0, u);
             lds_put(lo, hi, i1, v);
@@ -157,7 +161,7 @@ __global__ void __launch_bounds__(512) k_ntt_pass(PassArgs a) {
         const uint64_t col = col0 + c;
         if (col < width) {
             Fr x = lds_get(lo, hi, e);
-            if (a.store_scale) x = mul(x, gload(a.store_scale + p));
+            if (a.store_scale) x = mul(x, ld_pinned(a.store_scale + p));
             gstore(a.dst + p * width + col, x);
         }
     }

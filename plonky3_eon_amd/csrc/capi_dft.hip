@@ -239,6 +239,14 @@ int eon_ctx_create(int device_ordinal, eon_ctx** out) {
         return EON_E_DEVICE;
     }
     c->stream = c->own_stream;
+    // MSM side stream: non-blocking so that it overlaps null-stream work (ordered by events)
+    if (hipStreamCreateWithFlags(&c->msm_side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->msm_ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->msm_ev[1], hipEventDisableTiming) != hipSuccess) {
+        (void)hipStreamDestroy(c->own_stream);
+        delete c;
+        return EON_E_DEVICE;
+    }
     if (const char* e = getenv("EON_NTT_MAX_STAGES")) c->ntt_max_stages = (uint32_t)atoi(e);
     if (const char* e = getenv("EON_NTT_TPB")) c->ntt_tpb = (uint32_t)atoi(e);
     if (const char* e = getenv("EON_NTT_LOG_CB")) c->ntt_log_cb = atoi(e) > 3 ? 3 : atoi(e);
@@ -250,6 +258,7 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamSynchronize(ctx->msm_side);
     ctx->tw_fwd.release();
     ctx->tw_inv.release();
     for (auto& kv : ctx->tables) kv.second.release();
@@ -259,12 +268,16 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     }
     for (auto e : ctx->prof.pool) (void)hipEventDestroy(e);
     ctx->msm.release();
+    ctx->msm_b.release();
     ctx->sel_tab.release();
     ctx->kzg_tmp.release();
     ctx->scratch.release();
     ctx->stage_in.release();
     ctx->stage_out.release();
     (void)hipStreamDestroy(ctx->own_stream);
+    (void)hipStreamDestroy(ctx->msm_side);
+    (void)hipEventDestroy(ctx->msm_ev[0]);
+    (void)hipEventDestroy(ctx->msm_ev[1]);
     delete ctx;
 }
 

@@ -49,10 +49,13 @@ struct Status {
 // device workspace of one MSM pipeline run (msm.hip); grows on demand, reused across calls
 struct MsmWork {
     DevBuf keys, vals, keys2, vals2, start, count, piece_off, off2, owner, piece_sums,
-        piece_sums2, bucket_sums, red_a, red_b, temp, results;
+        piece_sums2, bucket_sums, red_a, red_b, temp, results, levels;
+    uint32_t* host_counts = nullptr;  // pinned read-back slots
     void release() {
+        if (host_counts) (void)hipHostFree(host_counts);
+        host_counts = nullptr;
         for (DevBuf* b : {&keys, &vals, &keys2, &vals2, &start, &count, &piece_off, &off2, &owner,
-                          &piece_sums, &piece_sums2, &bucket_sums, &red_a, &red_b, &temp,
+                          &piece_sums, &piece_sums2, &bucket_sums, &red_a, &red_b, &temp, &levels,
                           &results})
             b->release();
     }
@@ -97,8 +100,10 @@ struct eon_ctx {
     // per-launch HIP-event timing (eon_ctx_profile_*)
     eon::Profiler prof;
 
-    // MSM pipeline workspace
-    eon::MsmWork msm;
+    // MSM pipeline workspaces: batches alternate between `stream` (msm) and msm_side (msm_b)
+    eon::MsmWork msm, msm_b;
+    hipStream_t msm_side = nullptr;
+    hipEvent_t msm_ev[2] = {nullptr, nullptr};
 
     // quotient: vanishing-polynomial table; KZG opening scan workspace
     eon::DevBuf sel_tab, kzg_tmp;

@@ -9,13 +9,16 @@
 //                       (bucket key, point reference | sign) pair per nonzero digit.
 //   2. radix sort       hipCUB DeviceRadixSort on the c-bit keys (zero digits sort last).
 //   3. k_bucket_start   bucket boundaries in the sorted pairs.
-//   4. pieces           every bucket is cut into pieces of <= PIECE entries (load balance under
-//                       skewed scalars); exclusive scan of piece counts.
-//   5. k_piece_sum      one thread per piece: XYZZ mixed additions of affine bases.
+//   4. pieces           a piece is the part of a bucket inside one CHUNK-aligned run of sorted
+//                       pairs; exclusive scan of the per-bucket piece counts.
+//   5. k_piece_sum      one thread per CHUNK of sorted pairs (every lane does the same number of
+//                       XYZZ mixed additions of affine bases), flushing a partial per piece.
 //   6. k_partial_combine levels of <= PIECE-way sums until each bucket holds one partial
 //                       (log-depth under any skew, e.g. all-equal scalars), k_bucket_final.
-//   7. k_segment_sum /  sum_d d * B_d per group: segments of SEG buckets by running sums, the
-//      k_tree_sum       segment offset applied by a short double-and-add, then LDS tree sums.
+//   7. k_seg_level /    sum_d d * B_d per group as a recursive weighted sum: with T_j / U_j the
+//      k_tree_sum /     plain / locally weighted sums of segment j (SEG buckets, by running sums),
+//      k_seg_final      W(S) = SEG * W(T) + sum_j U_j; the U sums by LDS trees, the SEG powers by
+//                       doublings in a per-group Horner step (~2 additions per bucket).
 //   8. k_window_horner  (per-window buckets only) sum_w 2^(c*w) G_w per MSM; batched affine.
 //
 // Batched mode (eon_msm_g1_columns*): one pipeline run handles many MSMs at once -- the columns
@@ -49,7 +52,8 @@ struct eon_msm_bases {
 
 namespace eon {
 
-constexpr uint32_t PIECE = 32;  // max mixed additions per piece
+constexpr uint32_t CHUNK = 128;  // sorted pairs per k_piece_sum thread
+constexpr uint32_t PIECE = 32;   // partials per combine step
 constexpr uint32_t SEG = 8;     // buckets per reduction segment
 constexpr uint32_t TREE = 256;  // points per tree-reduction block
 
@@ -135,23 +139,38 @@ __global__ void k_piece_owner(const uint32_t* piece_off, uint32_t nb, uint32_t* 
     for (uint32_t p = piece_off[b]; p < piece_off[b + 1]; p++) owner[p] = b;
 }
 
-__global__ void k_piece_sum(const uint32_t* vals, const uint32_t* start, const uint32_t* piece_off,
-                            const uint32_t* owner, uint32_t n_pieces, const G1Affine* pts,
+// count[b] = the CHUNK-aligned runs bucket b's pairs [start[b], start[b+1]) touch (0 if empty)
+__global__ void k_chunk_count(const uint32_t* start, uint32_t nb, uint32_t* count) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nb) return;
+    const uint32_t s = b == nb ? 0 : start[b], e = b == nb ? 0 : start[b + 1];
+    count[b] = s == e ? 0 : (e - 1) / CHUNK - s / CHUNK + 1;
+}
+
+// Thread t sums the sorted pairs [t CHUNK, (t+1) CHUNK) (nonzero digits only): one partial per
+// bucket run, stored at piece_off[b] + t - start[b] / CHUNK.
+__global__ void k_piece_sum(const uint32_t* keys, const uint32_t* vals, const uint32_t* start,
+                            const uint32_t* piece_off, uint32_t n_pairs, const G1Affine* pts,
                             G1Xyzz* piece_sums) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_pieces) return;
-    const uint32_t b = owner[p];
-    const uint32_t j = p - piece_off[b];
-    const uint32_t e0 = start[b] + j * PIECE;
-    const uint32_t e1 = min(e0 + PIECE, start[b + 1]);
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t e0 = t * CHUNK;
+    if (e0 >= n_pairs) return;
+    const uint32_t e1 = min(e0 + CHUNK, n_pairs);
+    uint32_t b = keys[e0];
     G1Xyzz acc = xyzz_inf();
     for (uint32_t e = e0; e < e1; e++) {
+        const uint32_t k = keys[e];
+        if (k != b) {
+            st_xyzz(piece_sums + piece_off[b] + t - start[b] / CHUNK, acc);
+            acc = xyzz_inf();
+            b = k;
+        }
         const uint32_t v = vals[e];
         G1Affine a = ld_affine(pts + (v & 0x7fffffffu));
         if (v >> 31) a = affine_neg(a);
         acc = xyzz_add_affine(acc, a);
     }
-    st_xyzz(piece_sums + p, acc);
+    st_xyzz(piece_sums + piece_off[b] + t - start[b] / CHUNK, acc);
 }
 
 // One combine level: new partial p of bucket b sums old partials
@@ -185,23 +204,41 @@ __global__ void k_bucket_final(const uint32_t* off, uint32_t nb, const G1Xyzz* p
     st_xyzz(bucket_sums + b, off[b + 1] > off[b] ? ld_xyzz(partials + off[b]) : xyzz_inf());
 }
 
-// Segment s of group g covers buckets [lo, lo + SEG) (bucket b holds digit b + 1):
-// out = sum_b (b + 1) * S_b = (running-sum form) + lo * (sum_b S_b)
-__global__ void k_segment_sum(const G1Xyzz* bucket_sums, uint32_t B, uint32_t groups,
-                              G1Xyzz* seg_out) {
-    const uint32_t nseg = B / SEG;
+// One level of the weighted bucket sum: segment j of group g covers x = X[g L + j seg ..+ seg);
+// T = sum_k x_k and U = sum_k k x_k, by running sums from the top (2 (seg - 1) + 1 additions).
+__global__ void __launch_bounds__(64) k_seg_level(const G1Xyzz* X, uint32_t L, uint32_t seg, uint32_t groups, G1Xyzz* T,
+                            G1Xyzz* U) {
+    const uint32_t nseg = L / seg;
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nseg * groups) return;
-    const uint32_t g = t / nseg, s = t % nseg;
-    const uint32_t lo = s * SEG;
-    const G1Xyzz* sb = bucket_sums + (uint64_t)g * B + lo;
+    const G1Xyzz* x = X + (uint64_t)(t / nseg) * L + (uint64_t)(t % nseg) * seg;
     G1Xyzz run = xyzz_inf(), acc = xyzz_inf();
-    for (int k = SEG - 1; k >= 0; k--) {
-        run = xyzz_add(run, ld_xyzz(sb + k));
+    for (uint32_t k = seg - 1; k >= 1; k--) {
+        run = xyzz_add(run, ld_xyzz(x + k));
         acc = xyzz_add(acc, run);
     }
-    if (lo) acc = xyzz_add(acc, xyzz_mul_small(run, lo));
-    st_xyzz(seg_out + t, acc);
+    run = xyzz_add(run, ld_xyzz(x));
+    st_xyzz(T + t, run);
+    st_xyzz(U + t, acc);
+}
+
+constexpr uint32_t MAX_SEG_LEVELS = 24;
+struct SegLogs {
+    uint8_t v[MAX_SEG_LEVELS];
+};
+
+// out[g] = usum[0] + s_0 (usum[1] + s_1 (... + s_{m-2} usum[m-1])) + t_final[g], s_l = 2^logs[l]
+// (usum[l] = sum of level l's U over group g, stored at usum[l * groups + g])
+__global__ void k_seg_final(const G1Xyzz* usum, uint32_t m, SegLogs logs, uint32_t groups,
+                            const G1Xyzz* t_final, G1Xyzz* out) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= groups) return;
+    G1Xyzz acc = ld_xyzz(usum + (uint64_t)(m - 1) * groups + g);
+    for (int l = (int)m - 2; l >= 0; l--) {
+        for (uint32_t d = 0; d < logs.v[l]; d++) acc = xyzz_dbl(acc);
+        acc = xyzz_add(acc, ld_xyzz(usum + (uint64_t)l * groups + g));
+    }
+    st_xyzz(out + g, xyzz_add(acc, ld_xyzz(t_final + g)));
 }
 
 // out[g * gridDim.x + blk] = sum of in[g * n + blk * TREE .. + TREE)
@@ -370,21 +407,42 @@ Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32
     return Status::ok();
 }
 
-// One batch of `cols` MSMs of length n over bases[0..n): MSM j uses scalars[i * ld + j].
-// Results (affine) are written to the device array `out_dev` (cols entries).
-static Status msm_batch(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, uint64_t n,
-                        uint64_t ld, uint32_t cols, G1Affine* out_dev) {
-    hipStream_t st = ctx->stream;
-    MsmWork& wk = ctx->msm;
-    const uint32_t c = b->precomputed ? b->c : choose_c(n, false);
-    const uint32_t W = b->precomputed ? b->windows : (255 + c - 1) / c;
-    const uint32_t B = 1u << (c - 1);
-    const uint32_t groups = b->precomputed ? cols : cols * W;
-    const uint32_t nb = groups * B;
-    const uint64_t E = n * W * cols;
-    if (E >= (1ull << 32)) return Status::err(EON_E_SHAPE, "MSM too large for 32-bit pair indices");
-    uint32_t key_bits = 1;
-    while ((1ull << key_bits) <= nb) key_bits++;
+// One batch of `cols` MSMs of length n over bases[0..n): MSM j uses scalars[i * ld + j].  A batch
+// runs in three steps on one stream with its own workspace, so that consecutive batches on two
+// streams overlap the memory-bound digit sort of one with the VALU-bound piece sums of the other:
+//   batch_sort    digits, radix sort, bucket starts, piece offsets; reads back the pair / piece
+//                 counts (synchronises its stream)
+//   batch_pieces  k_piece_sum (asynchronous)
+//   batch_reduce  combine levels (count read-backs), bucket sums, weighted bucket reduction;
+//                 leaves one XYZZ point per column in `out_dev`
+struct Batch {
+    const Fr* scalars = nullptr;
+    uint32_t cols = 0;
+    G1Xyzz* out = nullptr;
+    uint32_t c = 0, W = 0, B = 0, groups = 0, nb = 0, key_bits = 0;
+    uint64_t E = 0, max_pieces = 0;
+    size_t sort_bytes = 0, scan_bytes = 0;
+    uint32_t n_pieces = 0, n_pairs = 0;
+};
+
+static bool msm_debug() {
+    static const bool d = getenv("EON_MSM_DEBUG") != nullptr;
+    return d;
+}
+
+static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint64_t ld, Batch& bt,
+                         MsmWork& wk, hipStream_t st) {
+    bt.c = b->precomputed ? b->c : choose_c(n, false);
+    bt.W = b->precomputed ? b->windows : (255 + bt.c - 1) / bt.c;
+    bt.B = 1u << (bt.c - 1);
+    bt.groups = b->precomputed ? bt.cols : bt.cols * bt.W;
+    bt.nb = bt.groups * bt.B;
+    bt.E = n * bt.W * bt.cols;
+    if (bt.E >= (1ull << 32)) return Status::err(EON_E_SHAPE, "MSM too large for 32-bit pair indices");
+    bt.key_bits = 1;
+    while ((1ull << bt.key_bits) <= bt.nb) bt.key_bits++;
+    const uint64_t E = bt.E;
+    const uint32_t nb = bt.nb;
 
     EON_HIP(wk.keys.ensure(E * 4));
     EON_HIP(wk.vals.ensure(E * 4));
@@ -393,76 +451,87 @@ static Status msm_batch(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars,
     EON_HIP(wk.start.ensure((nb + 1) * 4ull));
     EON_HIP(wk.count.ensure((nb + 1) * 4ull));
     EON_HIP(wk.piece_off.ensure((nb + 1) * 4ull));
-    size_t sort_bytes = 0, scan_bytes = 0;
-    EON_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, wk.keys.as<uint32_t>(),
+    EON_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bt.sort_bytes, wk.keys.as<uint32_t>(),
                                                wk.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
-                                               wk.vals2.as<uint32_t>(), (int)E, 0, key_bits, st));
-    EON_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, wk.count.as<uint32_t>(),
+                                               wk.vals2.as<uint32_t>(), (int)E, 0, bt.key_bits, st));
+    EON_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bt.scan_bytes, wk.count.as<uint32_t>(),
                                              wk.piece_off.as<uint32_t>(), (int)(nb + 1), st));
-    EON_HIP(wk.temp.ensure(std::max(sort_bytes, scan_bytes)));
+    EON_HIP(wk.temp.ensure(std::max(bt.sort_bytes, bt.scan_bytes)));
+    bt.max_pieces = E / CHUNK + nb + 1;  // >= the real piece count
+    EON_HIP(wk.owner.ensure(bt.max_pieces * 4));
+    EON_HIP(wk.piece_sums.ensure(bt.max_pieces * sizeof(G1Xyzz)));
+    EON_HIP(wk.piece_sums2.ensure(bt.max_pieces * sizeof(G1Xyzz)));
+    EON_HIP(wk.bucket_sums.ensure((uint64_t)nb * sizeof(G1Xyzz)));
+    EON_HIP(wk.off2.ensure((nb + 1) * 4ull));
+    if (!wk.host_counts) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&wk.host_counts), 64));
 
     Profiler* prof = &ctx->prof;
-    prof->begin("k_msm_digits", n * cols * 32 + E * 8, st);
-    hipLaunchKernelGGL(k_msm_digits, dim3(blocks_for(n * cols, 256)), dim3(256), 0, st, scalars, n,
-                       ld, cols, c, W, (uint32_t)b->precomputed, wk.keys.as<uint32_t>(),
+    prof->begin("k_msm_digits", n * bt.cols * 32 + E * 8, st);
+    hipLaunchKernelGGL(k_msm_digits, dim3(blocks_for(n * bt.cols, 256)), dim3(256), 0, st, bt.scalars,
+                       n, ld, bt.cols, bt.c, bt.W, (uint32_t)b->precomputed, wk.keys.as<uint32_t>(),
                        wk.vals.as<uint32_t>());
     prof->end(st);
     EON_HIP(hipGetLastError());
     prof->begin("radix_sort_pairs", E * 16, st);
-    EON_HIP(hipcub::DeviceRadixSort::SortPairs(wk.temp.p, sort_bytes, wk.keys.as<uint32_t>(),
+    EON_HIP(hipcub::DeviceRadixSort::SortPairs(wk.temp.p, bt.sort_bytes, wk.keys.as<uint32_t>(),
                                                wk.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
-                                               wk.vals2.as<uint32_t>(), (int)E, 0, key_bits, st));
+                                               wk.vals2.as<uint32_t>(), (int)E, 0, bt.key_bits, st));
     prof->end(st);
     hipLaunchKernelGGL(k_bucket_start, dim3(blocks_for(E + 1, 256)), dim3(256), 0, st,
                        wk.keys2.as<uint32_t>(), E, nb, wk.start.as<uint32_t>());
-    hipLaunchKernelGGL(k_level_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_chunk_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st,
                        wk.start.as<uint32_t>(), nb, wk.count.as<uint32_t>());
-    EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, scan_bytes, wk.count.as<uint32_t>(),
+    EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, bt.scan_bytes, wk.count.as<uint32_t>(),
                                              wk.piece_off.as<uint32_t>(), (int)(nb + 1), st));
-    const uint64_t max_pieces = E / PIECE + nb + 1;  // >= the real piece count
-    EON_HIP(wk.owner.ensure(max_pieces * 4));
-    EON_HIP(wk.piece_sums.ensure(max_pieces * sizeof(G1Xyzz)));
-    EON_HIP(wk.bucket_sums.ensure((uint64_t)nb * sizeof(G1Xyzz)));
-    EON_HIP(wk.off2.ensure((nb + 1) * 4ull));
-    hipLaunchKernelGGL(k_piece_owner, dim3(blocks_for(nb, 256)), dim3(256), 0, st,
-                       wk.piece_off.as<uint32_t>(), nb, wk.owner.as<uint32_t>());
     // launches are sized by the real counts (8-byte read-back: pieces, nonzero digits)
-    uint32_t counts[2] = {0, 0};
-    EON_HIP(hipMemcpyAsync(&counts[0], wk.piece_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
-    EON_HIP(hipMemcpyAsync(&counts[1], wk.start.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
+    EON_HIP(hipMemcpyAsync(wk.host_counts, wk.piece_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
+    EON_HIP(hipMemcpyAsync(wk.host_counts + 1, wk.start.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
     EON_HIP(hipStreamSynchronize(st));
-    uint32_t n_pieces = counts[0];
-    const uint32_t n_pairs = counts[1];
-    static const bool debug = getenv("EON_MSM_DEBUG") != nullptr;
-    if (debug)
+    bt.n_pieces = wk.host_counts[0];
+    bt.n_pairs = wk.host_counts[1];
+    if (msm_debug())
         fprintf(stderr, "msm_batch n=%llu cols=%u c=%u W=%u nb=%u E=%llu pairs=%u pieces=%u\n",
-                (unsigned long long)n, cols, c, W, nb, (unsigned long long)E, n_pairs, n_pieces);
+                (unsigned long long)n, bt.cols, bt.c, bt.W, nb, (unsigned long long)E, bt.n_pairs,
+                bt.n_pieces);
+    return Status::ok();
+}
+
+static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt, MsmWork& wk,
+                           hipStream_t st) {
     const G1Affine* pts = b->precomputed ? b->table.as<G1Affine>() : b->points.as<G1Affine>();
-    // algorithmic bytes: every nonzero digit reads its 4-byte reference and a 64-byte affine
-    // base; every piece writes one 128-byte XYZZ partial
-    prof->begin("k_piece_sum", (uint64_t)n_pairs * 68 + (uint64_t)n_pieces * 128, st);
-    if (n_pieces)
-        hipLaunchKernelGGL(k_piece_sum, dim3(blocks_for(n_pieces, 64)), dim3(64), 0, st,
-                           wk.vals2.as<uint32_t>(), wk.start.as<uint32_t>(),
-                           wk.piece_off.as<uint32_t>(), wk.owner.as<uint32_t>(), n_pieces, pts,
+    // algorithmic bytes: every nonzero digit reads its 4-byte key, 4-byte reference and 64-byte
+    // affine base; every piece writes one 128-byte XYZZ partial
+    ctx->prof.begin("k_piece_sum", (uint64_t)bt.n_pairs * 72 + (uint64_t)bt.n_pieces * 128, st);
+    if (bt.n_pairs)
+        hipLaunchKernelGGL(k_piece_sum, dim3(blocks_for((bt.n_pairs + CHUNK - 1) / CHUNK, 64)), dim3(64),
+                           0, st, wk.keys2.as<uint32_t>(), wk.vals2.as<uint32_t>(),
+                           wk.start.as<uint32_t>(), wk.piece_off.as<uint32_t>(), bt.n_pairs, pts,
                            wk.piece_sums.as<G1Xyzz>());
-    prof->end(st);
+    ctx->prof.end(st);
+    EON_HIP(hipGetLastError());
+    return Status::ok();
+}
+
+static Status batch_reduce(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, MsmWork& wk,
+                           hipStream_t st) {
+    Profiler* prof = &ctx->prof;
+    const uint32_t nb = bt.nb, groups = bt.groups, B = bt.B;
     // combine levels until every bucket holds one partial (skewed scalars put many pieces in a
     // bucket: all-equal scalars put n pieces in one bucket per window)
     uint32_t* off_cur = wk.piece_off.as<uint32_t>();
     uint32_t* off_nxt = wk.off2.as<uint32_t>();
     G1Xyzz* part_cur = wk.piece_sums.as<G1Xyzz>();
-    EON_HIP(wk.piece_sums2.ensure(max_pieces * sizeof(G1Xyzz)));
     G1Xyzz* part_nxt = wk.piece_sums2.as<G1Xyzz>();
+    uint32_t n_pieces = bt.n_pieces;
     for (int level = 0; level < 8; level++) {
         hipLaunchKernelGGL(k_level_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st, off_cur,
                            nb, wk.count.as<uint32_t>());
-        EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, scan_bytes, wk.count.as<uint32_t>(),
+        EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, bt.scan_bytes, wk.count.as<uint32_t>(),
                                                  off_nxt, (int)(nb + 1), st));
-        uint32_t n_new = 0;
-        EON_HIP(hipMemcpyAsync(&n_new, off_nxt + nb, 4, hipMemcpyDeviceToHost, st));
+        EON_HIP(hipMemcpyAsync(wk.host_counts + 2, off_nxt + nb, 4, hipMemcpyDeviceToHost, st));
         EON_HIP(hipStreamSynchronize(st));
-        if (debug) fprintf(stderr, "  level %d: %u -> %u partials\n", level, n_pieces, n_new);
+        const uint32_t n_new = wk.host_counts[2];
+        if (msm_debug()) fprintf(stderr, "  level %d: %u -> %u partials\n", level, n_pieces, n_new);
         if (n_new == n_pieces) break;  // every bucket already holds at most one partial
         hipLaunchKernelGGL(k_piece_owner, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_nxt, nb,
                            wk.owner.as<uint32_t>());
@@ -476,35 +545,58 @@ static Status msm_batch(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars,
     }
     hipLaunchKernelGGL(k_bucket_final, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_cur, nb,
                        part_cur, wk.bucket_sums.as<G1Xyzz>());
-    // sum_d d * B_d per group
-    const uint32_t nseg = B / SEG;  // c >= 4, so B >= SEG
-    EON_HIP(wk.red_a.ensure((uint64_t)groups * nseg * sizeof(G1Xyzz)));
-    EON_HIP(wk.red_b.ensure((uint64_t)groups * nseg * sizeof(G1Xyzz)));
-    prof->begin("k_segment_sum", (uint64_t)nb * 128 + (uint64_t)groups * nseg * 128, st);
-    hipLaunchKernelGGL(k_segment_sum, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
-                       wk.bucket_sums.as<G1Xyzz>(), B, groups, wk.red_a.as<G1Xyzz>());
+    // sum_d d * B_d = W(S) + T(S) per group (bucket b holds digit b + 1), level by level
+    G1Xyzz* t_buf[2] = {wk.piece_sums.as<G1Xyzz>(), wk.piece_sums.as<G1Xyzz>() + (uint64_t)groups * (B / 2)};
+    G1Xyzz* u_buf = wk.piece_sums2.as<G1Xyzz>();
+    const uint32_t tree_max = (uint32_t)((uint64_t)groups * ((B / 2 + TREE - 1) / TREE));
+    EON_HIP(wk.red_a.ensure((uint64_t)tree_max * sizeof(G1Xyzz)));
+    EON_HIP(wk.red_b.ensure((uint64_t)tree_max * sizeof(G1Xyzz)));
+    EON_HIP(wk.levels.ensure((uint64_t)MAX_SEG_LEVELS * groups * sizeof(G1Xyzz)));
+    G1Xyzz* usum = wk.levels.as<G1Xyzz>();
+    SegLogs logs{};
+    const G1Xyzz* X = wk.bucket_sums.as<G1Xyzz>();
+    uint32_t L = B, m = 0;
+    prof->begin("k_seg_level", (uint64_t)nb * 128 + (uint64_t)nb / SEG * 256, st);
+    while (L > 1) {
+        const uint32_t seg = L < SEG ? L : SEG;
+        const uint32_t nseg = L / seg;
+        G1Xyzz* T = t_buf[m & 1];
+        hipLaunchKernelGGL(k_seg_level, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
+                           X, L, seg, groups, T, u_buf);
+        // usum[m] = sum over the group's nseg U values
+        const G1Xyzz* cur = u_buf;
+        uint32_t len = nseg;
+        G1Xyzz* bufs[2] = {wk.red_a.as<G1Xyzz>(), wk.red_b.as<G1Xyzz>()};
+        int which = 0;
+        while (len > 1) {
+            const uint32_t blk = (len + TREE - 1) / TREE;
+            G1Xyzz* dst = blk == 1 ? usum + (uint64_t)m * groups : bufs[which];
+            hipLaunchKernelGGL(k_tree_sum, dim3(blk, groups), dim3(TREE), 0, st, cur, len, dst);
+            cur = dst;
+            which ^= 1;
+            len = blk;
+        }
+        if (nseg == 1)
+            EON_HIP(hipMemcpyAsync(usum + (uint64_t)m * groups, u_buf, groups * sizeof(G1Xyzz),
+                                   hipMemcpyDeviceToDevice, st));
+        logs.v[m] = (uint8_t)(31 - __builtin_clz(seg));
+        X = T;
+        L = nseg;
+        m++;
+    }
+    G1Xyzz* per_group = wk.red_a.as<G1Xyzz>();
+    hipLaunchKernelGGL(k_seg_final, dim3(blocks_for(groups, 64)), dim3(64), 0, st, usum, m, logs, groups,
+                       X, per_group);
     prof->end(st);
-    G1Xyzz* cur = wk.red_a.as<G1Xyzz>();
-    G1Xyzz* nxt = wk.red_b.as<G1Xyzz>();
-    uint32_t len = nseg;
-    while (len > 1) {
-        const uint32_t blk = (len + TREE - 1) / TREE;
-        prof->begin("k_tree_sum", (uint64_t)groups * (len + blk) * 128, st);
-        hipLaunchKernelGGL(k_tree_sum, dim3(blk, groups), dim3(TREE), 0, st, cur, len, nxt);
-        prof->end(st);
-        std::swap(cur, nxt);
-        len = blk;
-    }
     EON_HIP(hipGetLastError());
-    // `cur` holds one point per group; per column: the group itself (fixed base) or the
-    // Horner combination of its windows; then batched XYZZ -> affine on device
-    G1Xyzz* per_col = cur;
+    // one point per group; per column: the group itself (fixed base) or the Horner combination of
+    // its windows
     if (!b->precomputed) {
-        hipLaunchKernelGGL(k_window_horner, dim3(blocks_for(cols, 64)), dim3(64), 0, st, cur, cols, W,
-                           c, nxt);
-        per_col = nxt;
+        hipLaunchKernelGGL(k_window_horner, dim3(blocks_for(bt.cols, 64)), dim3(64), 0, st, per_group,
+                           bt.cols, bt.W, bt.c, bt.out);
+    } else {
+        EON_HIP(hipMemcpyAsync(bt.out, per_group, bt.cols * sizeof(G1Xyzz), hipMemcpyDeviceToDevice, st));
     }
-    EON_HIP(launch_batch_to_affine(per_col, cols, out_dev, st));
     return Status::ok();
 }
 
@@ -526,12 +618,43 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
     if (cpb < 1) cpb = 1;
     const uint64_t max_groups = b->precomputed ? cpb : cpb * W;
     if (max_groups > 65535) cpb = b->precomputed ? 65535 : 65535 / W;
-    EON_HIP(ctx->msm.results.ensure(width * sizeof(G1Affine)));
+    // every batch leaves XYZZ results; one batched XYZZ -> affine conversion at the end (the
+    // conversion is an inversion-latency-bound launch, so it is paid once per call)
+    EON_HIP(ctx->msm.results.ensure(width * (sizeof(G1Affine) + sizeof(G1Xyzz))));
     G1Affine* res = ctx->msm.results.as<G1Affine>();
+    G1Xyzz* res_xyzz = reinterpret_cast<G1Xyzz*>(res + width);
+
+    std::vector<Batch> batches;
     for (uint32_t j0 = 0; j0 < width; j0 += (uint32_t)cpb) {
-        const uint32_t cols = (uint32_t)std::min<uint64_t>(cpb, width - j0);
-        EON_TRY(msm_batch(ctx, b, scalars + j0, n, width, cols, res + j0));
+        Batch bt;
+        bt.scalars = scalars + j0;
+        bt.cols = (uint32_t)std::min<uint64_t>(cpb, width - j0);
+        bt.out = res_xyzz + j0;
+        batches.push_back(bt);
     }
+    // batches alternate between the context stream and the MSM side stream (each with its own
+    // workspace); the side stream starts after the work already queued on the context stream and
+    // the context stream resumes after the side stream's last batch
+    const bool two = batches.size() > 1;
+    hipStream_t sts[2] = {ctx->stream, ctx->msm_side};
+    MsmWork* wks[2] = {&ctx->msm, &ctx->msm_b};
+    if (two) {
+        EON_HIP(hipEventRecord(ctx->msm_ev[0], sts[0]));
+        EON_HIP(hipStreamWaitEvent(sts[1], ctx->msm_ev[0], 0));
+    }
+    EON_TRY(batch_sort(ctx, b, n, width, batches[0], *wks[0], sts[0]));
+    for (size_t k = 0; k < batches.size(); k++) {
+        const int i = (int)(k & 1);
+        EON_TRY(batch_pieces(ctx, b, batches[k], *wks[i], sts[i]));
+        if (k + 1 < batches.size())
+            EON_TRY(batch_sort(ctx, b, n, width, batches[k + 1], *wks[i ^ 1], sts[i ^ 1]));
+        EON_TRY(batch_reduce(ctx, b, batches[k], *wks[i], sts[i]));
+    }
+    if (two) {
+        EON_HIP(hipEventRecord(ctx->msm_ev[1], sts[1]));
+        EON_HIP(hipStreamWaitEvent(sts[0], ctx->msm_ev[1], 0));
+    }
+    EON_HIP(launch_batch_to_affine(res_xyzz, width, res, ctx->stream));
     EON_HIP(hipMemcpyAsync(out_host, res, width * sizeof(G1Affine), hipMemcpyDeviceToHost, ctx->stream));
     EON_HIP(hipStreamSynchronize(ctx->stream));
     return Status::ok();

@@ -309,12 +309,130 @@ class ProveWorkload:
         return cpu_baseline_prove(self.log_n, self.vl, self.consts)
 
 
+
+class FourStepWorkload:
+    """configs[4] (i): one forward DFT of 2^log_n Fr (natural in / natural out semantics) as a
+    four-step N1 x N2 transform split over the ranks, one RCCL all_to_all for the transpose
+    (plonky3_eon_amd.distributed.fourstep_dft).  Total size fixed: strong scaling."""
+
+    scaling = "strong"
+
+    def __init__(self, args, ctx, dev, rank):
+        import torch
+
+        from plonky3_eon_amd import distributed as D
+
+        self.args, self.ctx, self.dev, self.rank = args, ctx, dev, rank
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.log_n = args.log_ntt
+        log_n1, log_n2 = D.fourstep_split(self.log_n)
+        cols = (1 << log_n2) // self.world
+        self.local = torch.from_numpy(synthetic_fr(1 << log_n1, cols, 4321 + rank).view(np.int64)).to(dev)
+
+    def step(self):
+        from plonky3_eon_amd import distributed as D
+
+        self.out = D.fourstep_dft(self.ctx, self.local, self.log_n, self.rank, self.world)
+
+    def describe(self, world):
+        return (f"configs[4] (i): forward DFT 2^{self.log_n} over BN254 Fr, four-step "
+                f"2^{(self.log_n + 1) // 2} x 2^{self.log_n // 2}, all_to_all transpose over {world} GPU(s)",
+                1, 1 << self.log_n, f"fourstep x{world}")
+
+    def throughput(self, world, ms):
+        n = 1 << self.log_n
+        return {"elements_per_s": round(n / (ms * 1e-3), 1)}, (n / 2) * self.log_n / world + n / world
+
+    def cpu_baseline(self):
+        from oracle import coracle
+
+        coracle.build()
+        log_s = 22
+        x = synthetic_fr(1 << log_s, 1, 99)
+        coracle.dft_batch(x[:1024])
+        t0 = time.perf_counter()
+        coracle.dft_batch(x)
+        dt = time.perf_counter() - t0
+        scale = ((1 << self.log_n) * self.log_n) / ((1 << log_s) * log_s)
+        return {
+            "value": round(dt * scale * 1e3, 1),
+            "unit": "ms",
+            "cores": coracle.num_threads(),
+            "kind": "port",
+            "sample": f"C restatement of Radix2Dit::dft_batch on one 2^{log_s} column ({dt:.2f} s), "
+                      f"scaled by N log N to 2^{self.log_n}",
+        }
+
+
+class MsmShardWorkload:
+    """configs[4] (ii): one MSM of 2^log_msm points split by contiguous point range over the ranks
+    (2^24 / G per GPU), per-rank Pippenger + all-gather of the partial points + their sum
+    (plonky3_eon_amd.distributed.msm_sharded).  Total size fixed: strong scaling.  Bases are a
+    synthetic SRS (alpha^i G1, per-rank alpha), fixed-base tables built untimed."""
+
+    scaling = "strong"
+
+    def __init__(self, args, ctx, dev, rank):
+        from plonky3_eon_amd import distributed as D
+        from plonky3_eon_amd.msm import MsmBases, srs_powers
+
+        self.args, self.ctx, self.dev = args, ctx, dev
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        n = 1 << args.log_shard_msm
+        lo, hi = D.shard_range(n, rank, self.world)
+        self.n_total, self.n_local = n, hi - lo
+        self.bases = MsmBases(srs_powers(self.n_local, 777 + rank, ctx), ctx, precompute=True)
+        import torch
+
+        self.scalars = torch.from_numpy(synthetic_fr(self.n_local, 1, 55 + rank).view(np.int64)).to(dev)
+        self.group = None
+
+    def step(self):
+        from plonky3_eon_amd import distributed as D
+
+        if self.world > 1:
+            self.out = D.msm_sharded(self.bases, self.scalars.reshape(-1, 4), self.dev, self.group)
+        else:
+            self.out = self.bases.msm(self.scalars.reshape(-1, 4))
+
+    def describe(self, world):
+        return (f"configs[4] (ii): MSM 2^{self.args.log_shard_msm} BN254 G1 points split by point range over "
+                f"{world} GPU(s) (2^{self.args.log_shard_msm} / {world} per GPU)", 1, self.n_total,
+                f"msm-shard x{world}")
+
+    def throughput(self, world, ms):
+        return {"points_per_s": round(self.n_total / (ms * 1e-3), 1)}, None
+
+    def cpu_baseline(self):
+        from oracle import coracle
+
+        coracle.build()
+        n = 1 << 18
+        pts = coracle.g1_srs(1 << 12, coracle.fr_from_u64(777))
+        pts = np.concatenate([pts] * (n >> 12))
+        s = synthetic_fr(n, 1, 12).reshape(n, 4)
+        t0 = time.perf_counter()
+        coracle.g1_msm(pts, s)
+        dt = time.perf_counter() - t0
+        scale = self.n_total / n
+        return {
+            "value": round(dt * scale * 1e3, 1),
+            "unit": "ms",
+            "cores": coracle.num_threads(),
+            "kind": "port",
+            "projected": True,
+            "sample": f"C Pippenger restatement on 2^18 points ({dt:.2f} s), scaled linearly to "
+                      f"2^{self.args.log_shard_msm}",
+        }
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default: 3 (prove), 10 (lde, msm)")
     ap.add_argument("--warmup", type=int, default=None, help="default: 1 (prove), 3 (lde, msm)")
-    ap.add_argument("--workload", choices=["prove", "lde", "msm"], default="prove")
+    ap.add_argument("--workload", choices=["prove", "lde", "msm", "ntt4", "msm-shard"], default="prove")
+    ap.add_argument("--log-ntt", type=int, default=26, help="ntt4: transform size (configs[4] (i))")
+    ap.add_argument("--log-shard-msm", type=int, default=24, help="msm-shard: total points (configs[4] (ii))")
     ap.add_argument("--log-trace", type=int, default=17)
     ap.add_argument("--vector-len", type=int, default=8)
     ap.add_argument("--log-n", type=int, default=20)
@@ -347,7 +465,8 @@ def main() -> int:
 
     ctx = Context(local_rank)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    wl = {"lde": LdeWorkload, "msm": MsmWorkload, "prove": ProveWorkload}[args.workload](args, ctx, dev, rank)
+    wl = {"lde": LdeWorkload, "msm": MsmWorkload, "prove": ProveWorkload, "ntt4": FourStepWorkload,
+          "msm-shard": MsmShardWorkload}[args.workload](args, ctx, dev, rank)
 
     for _ in range(args.warmup):
         wl.step()

@@ -199,6 +199,15 @@ int eon_p2air_quotient_values_dev(eon_ctx* ctx, const eon_p2air* air, const eon_
 int eon_fr_lincomb_dev(eon_ctx* ctx, const eon_fr* in, uint32_t k, uint64_t rows,
                        const eon_fr* coeffs, eon_fr* out);
 
+/* ---- four-step NTT across ranks (BASELINE configs[4]) ------------------------
+ * Step 2 + the local half of step 3 of a size-2^log_n forward DFT split as N1 x N2
+ * (N1 = 2^log_n1): y is the rank's N1 x cols block (columns col0 .. col0+cols of the N1 x N2 view
+ * x[N2 i1 + i2], after a size-N1 eon_dft_batch_dev over its columns); writes
+ * send[h][i2][k1'] = y[h N1/parts + k1'][i2] * w_N^((col0 + i2)(h N1/parts + k1')), i.e. `parts`
+ * contiguous cols x (N1/parts) blocks, one per destination rank (device pointers). */
+int eon_fourstep_twiddle_pack_dev(eon_ctx* ctx, const eon_fr* y, uint32_t log_n, uint32_t log_n1,
+                                  uint64_t col0, uint32_t cols, uint32_t parts, eon_fr* send);
+
 /* ---- test SRS (setup, not prove time) --------------------------------------------------------
  * init_srs_unsafe's g1_powers (kzg/src/params.rs:123-139): out[i] = alpha^i * G1::generator(),
  * affine, i < n.  `alpha` is a host pointer; `out` host (eon_g1_srs_powers) or device (_dev). */

@@ -96,6 +96,7 @@ SIGNATURES = {
     "eon_p2air_generate_trace_dev": (_INT, [_P, _P, _P, _U64, _P]),
     "eon_p2air_quotient_values_dev": (_INT, [_P, _P, _P, _U32, _U32, _P, _P]),
     "eon_fr_lincomb_dev": (_INT, [_P, _P, _U32, _U64, _P, _P]),
+    "eon_fourstep_twiddle_pack_dev": (_INT, [_P, _P, _U32, _U32, _U64, _U32, _U32, _P]),
 }
 
 _lib = None

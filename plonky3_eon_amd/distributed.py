@@ -1,6 +1,14 @@
-"""Lane-sharded eon-uni-stark prove across ranks: one process per GPU, torch.distributed
-(backend "nccl" = RCCL over xGMI on the MI355X node; "gloo" for the CPU tests and for several
-ranks sharing one GPU).
+"""Multi-GPU hot path: one process per GPU, torch.distributed (backend "nccl" =
+RCCL over xGMI on the MI355X node; "gloo" for the CPU tests and for several ranks sharing one
+GPU).  Three shardings:
+
+* the eon-uni-stark prove split by vector lane (below; `prover.prove(..., shard=Shard(...))`);
+* a single large forward DFT as a four-step N1 x N2 transform with one all_to_all
+  (`fourstep_dft`, BASELINE configs[4] (i));
+* an MSM split by point range with an all-gather of per-rank partial points
+  (`msm_sharded`, configs[4] (ii)).
+
+Lane-sharded prove:
 
 The sharding is SURVEY.md 8(e)'s preferred scheme for the vectorized Poseidon2-AIR.  The AIR
 evaluates its VECTOR_LEN lanes one after another (poseidon2-air/src/vectorized.rs:259-274), so
@@ -130,3 +138,114 @@ def gather_columns(local: np.ndarray, device, group=None) -> np.ndarray:
 
     t = torch.from_numpy(np.ascontiguousarray(local).view(np.int64)).to(device)
     return all_gather_rows(t, group).cpu().numpy().view(np.uint64).reshape(-1, COLUMN_RECORD)
+
+
+# ---- four-step NTT across ranks (BASELINE configs[4]) -----------------------------
+
+def all_to_all_blocks(send, group=None):
+    """send: (world, ...) -> recv with recv[g] = rank g's send[this rank] (RCCL all_to_all over
+    xGMI for nccl; staged through host memory for gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "nccl":
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send.contiguous(), group=group)
+        return recv
+    h = send.contiguous().cpu()
+    recv = torch.empty_like(h)
+    dist.all_to_all_single(recv, h, group=group)
+    return recv.to(send.device)
+
+
+def fourstep_split(log_n: int):
+    """N = N1 N2 with N1 = 2^ceil(log_n / 2)."""
+    log_n1 = (log_n + 1) // 2
+    return log_n1, log_n - log_n1
+
+
+def fourstep_dft(ctx, local, log_n: int, rank: int = 0, world: int = 1, group=None):
+    """Forward DFT of length N = 2^log_n (Radix2Dit natural order, dft/src/traits.rs:27-61) split
+    over `world` ranks as a four-step N1 x N2 transform.
+
+    local: this rank's (N1, N2/world, 4) int64 device block -- columns [rank C, (rank+1) C) of the
+    N1 x N2 view M[i1][i2] = x[N2 i1 + i2].  Returns the (N2, N1/world, 4) block of the N2 x N1 view
+    of X: out[k2][k1'] = X[N1 k2 + rank N1/world + k1'].  One all_to_all (the transpose) is the only
+    exchange."""
+    import torch
+
+    log_n1, log_n2 = fourstep_split(log_n)
+    n1, n2 = 1 << log_n1, 1 << log_n2
+    cols = n2 // world
+    if n2 % world or n1 % world:
+        raise _lib.EonError(_lib.EON_E_SHAPE, f"2^{log_n} does not split over {world} ranks")
+    if tuple(local.shape[:2]) != (n1, cols):
+        raise _lib.EonError(_lib.EON_E_SHAPE, f"local block must be ({n1}, {cols}, 4)")
+    local = local.contiguous()
+    stream = torch.cuda.current_stream(local.device).cuda_stream
+    ctx.set_stream(stream)
+    # 1. size-N1 DFTs of the rank's columns
+    y = torch.empty_like(local)
+    ctx.check(ctx.lib.eon_dft_batch_dev(ctx.handle, ctypes.c_void_p(local.data_ptr()),
+                                        ctypes.c_void_p(y.data_ptr()), n1, cols, 0))
+    # 2. twiddles, packed per destination rank
+    send = torch.empty((world, cols, n1 // world, 4), dtype=torch.int64, device=local.device)
+    ctx.check(ctx.lib.eon_fourstep_twiddle_pack_dev(ctx.handle, ctypes.c_void_p(y.data_ptr()), log_n, log_n1,
+                                                    rank * cols, cols, world, ctypes.c_void_p(send.data_ptr())))
+    del y
+    # 3. transpose across ranks
+    recv = all_to_all_blocks(send, group) if world > 1 else send
+    z = recv.reshape(n2, n1 // world, 4)
+    # 4. size-N2 DFTs over i2
+    out = torch.empty_like(z)
+    ctx.set_stream(stream)
+    ctx.check(ctx.lib.eon_dft_batch_dev(ctx.handle, ctypes.c_void_p(z.data_ptr()),
+                                        ctypes.c_void_p(out.data_ptr()), n2, n1 // world, 0))
+    return out
+
+
+def fourstep_scatter(x, log_n: int, rank: int, world: int):
+    """The rank's input block of a natural-order vector x (N, 4): columns [rank C, (rank+1) C) of
+    the N1 x N2 view."""
+    log_n1, log_n2 = fourstep_split(log_n)
+    c = (1 << log_n2) // world
+    return x.reshape(1 << log_n1, 1 << log_n2, 4)[:, rank * c:(rank + 1) * c]
+
+
+def fourstep_gather_index(log_n: int, rank: int, world: int):
+    """Natural indices of X held by the rank's output block (N2, N1/world), row-major."""
+    log_n1, log_n2 = fourstep_split(log_n)
+    n1, n2 = 1 << log_n1, 1 << log_n2
+    per = n1 // world
+    k2 = np.arange(n2, dtype=np.int64)[:, None]
+    k1 = rank * per + np.arange(per, dtype=np.int64)[None, :]
+    return (n1 * k2 + k1).reshape(-1)
+
+
+# ---- MSM sharded by point range (SURVEY.md 8(e); BASELINE configs[4] (ii)) -----------------------
+
+def shard_range(n: int, rank: int, world: int):
+    """Contiguous scalar / base range of `rank` (sizes differ by at most one)."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def msm_sharded(bases, scalars_local, device, group=None):
+    """sum_i s_i P_i over every rank's range: a full Pippenger per rank on its contiguous range
+    (`bases` = MsmBases over that range), then an all-gather of the G affine partial points and
+    their sum.  RCCL reductions cannot express EC addition, so the sum is one more device MSM
+    with unit scalars (eon_g1_multi_exp).  Returns the (8,) affine result on every rank."""
+    import torch
+
+    from .field import fr_mont
+    from .msm import multi_exp
+
+    part = bases.msm(scalars_local)
+    t = torch.from_numpy(np.ascontiguousarray(part).view(np.int64)).to(device)
+    parts = all_gather_rows(t, group).cpu().numpy().view(np.uint64).reshape(-1, 8)
+    ones = np.zeros((parts.shape[0], 4), dtype=np.uint64)
+    one = fr_mont(1)
+    for i in range(4):
+        ones[:, i] = (one >> (64 * i)) & 0xFFFFFFFFFFFFFFFF
+    return multi_exp(parts, ones, bases.ctx)

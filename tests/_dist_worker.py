@@ -6,6 +6,10 @@ RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment, backend gloo).
           gather_columns must reproduce the single-process oracle quotient.
   gpu  -- the product path (plonky3_eon_amd.prover.prove with a Shard) on cuda:0 for every rank;
           rank 0 also runs the unsharded prove and every proof field must match bit for bit.
+  a2a  -- all_to_all_blocks layout, and the four-step decomposition with oracle DFTs standing in
+          for the kernels (CPU).
+  fourstep / msmshard -- the product four-step DFT and the point-range-sharded MSM on cuda:0,
+          against the oracle's full-length DFT / MSM.
 
 Writes {"ok": true} or {"ok": false, "why": ...} as JSON to argv[2].
 """
@@ -126,6 +130,83 @@ def run_gpu(rank, world, group):
     return None
 
 
+def _tw_pack(y, log_n, log_n1, col0, parts):
+    """The documented contract of eon_fourstep_twiddle_pack_dev, in Python ints (test only)."""
+    n1, cols = y.shape[0], y.shape[1]
+    w = O.two_adic_generator(log_n)
+    per = n1 // parts
+    send = np.zeros((parts, cols, per, 4), dtype=np.uint64)
+    for k1 in range(n1):
+        for i2 in range(cols):
+            z = val(y[k1, i2]) * pow(w, (col0 + i2) * k1, O.P) % O.P
+            send[k1 // per, i2, k1 % per] = lim(z)
+    return send
+
+
+def run_a2a(rank, world, group):
+    import torch
+
+    from plonky3_eon_amd import distributed as D
+
+    send = torch.zeros((world, 3, 2), dtype=torch.int64)
+    for h in range(world):
+        send[h, :, 0] = rank
+        send[h, :, 1] = h
+    recv = D.all_to_all_blocks(send, group)
+    for g in range(world):
+        if not (bool((recv[g, :, 0] == g).all()) and bool((recv[g, :, 1] == rank).all())):
+            return "all_to_all_blocks layout"
+    for log_n in (6, 7):
+        n = 1 << log_n
+        log_n1, log_n2 = D.fourstep_split(log_n)
+        x = C.random_fr(log_n, n).reshape(n, 4)
+        local = np.ascontiguousarray(D.fourstep_scatter(x, log_n, rank, world))
+        y = C.dft_batch(local)
+        send = _tw_pack(y, log_n, log_n1, rank * local.shape[1], world)
+        recv = D.all_to_all_blocks(torch.from_numpy(send.view(np.int64)), group).numpy().view(np.uint64)
+        out = C.dft_batch(np.ascontiguousarray(recv.reshape(1 << log_n2, -1, 4)))
+        want = C.dft_batch(x.reshape(n, 1, 4)).reshape(n, 4)
+        if not np.array_equal(out.reshape(-1, 4), want[D.fourstep_gather_index(log_n, rank, world)]):
+            return f"four-step decomposition at 2^{log_n}"
+    return None
+
+
+def run_fourstep(rank, world, group):
+    import torch
+
+    from plonky3_eon_amd import Context
+    from plonky3_eon_amd import distributed as D
+
+    ctx = Context(0)
+    for log_n in (10, 11):
+        n = 1 << log_n
+        x = C.random_fr(log_n + 40, n).reshape(n, 4)
+        local = torch.from_numpy(np.ascontiguousarray(D.fourstep_scatter(x, log_n, rank, world)).view(np.int64))
+        out = D.fourstep_dft(ctx, local.to("cuda:0"), log_n, rank, world, group)
+        got = out.cpu().numpy().view(np.uint64).reshape(-1, 4)
+        want = C.dft_batch(x.reshape(n, 1, 4)).reshape(n, 4)[D.fourstep_gather_index(log_n, rank, world)]
+        if not np.array_equal(got, want):
+            return f"four-step DFT 2^{log_n} rank {rank}/{world}"
+    return None
+
+
+def run_msmshard(rank, world, group):
+    from plonky3_eon_amd import Context
+    from plonky3_eon_amd import distributed as D
+    from plonky3_eon_amd.msm import MsmBases
+
+    ctx = Context(0)
+    n = 3000
+    srs = C.g1_srs(n, C.fr_from_u64(777))
+    s = C.random_fr(5, n).reshape(n, 4)
+    lo, hi = D.shard_range(n, rank, world)
+    bases = MsmBases(np.ascontiguousarray(srs[lo:hi]), ctx, precompute=True)
+    got = D.msm_sharded(bases, np.ascontiguousarray(s[lo:hi]), "cuda:0", group)
+    if not np.array_equal(np.asarray(got).reshape(8), C.g1_msm(srs, s)):
+        return "sharded MSM != full MSM"
+    return None
+
+
 def main():
     import torch.distributed as dist
 
@@ -133,7 +214,9 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        why = (run_cpu if mode == "cpu" else run_gpu)(rank, world, None)
+        fn = {"cpu": run_cpu, "gpu": run_gpu, "a2a": run_a2a, "fourstep": run_fourstep,
+              "msmshard": run_msmshard}[mode]
+        why = fn(rank, world, None)
     except Exception:
         why = traceback.format_exc()
     finally:

@@ -38,3 +38,16 @@ def test_sharded_quotient_gloo_world2():
 def test_sharded_quotient_gloo_world4():
     res = run_world("cpu", 4, timeout=600)
     assert all(r["ok"] for r in res), [r["why"] for r in res]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_fourstep_exchange_gloo(world):
+    res = run_world("a2a", world, timeout=600)
+    assert all(r["ok"] for r in res), [r["why"] for r in res]
+
+
+def test_shard_range_partition():
+    for n in (1, 7, 4096, 4099):
+        for world in (1, 2, 3, 8):
+            r = [D.shard_range(n, g, world) for g in range(world)]
+            assert r[0][0] == 0 and r[-1][1] == n and all(a[1] == b[0] for a, b in zip(r, r[1:]))

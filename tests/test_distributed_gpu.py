@@ -12,3 +12,15 @@ pytestmark = pytest.mark.gpu
 def test_sharded_prove_matches_single(world, log_n, vl):
     res = run_world("gpu", world, timeout=900, extra_env={"EON_T_LOG_N": str(log_n), "EON_T_VL": str(vl)})
     assert all(r["ok"] for r in res), [r["why"] for r in res]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_fourstep_dft_matches_oracle(world):
+    res = run_world("fourstep", world, timeout=900)
+    assert all(r["ok"] for r in res), [r["why"] for r in res]
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_sharded_msm_matches_full(world):
+    res = run_world("msmshard", world, timeout=900)
+    assert all(r["ok"] for r in res), [r["why"] for r in res]

@@ -4,20 +4,29 @@
 Contract (see DESIGN.md "Measurement"): `python bench.py --gpus N --steps K --warmup W` runs W
 untimed steps, then times exactly K steps bracketed by a barrier + device synchronize, takes the
 max over ranks, and rank 0 prints ONE JSON line.  For N > 1 it is launched by
-torch.distributed.run (one process per GPU, RCCL backend); the workload is column-sharded, so
-each rank owns its own columns and there is no collective on the data path (weak scaling).
+torch.distributed.run (one process per GPU, RCCL backend).
 
-Workload (default, BASELINE.json configs[1]): Radix2DitParallel-semantics coset_lde_batch of a
-2^20 x 64 BN254 Fr matrix, added_bits = 1, shift = GENERATOR = 5, natural output order -- the LDE
-that KzgPcs::get_evaluations_on_domain needs (kzg/src/pcs.rs:267-287) and dft/benches/fft.rs
-times.  Inputs are synthetic uniform Fr, resident in HBM before the timed region.
+Workloads (--workload):
+  prove (default)  BASELINE.json configs[3] and the headline metric: eon-uni-stark prove of the
+                   vectorized Poseidon2-AIR (VECTOR_LEN 8, log-trace-length 17 = 2^20
+                   permutations) with KzgPcs over BN254.  At N > 1 the ONE proof is split by vector
+                   lane (plonky3_eon_amd/distributed.py): strong scaling.
+  lde              configs[1]: coset_lde_batch 2^20 x 64, added_bits 1, shift 5 (column-sharded,
+                   weak scaling).
+  msm              configs[2]: 2^20-point MSM over the alpha = 12345 SRS (weak scaling).
+  ntt4, msm-shard  configs[4]: 2^26 four-step DFT (one all_to_all) and 2^24-point MSM split by
+                   point range (strong scaling).
+Inputs are synthetic, resident in HBM before the timed region.
 
 Also reported:
-  roofline     -- for the dominant kernel: algorithmic bytes per launch / average launch
-                  duration (HIP events on the launch stream, eon_ctx_profile) vs 8 TB/s HBM;
-                  `valu` adds the integer roofline (algorithmic mulmods / measured peak).
-  cpu_baseline -- the C restatement of Radix2DitParallel::coset_lde_batch (oracle/eon_oracle.c,
-                  OpenMP) timed on this host on a bounded column sample, rank 0 at N = 1 only.
+  roofline     -- for the dominant kernel (largest total time): algorithmic bytes per launch /
+                  average launch duration (HIP events on the launch stream, eon_ctx_profile) vs
+                  8 TB/s HBM, `traffic` from the committed PMC pass (profiles/traffic_*.json);
+                  `valu` is the binding integer roofline of the same kernel: its algorithmic
+                  256-bit Montgomery products per launch / launch duration vs the measured
+                  mulmod peak (tools/ubench_mulmod.hip).
+  cpu_baseline -- the C restatement (oracle/eon_oracle.c, OpenMP) of the same work timed on this
+                  host on a bounded sample, rank 0 at N = 1 only.
 """
 
 from __future__ import annotations
@@ -37,7 +46,7 @@ sys.path.insert(0, str(ROOT))
 METRIC = "eon-uni-stark prove ms, Poseidon2-AIR 2^20 rows KZG/BN254, at 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # measured 256-bit Montgomery multiply peak (tools/ubench_mulmod.hip, MI355X, FIPS variant)
-MULMOD_PEAK_PER_S = 1.27e11
+MULMOD_PEAK_PER_S = 1.29e11
 FR_P = [0x43E1F593F0000001, 0x2833E84879B97091, 0xB85045B68181585D, 0x30644E72E131A029]
 
 
@@ -511,11 +520,19 @@ def main() -> int:
         "alg_bytes_per_launch": int(bytes_per_launch),
         "kernels": prof,
     }
-    if mulmods is not None:
+    kmm = kst.get("alg_mulmods", 0)
+    if kmm:
+        rate = kmm / kst["launches"] / (avg_ms * 1e-3)
         roof["valu"] = {
             "binding": True,
-            "achieved_mulmod_per_s": round(mulmods / (gpu_total_ms * 1e-3), 1),
+            "alg_mulmods_per_launch": int(kmm / kst["launches"]),
+            "achieved_mulmod_per_s": round(rate, 1),
             "peak_mulmod_per_s": MULMOD_PEAK_PER_S,
+            "frac": round(rate / MULMOD_PEAK_PER_S, 4),
+        }
+    if mulmods is not None:
+        roof["valu_whole_step"] = {
+            "achieved_mulmod_per_s": round(mulmods / (gpu_total_ms * 1e-3), 1),
             "frac": round(mulmods / (gpu_total_ms * 1e-3) / MULMOD_PEAK_PER_S, 4),
         }
     result = {

@@ -318,12 +318,12 @@ int eon_ctx_profile(eon_ctx* ctx, int enable) {
 }
 
 int eon_ctx_profile_report(eon_ctx* ctx, char* buf, uint64_t len) {
-    // JSON: {"kernel name": {"launches": n, "total_ms": t, "alg_bytes": b}, ...}
+    // JSON: {"kernel name": {"launches": n, "total_ms": t, "alg_bytes": b, "alg_mulmods": m}, ...}
     if (!ctx || !buf || len == 0) return EON_E_ARG;
     std::lock_guard<std::mutex> lk(ctx->mu);
     (void)hipSetDevice(ctx->device);
     struct Agg {
-        uint64_t n = 0, bytes = 0;
+        uint64_t n = 0, bytes = 0, mulmods = 0;
         double ms = 0;
     };
     std::map<std::string, Agg> agg;
@@ -335,13 +335,17 @@ int eon_ctx_profile_report(eon_ctx* ctx, char* buf, uint64_t len) {
         a.n++;
         a.ms += ms;
         a.bytes += r.alg_bytes;
+        a.mulmods += r.alg_mulmods;
     }
     std::string out = "{";
     char tmp[256];
     for (auto& kv : agg) {
-        snprintf(tmp, sizeof tmp, "%s\"%s\": {\"launches\": %llu, \"total_ms\": %.6f, \"alg_bytes\": %llu}",
+        snprintf(tmp, sizeof tmp,
+                 "%s\"%s\": {\"launches\": %llu, \"total_ms\": %.6f, \"alg_bytes\": %llu, "
+                 "\"alg_mulmods\": %llu}",
                  out.size() > 1 ? ", " : "", kv.first.c_str(), (unsigned long long)kv.second.n,
-                 kv.second.ms, (unsigned long long)kv.second.bytes);
+                 kv.second.ms, (unsigned long long)kv.second.bytes,
+                 (unsigned long long)kv.second.mulmods);
         out += tmp;
     }
     out += "}";

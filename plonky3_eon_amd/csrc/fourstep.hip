@@ -94,7 +94,8 @@ int eon_fourstep_twiddle_pack_dev(eon_ctx* ctx, const eon_fr* y, uint32_t log_n,
         // the bounded table cache may have been flushed while building t_hi: look t_lo up again
         EON_TRY(get_power_table(ctx, lo_bits, w, Fr::one(), false, &t_lo));
         const dim3 grid((cols + FS_TILE - 1) / FS_TILE, (n1 + FS_TILE - 1) / FS_TILE);
-        ctx->prof.begin("k_fourstep_twiddle_pack", (uint64_t)n1 * cols * 64, ctx->stream);
+        ctx->prof.begin("k_fourstep_twiddle_pack", (uint64_t)n1 * cols * 64, ctx->stream,
+                        (uint64_t)n1 * cols * 2);
         hipLaunchKernelGGL(k_fourstep_twiddle_pack, grid, dim3(FS_TILE, FS_ROWS), 0, ctx->stream,
                            reinterpret_cast<const Fr*>(y), n1, cols, col0, n1 / parts, log_n, lo_bits,
                            t_lo, t_hi, reinterpret_cast<Fr*>(send));

@@ -9,16 +9,19 @@
 //                       (bucket key, point reference | sign) pair per nonzero digit.
 //   2. radix sort       hipCUB DeviceRadixSort on the c-bit keys (zero digits sort last).
 //   3. k_bucket_start   bucket boundaries in the sorted pairs.
-//   4. pieces           a piece is the part of a bucket inside one CHUNK-aligned run of sorted
-//                       pairs; exclusive scan of the per-bucket piece counts.
-//   5. k_piece_sum      one thread per CHUNK of sorted pairs (every lane does the same number of
+//   4. pieces           a piece is the part of a bucket inside one chunk (2^log_chunk aligned
+//                       sorted pairs); exclusive scan of the per-bucket piece counts.
+//   5. k_piece_sum      one thread per chunk of sorted pairs (every lane does the same number of
 //                       XYZZ mixed additions of affine bases), flushing a partial per piece.
 //   6. k_partial_combine levels of <= PIECE-way sums until each bucket holds one partial
 //                       (log-depth under any skew, e.g. all-equal scalars), k_bucket_final.
 //   7. k_seg_level /    sum_d d * B_d per group as a recursive weighted sum: with T_j / U_j the
 //      k_tree_sum /     plain / locally weighted sums of segment j (SEG buckets, by running sums),
 //      k_seg_final      W(S) = SEG * W(T) + sum_j U_j; the U sums by LDS trees, the SEG powers by
-//                       doublings in a per-group Horner step (~2 additions per bucket).
+//                       doublings in a per-group Horner step (~2 additions per bucket).  Batches
+//                       with < 64 groups (a single MSM) use the shorter-chain k_segment_sum
+//                       (running sums + lo * run) + one tree instead: there latency, not
+//                       additions, sets the time.
 //   8. k_window_horner  (per-window buckets only) sum_w 2^(c*w) G_w per MSM; batched affine.
 //
 // Batched mode (eon_msm_g1_columns*): one pipeline run handles many MSMs at once -- the columns
@@ -52,7 +55,9 @@ struct eon_msm_bases {
 
 namespace eon {
 
-constexpr uint32_t CHUNK = 128;  // sorted pairs per k_piece_sum thread
+// sorted pairs per k_piece_sum thread: 2^log_chunk, sized so a batch launches ~2^20 threads
+// (>= 4 waves on every SIMD) within [2^4, 2^7]
+constexpr uint32_t LOG_CHUNK_MIN = 4, LOG_CHUNK_MAX = 7;
 constexpr uint32_t PIECE = 32;   // partials per combine step
 constexpr uint32_t SEG = 8;     // buckets per reduction segment
 constexpr uint32_t TREE = 256;  // points per tree-reduction block
@@ -139,29 +144,29 @@ __global__ void k_piece_owner(const uint32_t* piece_off, uint32_t nb, uint32_t* 
     for (uint32_t p = piece_off[b]; p < piece_off[b + 1]; p++) owner[p] = b;
 }
 
-// count[b] = the CHUNK-aligned runs bucket b's pairs [start[b], start[b+1]) touch (0 if empty)
-__global__ void k_chunk_count(const uint32_t* start, uint32_t nb, uint32_t* count) {
+// count[b] = the chunk-aligned runs bucket b's pairs [start[b], start[b+1]) touch (0 if empty)
+__global__ void k_chunk_count(const uint32_t* start, uint32_t nb, uint32_t log_chunk, uint32_t* count) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b > nb) return;
     const uint32_t s = b == nb ? 0 : start[b], e = b == nb ? 0 : start[b + 1];
-    count[b] = s == e ? 0 : (e - 1) / CHUNK - s / CHUNK + 1;
+    count[b] = s == e ? 0 : ((e - 1) >> log_chunk) - (s >> log_chunk) + 1;
 }
 
-// Thread t sums the sorted pairs [t CHUNK, (t+1) CHUNK) (nonzero digits only): one partial per
-// bucket run, stored at piece_off[b] + t - start[b] / CHUNK.
+// Thread t sums the sorted pairs [t 2^log_chunk, (t+1) 2^log_chunk) (nonzero digits only): one
+// partial per bucket run, stored at piece_off[b] + t - (start[b] >> log_chunk).
 __global__ void k_piece_sum(const uint32_t* keys, const uint32_t* vals, const uint32_t* start,
-                            const uint32_t* piece_off, uint32_t n_pairs, const G1Affine* pts,
-                            G1Xyzz* piece_sums) {
+                            const uint32_t* piece_off, uint32_t n_pairs, uint32_t log_chunk,
+                            const G1Affine* pts, G1Xyzz* piece_sums) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t e0 = t * CHUNK;
+    const uint32_t e0 = t << log_chunk;
     if (e0 >= n_pairs) return;
-    const uint32_t e1 = min(e0 + CHUNK, n_pairs);
+    const uint32_t e1 = min(e0 + (1u << log_chunk), n_pairs);
     uint32_t b = keys[e0];
     G1Xyzz acc = xyzz_inf();
     for (uint32_t e = e0; e < e1; e++) {
         const uint32_t k = keys[e];
         if (k != b) {
-            st_xyzz(piece_sums + piece_off[b] + t - start[b] / CHUNK, acc);
+            st_xyzz(piece_sums + piece_off[b] + t - (start[b] >> log_chunk), acc);
             acc = xyzz_inf();
             b = k;
         }
@@ -170,7 +175,7 @@ __global__ void k_piece_sum(const uint32_t* keys, const uint32_t* vals, const ui
         if (v >> 31) a = affine_neg(a);
         acc = xyzz_add_affine(acc, a);
     }
-    st_xyzz(piece_sums + piece_off[b] + t - start[b] / CHUNK, acc);
+    st_xyzz(piece_sums + piece_off[b] + t - (start[b] >> log_chunk), acc);
 }
 
 // One combine level: new partial p of bucket b sums old partials
@@ -202,6 +207,26 @@ __global__ void k_bucket_final(const uint32_t* off, uint32_t nb, const G1Xyzz* p
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     st_xyzz(bucket_sums + b, off[b + 1] > off[b] ? ld_xyzz(partials + off[b]) : xyzz_inf());
+}
+
+// Segment s of group g covers buckets [lo, lo + SEG) (bucket b holds digit b + 1):
+// out = sum_b (b + 1) * S_b = (running-sum form) + lo * (sum_b S_b).  The latency-optimal form
+// for few groups (one short chain per segment, one tree): used when a batch has < 64 groups.
+__global__ void __launch_bounds__(64) k_segment_sum(const G1Xyzz* bucket_sums, uint32_t B,
+                                                    uint32_t groups, G1Xyzz* seg_out) {
+    const uint32_t nseg = B / SEG;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nseg * groups) return;
+    const uint32_t g = t / nseg, s = t % nseg;
+    const uint32_t lo = s * SEG;
+    const G1Xyzz* sb = bucket_sums + (uint64_t)g * B + lo;
+    G1Xyzz run = xyzz_inf(), acc = xyzz_inf();
+    for (int k = SEG - 1; k >= 0; k--) {
+        run = xyzz_add(run, ld_xyzz(sb + k));
+        acc = xyzz_add(acc, run);
+    }
+    if (lo) acc = xyzz_add(acc, xyzz_mul_small(run, lo));
+    st_xyzz(seg_out + t, acc);
 }
 
 // One level of the weighted bucket sum: segment j of group g covers x = X[g L + j seg ..+ seg);
@@ -419,7 +444,7 @@ struct Batch {
     const Fr* scalars = nullptr;
     uint32_t cols = 0;
     G1Xyzz* out = nullptr;
-    uint32_t c = 0, W = 0, B = 0, groups = 0, nb = 0, key_bits = 0;
+    uint32_t c = 0, W = 0, B = 0, groups = 0, nb = 0, key_bits = 0, log_chunk = 0;
     uint64_t E = 0, max_pieces = 0;
     size_t sort_bytes = 0, scan_bytes = 0;
     uint32_t n_pieces = 0, n_pairs = 0;
@@ -457,7 +482,9 @@ static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint6
     EON_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bt.scan_bytes, wk.count.as<uint32_t>(),
                                              wk.piece_off.as<uint32_t>(), (int)(nb + 1), st));
     EON_HIP(wk.temp.ensure(std::max(bt.sort_bytes, bt.scan_bytes)));
-    bt.max_pieces = E / CHUNK + nb + 1;  // >= the real piece count
+    bt.log_chunk = LOG_CHUNK_MIN;
+    while (bt.log_chunk < LOG_CHUNK_MAX && (E >> (bt.log_chunk + 1)) >= (1ull << 20)) bt.log_chunk++;
+    bt.max_pieces = (E >> bt.log_chunk) + nb + 1;  // >= the real piece count
     EON_HIP(wk.owner.ensure(bt.max_pieces * 4));
     EON_HIP(wk.piece_sums.ensure(bt.max_pieces * sizeof(G1Xyzz)));
     EON_HIP(wk.piece_sums2.ensure(bt.max_pieces * sizeof(G1Xyzz)));
@@ -480,7 +507,7 @@ static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint6
     hipLaunchKernelGGL(k_bucket_start, dim3(blocks_for(E + 1, 256)), dim3(256), 0, st,
                        wk.keys2.as<uint32_t>(), E, nb, wk.start.as<uint32_t>());
     hipLaunchKernelGGL(k_chunk_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st,
-                       wk.start.as<uint32_t>(), nb, wk.count.as<uint32_t>());
+                       wk.start.as<uint32_t>(), nb, bt.log_chunk, wk.count.as<uint32_t>());
     EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, bt.scan_bytes, wk.count.as<uint32_t>(),
                                              wk.piece_off.as<uint32_t>(), (int)(nb + 1), st));
     // launches are sized by the real counts (8-byte read-back: pieces, nonzero digits)
@@ -501,15 +528,57 @@ static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt
     const G1Affine* pts = b->precomputed ? b->table.as<G1Affine>() : b->points.as<G1Affine>();
     // algorithmic bytes: every nonzero digit reads its 4-byte key, 4-byte reference and 64-byte
     // affine base; every piece writes one 128-byte XYZZ partial
-    ctx->prof.begin("k_piece_sum", (uint64_t)bt.n_pairs * 72 + (uint64_t)bt.n_pieces * 128, st);
+    // mulmods: one XYZZ mixed addition (madd-2008-s, 8M + 2S) per nonzero digit
+    ctx->prof.begin("k_piece_sum", (uint64_t)bt.n_pairs * 72 + (uint64_t)bt.n_pieces * 128, st,
+                    (uint64_t)bt.n_pairs * 10);
     if (bt.n_pairs)
-        hipLaunchKernelGGL(k_piece_sum, dim3(blocks_for((bt.n_pairs + CHUNK - 1) / CHUNK, 64)), dim3(64),
-                           0, st, wk.keys2.as<uint32_t>(), wk.vals2.as<uint32_t>(),
-                           wk.start.as<uint32_t>(), wk.piece_off.as<uint32_t>(), bt.n_pairs, pts,
-                           wk.piece_sums.as<G1Xyzz>());
+        hipLaunchKernelGGL(k_piece_sum,
+                           dim3(blocks_for(((uint64_t)bt.n_pairs + (1u << bt.log_chunk) - 1) >> bt.log_chunk, 64)),
+                           dim3(64), 0, st, wk.keys2.as<uint32_t>(), wk.vals2.as<uint32_t>(),
+                           wk.start.as<uint32_t>(), wk.piece_off.as<uint32_t>(), bt.n_pairs,
+                           bt.log_chunk, pts, wk.piece_sums.as<G1Xyzz>());
     ctx->prof.end(st);
     EON_HIP(hipGetLastError());
     return Status::ok();
+}
+
+// per-column output step shared by both bucket reductions
+static Status write_columns(const eon_msm_bases* b, const Batch& bt, const G1Xyzz* per_group,
+                            hipStream_t st) {
+    // one point per group; per column: the group itself (fixed base) or the Horner combination of
+    // its windows
+    if (!b->precomputed) {
+        hipLaunchKernelGGL(k_window_horner, dim3(blocks_for(bt.cols, 64)), dim3(64), 0, st, per_group,
+                           bt.cols, bt.W, bt.c, bt.out);
+        EON_HIP(hipGetLastError());
+    } else {
+        EON_HIP(hipMemcpyAsync(bt.out, per_group, bt.cols * sizeof(G1Xyzz), hipMemcpyDeviceToDevice, st));
+    }
+    return Status::ok();
+}
+
+// sum_d d * B_d per group, few-groups form: k_segment_sum + LDS trees (short dependency chains)
+static Status reduce_segments(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt, MsmWork& wk,
+                              hipStream_t st) {
+    const uint32_t nseg = bt.B / SEG;  // c >= 4, so B >= SEG
+    const uint32_t groups = bt.groups;
+    EON_HIP(wk.red_a.ensure((uint64_t)groups * nseg * sizeof(G1Xyzz)));
+    EON_HIP(wk.red_b.ensure((uint64_t)groups * nseg * sizeof(G1Xyzz)));
+    ctx->prof.begin("k_segment_sum", (uint64_t)bt.nb * 128 + (uint64_t)groups * nseg * 128, st);
+    hipLaunchKernelGGL(k_segment_sum, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
+                       wk.bucket_sums.as<G1Xyzz>(), bt.B, groups, wk.red_a.as<G1Xyzz>());
+    ctx->prof.end(st);
+    G1Xyzz* cur = wk.red_a.as<G1Xyzz>();
+    G1Xyzz* nxt = wk.red_b.as<G1Xyzz>();
+    uint32_t len = nseg;
+    while (len > 1) {
+        const uint32_t blk = (len + TREE - 1) / TREE;
+        hipLaunchKernelGGL(k_tree_sum, dim3(blk, groups), dim3(TREE), 0, st, cur, len, nxt);
+        std::swap(cur, nxt);
+        len = blk;
+    }
+    EON_HIP(hipGetLastError());
+    return write_columns(b, bt, cur, st);
 }
 
 static Status batch_reduce(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, MsmWork& wk,
@@ -535,7 +604,8 @@ static Status batch_reduce(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, MsmW
         if (n_new == n_pieces) break;  // every bucket already holds at most one partial
         hipLaunchKernelGGL(k_piece_owner, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_nxt, nb,
                            wk.owner.as<uint32_t>());
-        prof->begin("k_partial_combine", (uint64_t)(n_pieces + n_new) * 128, st);
+        prof->begin("k_partial_combine", (uint64_t)(n_pieces + n_new) * 128, st,
+                    (uint64_t)(n_pieces - n_new) * 14);  // add-2008-s: 12M + 2S
         hipLaunchKernelGGL(k_partial_combine, dim3(blocks_for(n_new, 64)), dim3(64), 0, st, off_cur,
                            off_nxt, wk.owner.as<uint32_t>(), n_new, part_cur, part_nxt);
         prof->end(st);
@@ -545,6 +615,7 @@ static Status batch_reduce(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, MsmW
     }
     hipLaunchKernelGGL(k_bucket_final, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_cur, nb,
                        part_cur, wk.bucket_sums.as<G1Xyzz>());
+    if (groups < 64) return reduce_segments(ctx, b, bt, wk, st);
     // sum_d d * B_d = W(S) + T(S) per group (bucket b holds digit b + 1), level by level
     G1Xyzz* t_buf[2] = {wk.piece_sums.as<G1Xyzz>(), wk.piece_sums.as<G1Xyzz>() + (uint64_t)groups * (B / 2)};
     G1Xyzz* u_buf = wk.piece_sums2.as<G1Xyzz>();
@@ -589,15 +660,7 @@ static Status batch_reduce(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, MsmW
                        X, per_group);
     prof->end(st);
     EON_HIP(hipGetLastError());
-    // one point per group; per column: the group itself (fixed base) or the Horner combination of
-    // its windows
-    if (!b->precomputed) {
-        hipLaunchKernelGGL(k_window_horner, dim3(blocks_for(bt.cols, 64)), dim3(64), 0, st, per_group,
-                           bt.cols, bt.W, bt.c, bt.out);
-    } else {
-        EON_HIP(hipMemcpyAsync(bt.out, per_group, bt.cols * sizeof(G1Xyzz), hipMemcpyDeviceToDevice, st));
-    }
-    return Status::ok();
+    return write_columns(b, bt, per_group, st);
 }
 
 Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, uint64_t n,

@@ -44,6 +44,7 @@ struct LaunchRecord {
     const char* kernel;
     uint64_t alg_bytes;  // algorithmic bytes of this launch (each element read + written once)
     hipEvent_t start, stop;
+    uint64_t alg_mulmods;  // algorithmic 256-bit Montgomery products of this launch (0: not counted)
 };
 struct Profiler {
     bool enabled = false;
@@ -59,9 +60,9 @@ struct Profiler {
         (void)hipEventCreate(&e);
         return e;
     }
-    void begin(const char* kernel, uint64_t bytes, hipStream_t st) {
+    void begin(const char* kernel, uint64_t bytes, hipStream_t st, uint64_t mulmods = 0) {
         if (!enabled) return;
-        LaunchRecord r{kernel, bytes, get(), get()};
+        LaunchRecord r{kernel, bytes, get(), get(), mulmods};
         (void)hipEventRecord(r.start, st);
         recs.push_back(r);
     }

@@ -296,7 +296,11 @@ hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
                                        "k_ntt_pass<false, 2>", "k_ntt_pass<false, 3>",
                                        "k_ntt_pass<true, 0>",  "k_ntt_pass<true, 1>",
                                        "k_ntt_pass<true, 2>",  "k_ntt_pass<true, 3>"};
-        if (prof) prof->begin(names[(s.dif ? 4 : 0) + log_cb], (64ull << s.log_m) * s.width, st);
+        // mulmods: one per butterfly (the BASELINE.md count), plus the fused input/output scalings
+        const uint64_t elems = (1ull << s.log_m) * s.width;
+        const uint64_t mm = elems / 2 * a.k + (a.load_scale ? elems : 0) + (a.has_load_const ? elems : 0) +
+                            (a.store_scale ? elems : 0);
+        if (prof) prof->begin(names[(s.dif ? 4 : 0) + log_cb], 64ull * elems, st, mm);
         hipError_t e = launch_pass(s.dif, log_cb, a, groups, col_tiles, s.max_threads ? s.max_threads : 512, st);
         if (prof) prof->end(st);
         if (e != hipSuccess) return e;

@@ -422,7 +422,7 @@ int eon_fr_lincomb_dev(eon_ctx* ctx, const eon_fr* in, uint32_t k, uint64_t rows
             c.c[j] = fr_from_abi(&coeffs[j]);
             if (!fr_is_canonical(c.c[j])) return Status::err(EON_E_ARG, "coefficient is not a canonical Fr");
         }
-        ctx->prof.begin("k_fr_lincomb", (k + 1) * rows * 32, ctx->stream);
+        ctx->prof.begin("k_fr_lincomb", (k + 1) * rows * 32, ctx->stream, (uint64_t)k * rows);
         hipLaunchKernelGGL(k_fr_lincomb, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, ctx->stream,
                            reinterpret_cast<const Fr*>(in), k, rows, c, reinterpret_cast<Fr*>(out));
         ctx->prof.end(ctx->stream);

@@ -2,7 +2,8 @@
 kernel, corrected as MI355X_MICROARCH.md prescribes: counters are in KB (x1024), and on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced streaming read (x2).
 
-usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <kernel-substring> <workload> <out.json>
+usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <kernel-substring> <workload | bench.json> <out.json>
+(a bench.json argument supplies config.workload from that bench line)
 """
 
 import csv
@@ -23,6 +24,9 @@ def per_dispatch(d, counter, kernel):
 
 def main():
     fdir, wdir, kernel, workload, out = sys.argv[1:6]
+    if workload.endswith(".json"):
+        txt = open(workload).read()
+        workload = json.loads(txt[txt.index("{"):])["config"]["workload"]
     fetch = per_dispatch(fdir, "FETCH_SIZE", kernel)
     write = per_dispatch(wdir, "WRITE_SIZE", kernel)
     if not fetch or not write:

@@ -58,5 +58,34 @@ def build(verbose: bool = False) -> Path:
     return LIB
 
 
+def build_variant(name: str, defines: list[str]) -> Path:
+    """Tuning builds: every source with extra -D flags -> build/variants/libeonhip_<name>.so, loaded
+    instead of the default library when EON_LIB points at it (plonky3_eon_amd/_lib.py)."""
+    out_dir = ROOT / "build" / "variants" / name
+    out_dir.mkdir(parents=True, exist_ok=True)
+
+    def comp(src: Path) -> Path:
+        obj = out_dir / (src.stem + ".o")
+        cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-c", str(src), "-o", str(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=8) as ex:
+        objs = list(ex.map(comp, sources()))
+    lib = ROOT / "build" / "variants" / f"libeonhip_{name}.so"
+    r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(lib)],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    return lib
+
+
 if __name__ == "__main__":
-    build(verbose=True)
+    import sys
+
+    if len(sys.argv) > 2 and sys.argv[1] == "variant":
+        print(build_variant(sys.argv[2], sys.argv[3:]))
+    else:
+        build(verbose=True)

@@ -107,11 +107,12 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not LIB_PATH.exists():
+    path = Path(os.environ["EON_LIB"]) if os.environ.get("EON_LIB") else LIB_PATH  # tuning variants
+    if not path.exists():
         raise ImportError(
-            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
         )
-    lib = ctypes.CDLL(os.fspath(LIB_PATH))
+    lib = ctypes.CDLL(os.fspath(path))
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -154,7 +154,10 @@ __global__ void k_chunk_count(const uint32_t* start, uint32_t nb, uint32_t log_c
 
 // Thread t sums the sorted pairs [t 2^log_chunk, (t+1) 2^log_chunk) (nonzero digits only): one
 // partial per bucket run, stored at piece_off[b] + t - (start[b] >> log_chunk).
-__global__ void k_piece_sum(const uint32_t* keys, const uint32_t* vals, const uint32_t* start,
+#ifndef EON_PIECE_MINWAVES
+#define EON_PIECE_MINWAVES 4
+#endif
+__global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum(const uint32_t* keys, const uint32_t* vals, const uint32_t* start,
                             const uint32_t* piece_off, uint32_t n_pairs, uint32_t log_chunk,
                             const G1Affine* pts, G1Xyzz* piece_sums) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -681,6 +684,9 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
     if (cpb < 1) cpb = 1;
     const uint64_t max_groups = b->precomputed ? cpb : cpb * W;
     if (max_groups > 65535) cpb = b->precomputed ? 65535 : 65535 / W;
+    // equal batches (164 columns -> 82 + 82, not 128 + 36): the two streams overlap evenly
+    const uint64_t n_batches = (width + cpb - 1) / cpb;
+    cpb = (width + n_batches - 1) / n_batches;
     // every batch leaves XYZZ results; one batched XYZZ -> affine conversion at the end (the
     // conversion is an inversion-latency-bound launch, so it is paid once per call)
     EON_HIP(ctx->msm.results.ensure(width * (sizeof(G1Affine) + sizeof(G1Xyzz))));

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "context.h"
 #include "ntt.h"
@@ -239,10 +240,36 @@ int eon_ctx_create(int device_ordinal, eon_ctx** out) {
         return EON_E_DEVICE;
     }
     c->stream = c->own_stream;
-    // MSM side stream: non-blocking so that it overlaps null-stream work (ordered by events)
-    if (hipStreamCreateWithFlags(&c->msm_side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->msm_ev[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->msm_ev[1], hipEventDisableTiming) != hipSuccess) {
+    // MSM streams: non-blocking so that they overlap null-stream work (ordered by events); the
+    // sort stream at the highest priority
+    int prio_least = 0, prio_greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+    bool ok = hipStreamCreateWithFlags(&c->msm_side, hipStreamNonBlocking) == hipSuccess;
+    if (const char* e = getenv("EON_MSM_SORT_CUS")) c->msm_sort_cus = (uint32_t)atoi(e);
+    hipDeviceProp_t prop{};
+    int ncu = 0;
+    if (hipGetDeviceProperties(&prop, device_ordinal) == hipSuccess) ncu = prop.multiProcessorCount;
+    if (const char* e = getenv("EON_PIECE_WAVES"))
+        if (ncu > 0) c->piece_block_cap = (uint32_t)atoi(e) * 4u * (uint32_t)ncu;
+    if (c->msm_sort_cus && ncu > 0 && c->msm_sort_cus < (uint32_t)ncu) {
+        // the sort CUs spread evenly over the CU index space (every (ncu / k)-th CU)
+        const uint32_t words = ((uint32_t)ncu + 31) / 32, stride = (uint32_t)ncu / c->msm_sort_cus;
+        std::vector<uint32_t> sort_mask(words, 0), comp_mask(words, 0);
+        for (uint32_t i = 0; i < (uint32_t)ncu; i++) {
+            const bool srt = (i % stride) == 0 && i / stride < c->msm_sort_cus;
+            (srt ? sort_mask : comp_mask)[i / 32] |= 1u << (i % 32);
+        }
+        ok = ok && hipExtStreamCreateWithCUMask(&c->msm_sort, words, sort_mask.data()) == hipSuccess &&
+             hipExtStreamCreateWithCUMask(&c->msm_comp[0], words, comp_mask.data()) == hipSuccess &&
+             hipExtStreamCreateWithCUMask(&c->msm_comp[1], words, comp_mask.data()) == hipSuccess;
+    } else {
+        c->msm_sort_cus = 0;
+        ok = ok && hipStreamCreateWithPriority(&c->msm_sort, hipStreamNonBlocking, prio_greatest) == hipSuccess;
+    }
+    for (hipEvent_t* e : {&c->msm_ev[0], &c->msm_ev[1], &c->msm_ev[2], &c->msm_sorted[0], &c->msm_sorted[1],
+                          &c->msm_sorted[2], &c->msm_reduced[0], &c->msm_reduced[1], &c->msm_reduced[2]})
+        ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
         (void)hipStreamDestroy(c->own_stream);
         delete c;
         return EON_E_DEVICE;
@@ -259,6 +286,9 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamSynchronize(ctx->msm_side);
+    (void)hipStreamSynchronize(ctx->msm_sort);
+    for (hipStream_t st : ctx->msm_comp)
+        if (st) (void)hipStreamSynchronize(st);
     ctx->tw_fwd.release();
     ctx->tw_inv.release();
     for (auto& kv : ctx->tables) kv.second.release();
@@ -269,6 +299,7 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     for (auto e : ctx->prof.pool) (void)hipEventDestroy(e);
     ctx->msm.release();
     ctx->msm_b.release();
+    ctx->msm_c.release();
     ctx->sel_tab.release();
     ctx->kzg_tmp.release();
     ctx->scratch.release();
@@ -276,8 +307,12 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     ctx->stage_out.release();
     (void)hipStreamDestroy(ctx->own_stream);
     (void)hipStreamDestroy(ctx->msm_side);
-    (void)hipEventDestroy(ctx->msm_ev[0]);
-    (void)hipEventDestroy(ctx->msm_ev[1]);
+    (void)hipStreamDestroy(ctx->msm_sort);
+    for (hipStream_t st : ctx->msm_comp)
+        if (st) (void)hipStreamDestroy(st);
+    for (hipEvent_t e : {ctx->msm_ev[0], ctx->msm_ev[1], ctx->msm_ev[2], ctx->msm_sorted[0], ctx->msm_sorted[1],
+                         ctx->msm_sorted[2], ctx->msm_reduced[0], ctx->msm_reduced[1], ctx->msm_reduced[2]})
+        (void)hipEventDestroy(e);
     delete ctx;
 }
 

@@ -100,10 +100,19 @@ struct eon_ctx {
     // per-launch HIP-event timing (eon_ctx_profile_*)
     eon::Profiler prof;
 
-    // MSM pipeline workspaces: batches alternate between `stream` (msm) and msm_side (msm_b)
-    eon::MsmWork msm, msm_b;
-    hipStream_t msm_side = nullptr;
-    hipEvent_t msm_ev[2] = {nullptr, nullptr};
+    // MSM pipeline: workspaces msm / msm_b / msm_c for batches k % 3; piece sums + reductions on
+    // `stream` / msm_side, digit sorts on the high-priority msm_sort (msm.hip: msm_run_columns)
+    eon::MsmWork msm, msm_b, msm_c;
+    hipStream_t msm_side = nullptr, msm_sort = nullptr;
+    // EON_MSM_SORT_CUS > 0: piece sums on msm_comp[2] (CU-masked to all but those CUs), sorts
+    // on msm_sort masked to them -- a full piece-sum launch leaves no room for a sort workgroup
+    uint32_t msm_sort_cus = 0;
+    // EON_PIECE_WAVES (1..4): cap k_piece_sum's grid at that many one-wave blocks per SIMD
+    // (0 = one thread per chunk, no cap)
+    uint32_t piece_block_cap = 0;
+    hipStream_t msm_comp[2] = {nullptr, nullptr};
+    hipEvent_t msm_ev[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t msm_sorted[3] = {nullptr, nullptr, nullptr}, msm_reduced[3] = {nullptr, nullptr, nullptr};
 
     // quotient: vanishing-polynomial table; KZG opening scan workspace
     eon::DevBuf sel_tab, kzg_tmp;

@@ -160,9 +160,11 @@ __global__ void k_chunk_count(const uint32_t* start, uint32_t nb, uint32_t log_c
 __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum(const uint32_t* keys, const uint32_t* vals, const uint32_t* start,
                             const uint32_t* piece_off, uint32_t n_pairs, uint32_t log_chunk,
                             const G1Affine* pts, G1Xyzz* piece_sums) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    // grid-stride over chunks: a capped grid (EON_PIECE_WAVES) leaves wave slots for the
+    // concurrent digit sort of the next batch
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; ((uint64_t)t << log_chunk) < n_pairs;
+         t += gridDim.x * blockDim.x) {
     const uint32_t e0 = t << log_chunk;
-    if (e0 >= n_pairs) return;
     const uint32_t e1 = min(e0 + (1u << log_chunk), n_pairs);
     uint32_t b = keys[e0];
     G1Xyzz acc = xyzz_inf();
@@ -179,6 +181,7 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum(const uint
         acc = xyzz_add_affine(acc, a);
     }
     st_xyzz(piece_sums + piece_off[b] + t - (start[b] >> log_chunk), acc);
+    }
 }
 
 // One combine level: new partial p of bucket b sums old partials
@@ -534,9 +537,10 @@ static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt
     // mulmods: one XYZZ mixed addition (madd-2008-s, 8M + 2S) per nonzero digit
     ctx->prof.begin("k_piece_sum", (uint64_t)bt.n_pairs * 72 + (uint64_t)bt.n_pieces * 128, st,
                     (uint64_t)bt.n_pairs * 10);
+    uint32_t blocks = blocks_for(((uint64_t)bt.n_pairs + (1u << bt.log_chunk) - 1) >> bt.log_chunk, 64);
+    if (ctx->piece_block_cap) blocks = std::min(blocks, ctx->piece_block_cap);
     if (bt.n_pairs)
-        hipLaunchKernelGGL(k_piece_sum,
-                           dim3(blocks_for(((uint64_t)bt.n_pairs + (1u << bt.log_chunk) - 1) >> bt.log_chunk, 64)),
+        hipLaunchKernelGGL(k_piece_sum, dim3(blocks),
                            dim3(64), 0, st, wk.keys2.as<uint32_t>(), wk.vals2.as<uint32_t>(),
                            wk.start.as<uint32_t>(), wk.piece_off.as<uint32_t>(), bt.n_pairs,
                            bt.log_chunk, pts, wk.piece_sums.as<G1Xyzz>());
@@ -701,27 +705,42 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
         bt.out = res_xyzz + j0;
         batches.push_back(bt);
     }
-    // batches alternate between the context stream and the MSM side stream (each with its own
-    // workspace); the side stream starts after the work already queued on the context stream and
-    // the context stream resumes after the side stream's last batch
-    const bool two = batches.size() > 1;
-    hipStream_t sts[2] = {ctx->stream, ctx->msm_side};
-    MsmWork* wks[2] = {&ctx->msm, &ctx->msm_b};
-    if (two) {
-        EON_HIP(hipEventRecord(ctx->msm_ev[0], sts[0]));
-        EON_HIP(hipStreamWaitEvent(sts[1], ctx->msm_ev[0], 0));
-    }
-    EON_TRY(batch_sort(ctx, b, n, width, batches[0], *wks[0], sts[0]));
+    // Three streams: every digit sort on the high-priority sort stream (so its memory-bound
+    // kernels get CU slots while a piece-sum launch fills the chip), piece sums + reductions
+    // alternating between the context stream and the side stream (batch k's reduction overlaps
+    // batch k+1's piece sums).  Three workspaces (batch k uses k % 3): sort(k+1) only waits for
+    // reduce(k-2), which finished while pieces(k-1) ran -- with two, it waited for reduce(k-1),
+    // starved by pieces(k), and the sort ended up exposed.  Events order sort(k) after
+    // reduce(k - 3) and pieces(k) after sort(k).
+    const bool masked = ctx->msm_sort_cus > 0;
+    hipStream_t comp[2] = {masked ? ctx->msm_comp[0] : ctx->stream, masked ? ctx->msm_comp[1] : ctx->msm_side};
+    hipStream_t sort_st = ctx->msm_sort;
+    MsmWork* wks[3] = {&ctx->msm, &ctx->msm_b, &ctx->msm_c};
+    EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));  // scalars and earlier work are ready
+    EON_HIP(hipStreamWaitEvent(sort_st, ctx->msm_ev[0], 0));
+    for (hipStream_t st : comp)
+        if (st != ctx->stream) EON_HIP(hipStreamWaitEvent(st, ctx->msm_ev[0], 0));
+    auto sort_batch = [&](size_t k) -> Status {
+        const int w = (int)(k % 3);
+        if (k >= 3) EON_HIP(hipStreamWaitEvent(sort_st, ctx->msm_reduced[w], 0));
+        EON_TRY(batch_sort(ctx, b, n, width, batches[k], *wks[w], sort_st));
+        EON_HIP(hipEventRecord(ctx->msm_sorted[w], sort_st));
+        return Status::ok();
+    };
+    EON_TRY(sort_batch(0));
     for (size_t k = 0; k < batches.size(); k++) {
-        const int i = (int)(k & 1);
-        EON_TRY(batch_pieces(ctx, b, batches[k], *wks[i], sts[i]));
-        if (k + 1 < batches.size())
-            EON_TRY(batch_sort(ctx, b, n, width, batches[k + 1], *wks[i ^ 1], sts[i ^ 1]));
-        EON_TRY(batch_reduce(ctx, b, batches[k], *wks[i], sts[i]));
+        const int i = (int)(k & 1), w = (int)(k % 3);
+        EON_HIP(hipStreamWaitEvent(comp[i], ctx->msm_sorted[w], 0));
+        EON_TRY(batch_pieces(ctx, b, batches[k], *wks[w], comp[i]));
+        if (k + 1 < batches.size()) EON_TRY(sort_batch(k + 1));
+        EON_TRY(batch_reduce(ctx, b, batches[k], *wks[w], comp[i]));
+        EON_HIP(hipEventRecord(ctx->msm_reduced[w], comp[i]));
     }
-    if (two) {
-        EON_HIP(hipEventRecord(ctx->msm_ev[1], sts[1]));
-        EON_HIP(hipStreamWaitEvent(sts[0], ctx->msm_ev[1], 0));
+    // the context stream resumes after both compute streams' last reductions
+    for (int i = 0; i < 2; i++) {
+        if (comp[i] == ctx->stream) continue;
+        EON_HIP(hipEventRecord(ctx->msm_ev[1 + i], comp[i]));
+        EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[1 + i], 0));
     }
     EON_HIP(launch_batch_to_affine(res_xyzz, width, res, ctx->stream));
     EON_HIP(hipMemcpyAsync(out_host, res, width * sizeof(G1Affine), hipMemcpyDeviceToHost, ctx->stream));

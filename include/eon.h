@@ -98,6 +98,13 @@ int eon_coset_idft_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t h
  * (lde_batch, dft/src/traits.rs:187-192).  `shift` is always a host pointer. */
 int eon_coset_lde_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
                         uint32_t width, uint32_t added_bits, const eon_fr* shift, int out_order);
+/* coset_dft_batch of the COEFFICIENT matrix zero-padded to height << added_bits -- the second
+ * half of coset_lde_batch (dft/src/traits.rs:226-249), and KzgPcs::get_evaluations_on_domain from
+ * the committed coefficients (kzg/src/pcs.rs:267-287, commit/src/testing.rs:93-105):
+ * out[k] = sum_j coeffs[j] (shift * w^k)^j, |K| = height << added_bits.  `in` != `out`. */
+int eon_coset_dft_padded_batch(eon_ctx* ctx, const eon_fr* coeffs, eon_fr* out, uint64_t height,
+                               uint32_t width, uint32_t added_bits, const eon_fr* shift,
+                               int out_order);
 
 /* device-pointer variants (same semantics, asynchronous on the context stream) */
 int eon_dft_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
@@ -111,6 +118,9 @@ int eon_coset_idft_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64
 int eon_coset_lde_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
                             uint32_t width, uint32_t added_bits, const eon_fr* shift,
                             int out_order);
+int eon_coset_dft_padded_batch_dev(eon_ctx* ctx, const eon_fr* coeffs, eon_fr* out, uint64_t height,
+                                   uint32_t width, uint32_t added_bits, const eon_fr* shift,
+                                   int out_order);
 
 /* ---- BN254 G1 multi-scalar multiplication -------------------------------------------------
  * Value of G1::multi_exp (bn254/src/curve.rs:158-179, halo2curves msm_best): sum_i s_i * P_i,

@@ -77,6 +77,8 @@ SIGNATURES = {
     "eon_coset_dft_batch_dev": (_INT, [_P, _P, _P, _U64, _U32, _P, _INT]),
     "eon_coset_idft_batch_dev": (_INT, [_P, _P, _P, _U64, _U32, _P]),
     "eon_coset_lde_batch_dev": (_INT, [_P, _P, _P, _U64, _U32, _U32, _P, _INT]),
+    "eon_coset_dft_padded_batch": (_INT, [_P, _P, _P, _U64, _U32, _U32, _P, _INT]),
+    "eon_coset_dft_padded_batch_dev": (_INT, [_P, _P, _P, _U64, _U32, _U32, _P, _INT]),
     "eon_msm_bases_create": (_INT, [_P, _P, _U64, _U32, ctypes.POINTER(_P)]),
     "eon_msm_bases_destroy": (None, [_P]),
     "eon_msm_bases_len": (_U64, [_P]),

@@ -70,7 +70,7 @@ Status get_power_table(eon_ctx* ctx, uint32_t log_n, const Fr& base, const Fr& s
 
 namespace {
 
-enum class Op { Dft, Idft, CosetDft, CosetIdft, CosetLde };
+enum class Op { Dft, Idft, CosetDft, CosetIdft, CosetLde, CosetDftPadded };
 
 int finish(eon_ctx* ctx, const Status& s) {
     if (s.bad()) ctx->last_error = s.msg;
@@ -90,7 +90,8 @@ Status check_shape(uint64_t height, uint32_t added_bits, uint32_t* log_h) {
 Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint32_t width,
                uint32_t added_bits, const eon_fr* shift_abi, int out_order) {
     uint32_t n = 0;
-    EON_TRY(check_shape(height, op == Op::CosetLde ? added_bits : 0, &n));
+    const bool grows = op == Op::CosetLde || op == Op::CosetDftPadded;
+    EON_TRY(check_shape(height, grows ? added_bits : 0, &n));
     if (out_order != EON_ORDER_NATURAL && out_order != EON_ORDER_BITREV)
         return Status::err(EON_E_ARG, "out_order must be EON_ORDER_NATURAL or EON_ORDER_BITREV");
     if (width == 0) return Status::ok();
@@ -101,7 +102,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         if (!fr_is_canonical(shift)) return Status::err(EON_E_ARG, "shift is not a canonical Fr");
     }
     const bool natural = out_order == EON_ORDER_NATURAL;
-    const uint32_t b = op == Op::CosetLde ? added_bits : 0;
+    const uint32_t b = grows ? added_bits : 0;
     EON_TRY(ensure_twiddles(ctx, n + b));
     const size_t mat_bytes = (size_t)height * width * sizeof(Fr);
     hipStream_t st = ctx->stream;
@@ -149,6 +150,37 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         return Status::ok();
     }
 
+    if (op == Op::CosetDftPadded) {
+        // coset_dft of the coefficients zero-padded to height * 2^b: coset_lde_batch without its
+        // idft (dft/src/traits.rs:226-249), i.e. KzgPcs::get_evaluations_on_domain from the
+        // committed coefficients (kzg/src/pcs.rs:267-287; commit/src/testing.rs:93-105)
+        if (in == out) return Status::err(EON_E_ARG, "padded coset DFT cannot run in place");
+        const Fr* table = nullptr;
+        EON_TRY(get_power_table(ctx, n, shift, Fr::one(), false, &table));
+        NetworkSpec f;
+        f.log_m = n + b;
+        f.src = in;
+        f.dst = out;
+        f.width = width;
+        f.tw = ctx->tw_fwd.as<Fr>();
+        f.load_scale = table;  // coefficient j times shift^j, indexed by source row
+        if (natural) {
+            f.dif = false;
+            f.first_stage = b;
+            f.load_mode = LOAD_BITREV_SPREAD;
+            f.load_param = b | (n << 8);
+        } else {
+            f.dif = true;
+            f.load_mode = LOAD_ZEROPAD;
+            f.load_param = (uint32_t)height;
+        }
+        f.max_stages_per_pass = ctx->ntt_max_stages;
+        f.max_threads = ctx->ntt_tpb;
+        f.log_cb_override = ctx->ntt_log_cb;
+        EON_HIP(run_network(f, st, &ctx->prof));
+        return Status::ok();
+    }
+
     NetworkSpec s;
     s.log_m = n;
     s.src = in;
@@ -192,11 +224,12 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
 Status dft_host(eon_ctx* ctx, Op op, const eon_fr* in, eon_fr* out, uint64_t height,
                 uint32_t width, uint32_t added_bits, const eon_fr* shift, int out_order) {
     uint32_t n = 0;
-    EON_TRY(check_shape(height, op == Op::CosetLde ? added_bits : 0, &n));
+    const bool grows = op == Op::CosetLde || op == Op::CosetDftPadded;
+    EON_TRY(check_shape(height, grows ? added_bits : 0, &n));
     if (width == 0) return Status::ok();
     if (!in || !out) return Status::err(EON_E_ARG, "null matrix pointer");
     const size_t in_bytes = (size_t)height * width * sizeof(Fr);
-    const size_t out_bytes = in_bytes << (op == Op::CosetLde ? added_bits : 0);
+    const size_t out_bytes = in_bytes << (grows ? added_bits : 0);
     EON_HIP(ctx->stage_in.ensure(in_bytes));
     EON_HIP(ctx->stage_out.ensure(out_bytes));
     EON_HIP(hipMemcpyAsync(ctx->stage_in.p, in, in_bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -409,6 +442,19 @@ int eon_coset_idft_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t h
 int eon_coset_lde_batch(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,
                         uint32_t width, uint32_t added_bits, const eon_fr* shift, int out_order) {
     return entry(ctx, false, Op::CosetLde, in, out, height, width, added_bits, shift, out_order);
+}
+
+int eon_coset_dft_padded_batch(eon_ctx* ctx, const eon_fr* coeffs, eon_fr* out, uint64_t height,
+                               uint32_t width, uint32_t added_bits, const eon_fr* shift,
+                               int out_order) {
+    if (!shift) return EON_E_ARG;
+    return entry(ctx, false, Op::CosetDftPadded, coeffs, out, height, width, added_bits, shift, out_order);
+}
+int eon_coset_dft_padded_batch_dev(eon_ctx* ctx, const eon_fr* coeffs, eon_fr* out, uint64_t height,
+                                   uint32_t width, uint32_t added_bits, const eon_fr* shift,
+                                   int out_order) {
+    if (!shift) return EON_E_ARG;
+    return entry(ctx, true, Op::CosetDftPadded, coeffs, out, height, width, added_bits, shift, out_order);
 }
 
 int eon_dft_batch_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint64_t height,

@@ -11,6 +11,10 @@ enum LoadMode : uint32_t {
     LOAD_BITREV = 1,   // reads source row reverse_bits(p, load_param)
     LOAD_SPREAD = 2,   // reads source row p >> load_param (LDE: bit-reversed coefficients spread)
     LOAD_ZEROPAD = 3,  // reads source row p if p < load_param, else zero
+    // reads source row reverse_bits(p >> b, n) with b = load_param & 0xff, n = load_param >> 8:
+    // the zero-padded natural vector's bit-reversed order after its first b DIT stages (which
+    // only replicate values), for evaluating coefficients on a larger coset
+    LOAD_BITREV_SPREAD = 4,
 };
 
 constexpr uint32_t NATURAL_IDX = 0xffffffffu;

@@ -106,6 +106,12 @@ __global__ void __launch_bounds__(512) k_ntt_pass(PassArgs a) {
                     break;
                 case LOAD_SPREAD: r = p >> a.load_param; break;
                 case LOAD_ZEROPAD: present = p < a.load_param; break;
+                case LOAD_BITREV_SPREAD: {
+                    const uint32_t nb = a.load_param >> 8;
+                    const uint64_t q = p >> (a.load_param & 0xff);
+                    r = nb ? (__builtin_bitreverse64(q) >> (64 - nb)) : 0;
+                    break;
+                }
                 default: break;
             }
             if (present) {

@@ -181,6 +181,13 @@ class _GpuDft:
         return self._wrap(self._call("eon_coset_lde_batch", mat, 1 << added_bits, added_bits,
                                      ctypes.byref(s), self.out_order))
 
+    def coset_dft_padded_batch(self, coeffs, added_bits: int, shift):
+        """coset_dft_batch of `coeffs` zero-padded to height << added_bits (coset_lde_batch minus
+        its idft; dft/src/traits.rs:226-249)."""
+        s = fr_to_abi(shift)
+        return self._wrap(self._call("eon_coset_dft_padded_batch", coeffs, 1 << added_bits, added_bits,
+                                     ctypes.byref(s), self.out_order))
+
     # single-column conveniences (dft/src/traits.rs:46,70,100,131,168,207)
     def dft(self, vec):
         return _col(self.dft_batch(_as_col(vec)))

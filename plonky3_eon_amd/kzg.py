@@ -6,8 +6,9 @@ Reference: ``KzgPcs`` (kzg/src/pcs.rs:143-402) implementing ``Pcs<Fr, Challenger
 * ``commit``                     -- coset_idft_batch of each matrix (pcs.rs:242) and one KZG
                                     commitment (MSM over the SRS g1_powers) per column
                                     (pcs.rs:244-251), as one batched device MSM.
-* ``get_evaluations_on_domain``  -- pcs.rs:267-287 evaluates every column at every point by
-                                    Horner; the same values come from one coset LDE.
+* ``get_evaluations_on_domain``  -- pcs.rs:267-287 evaluates every column's coefficients at
+                                    every point by Horner; the same values come from one coset
+                                    DFT of the zero-padded coefficients.
 * ``commit_quotient``            -- commit/src/pcs.rs:82-101: split_evals / split_domains
                                     (domain.rs:174-221), then commit.
 * ``open``                       -- pcs.rs:289-335: per (matrix, point) the synthetic-division
@@ -120,9 +121,9 @@ class GpuKzgPcs:
             return m.evals
         if domain.log_size < m.domain.log_size:
             raise _lib.EonError(_lib.EON_E_SHAPE, "evaluation domain smaller than the committed domain")
-        # f(domain.shift * w^k) = coset LDE of the evals on m.domain with shift domain.shift / m.domain.shift
-        rel = domain.shift * pow(m.domain.shift, -1, FR_MODULUS) % FR_MODULUS
-        return self.dft.coset_lde_batch(m.evals, domain.log_size - m.domain.log_size, rel)
+        # the reference evaluates the committed coefficients at every point by Horner; the same
+        # values are the coset DFT of the zero-padded coefficients (one forward network)
+        return self.dft.coset_dft_padded_batch(m.coeffs, domain.log_size - m.domain.log_size, domain.shift)
 
     def commit_quotient(self, quotient_domain: Domain, quotient_evals, num_chunks: int):
         """commit/src/pcs.rs:82-101; chunk c holds rows {i * num_chunks + c} (domain.rs:188-221)."""

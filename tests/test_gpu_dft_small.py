@@ -76,3 +76,17 @@ def test_coset_lde(ctx_passes, log_h, w, b):
         want = O.coset_lde(m, b, s)
         assert from_np(Radix2Dit(gpu_ctx).coset_lde_batch(x, b, s)) == want
         assert from_np(Radix2DitParallel(gpu_ctx).coset_lde_batch(x, b, s).storage) == O.bit_reverse_rows(want)
+
+
+@pytest.mark.parametrize("log_h,w,b", [(0, 1, 1), (1, 2, 2), (3, 3, 1), (5, 8, 2), (6, 9, 1), (7, 4, 3)])
+def test_coset_dft_padded(ctx_passes, log_h, w, b):
+    """coset_dft of the zero-padded coefficients (coset_lde_batch without its idft;
+    KzgPcs::get_evaluations_on_domain from committed coefficients)."""
+    gpu_ctx = ctx_passes
+    m = O.random_matrix(400 + log_h * 7 + w, 1 << log_h, w)
+    padded = m + [[0] * w for _ in range(((1 << log_h) << b) - (1 << log_h))]
+    x = to_np(m)
+    for s in (1, O.GENERATOR, 11 * O.two_adic_generator(log_h + b) % O.P):
+        want = O.coset_dft(padded, s)
+        assert from_np(Radix2Dit(gpu_ctx).coset_dft_padded_batch(x, b, s)) == want
+        assert from_np(Radix2DitParallel(gpu_ctx).coset_dft_padded_batch(x, b, s).storage) == O.bit_reverse_rows(want)

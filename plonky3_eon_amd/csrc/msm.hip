@@ -7,7 +7,9 @@
 // Pipeline (all on device, one stream):
 //   1. k_msm_digits     scalars (Montgomery) -> canonical -> signed c-bit digits; one
 //                       (bucket key, point reference | sign) pair per nonzero digit.
-//   2. radix sort       hipCUB DeviceRadixSort on the c-bit keys (zero digits sort last).
+//   2. radix sort       hipCUB DeviceRadixSort (stable onesweep) on the low c key bits of the
+//                       group-major pairs: buckets b' = magnitude * groups + group, zero digits
+//                       last (see k_msm_digits).
 //   3. k_bucket_start   bucket boundaries in the sorted pairs.
 //   4. pieces           a piece is the part of a bucket inside one chunk (2^log_chunk aligned
 //                       sorted pairs); exclusive scan of the per-bucket piece counts.
@@ -75,19 +77,26 @@ __device__ __forceinline__ uint32_t window_bits(const uint32_t* s, uint32_t pos,
     return (uint32_t)v & ((1u << c) - 1);
 }
 
-// One thread per (row i, MSM column col): the scalar is scalars[i * ld + col] (a row-major
-// matrix column; ld = 1, cols = 1 for a single MSM).  Group of a digit: the column (fixed-base
-// mode: every window shares the column's bucket set) or (column, window).
-__global__ void k_msm_digits(const Fr* scalars, uint64_t n, uint64_t ld, uint32_t cols, uint32_t c,
-                             uint32_t windows, uint32_t precomputed, uint32_t* keys, uint32_t* vals) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * cols) return;
-    const uint32_t col = (uint32_t)(t % cols);
-    const uint64_t i = t / cols;
+// Digit pairs.  Key of a nonzero digit: (group << c) | (|digit| - 1), group = the column
+// (fixed-base mode: every window shares the column's bucket set) or (column, window); zero digits
+// get the sentinel 0xFFFFFFFF.  Pairs are emitted group-major (e = group * n + i: (col * W + w) * n
+// + i in both modes) and radix-sorted on the low c key bits only -- 2 passes of the stable
+// onesweep instead of 3 on the full key -- so equal magnitudes stay in group order: the sorted
+// pairs run over buckets b' = (|digit| - 1) * groups + group, each contiguous.
+constexpr uint32_t DIGIT_COLS = 4;  // widest scalar tile of one 256-thread block: 64 rows x 4 cols
+
+__global__ void __launch_bounds__(256) k_msm_digits(const Fr* scalars, uint64_t n, uint64_t ld,
+                                                    uint32_t cols, uint32_t c, uint32_t windows,
+                                                    uint32_t precomputed, uint32_t tile_cols,
+                                                    uint32_t* keys, uint32_t* vals) {
+    // a block reads 256 / tile_cols row segments of tile_cols adjacent columns (up to 128
+    // contiguous bytes), so the group-major writes stay in runs of consecutive rows
+    const uint32_t col = blockIdx.y * tile_cols + threadIdx.x % tile_cols;
+    const uint64_t i = (uint64_t)blockIdx.x * (256 / tile_cols) + threadIdx.x / tile_cols;
+    if (col >= cols || i >= n) return;
     Fr s = to_canonical(ld_pinned(scalars + i * ld + col));
     pin(s);
     const uint32_t B = 1u << (c - 1);
-    const uint32_t sentinel = (precomputed ? cols : cols * windows) * B;
     uint32_t carry = 0;
     for (uint32_t w = 0; w < windows; w++) {
         const uint32_t raw = window_bits(s.v, w * c, c) + carry;
@@ -102,17 +111,22 @@ __global__ void k_msm_digits(const Fr* scalars, uint64_t n, uint64_t ld, uint32_
             neg = 0;
             carry = 0;
         }
-        const uint64_t e = ((uint64_t)w * n + i) * cols + col;
+        const uint64_t e = ((uint64_t)col * windows + w) * n + i;
         if (mag == 0) {
-            keys[e] = sentinel;
+            keys[e] = 0xFFFFFFFFu;
             vals[e] = 0;
         } else {
             const uint32_t g = precomputed ? col : col * windows + w;
-            keys[e] = g * B + mag - 1;
+            keys[e] = (g << c) | (mag - 1);
             const uint32_t ref = precomputed ? (uint32_t)(i * windows + w) : (uint32_t)i;
             vals[e] = ref | (neg << 31);
         }
     }
+}
+
+// bucket index b' of a sorted key (nb for the zero-digit sentinel)
+__device__ __forceinline__ uint32_t bucket_of(uint32_t key, uint32_t c, uint32_t groups, uint32_t nb) {
+    return key == 0xFFFFFFFFu ? nb : (key & ((1u << (c - 1)) - 1)) * groups + (key >> c);
 }
 
 // per-window sums -> per-column result: sum_w 2^(c*w) * G[col*W + w] (one thread per column)
@@ -129,12 +143,13 @@ __global__ void k_window_horner(const G1Xyzz* gs, uint32_t cols, uint32_t W, uin
     st_xyzz(out + col, acc);
 }
 
-// start[b] = index of the first sorted pair with key >= b, for b in [0, nb]
-__global__ void k_bucket_start(const uint32_t* keys, uint64_t E, uint32_t nb, uint32_t* start) {
+// start[b'] = index of the first sorted pair in bucket >= b', for b' in [0, nb]
+__global__ void k_bucket_start(const uint32_t* keys, uint64_t E, uint32_t c, uint32_t groups,
+                               uint32_t nb, uint32_t* start) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > E) return;
-    const int64_t prev = i == 0 ? -1 : (int64_t)min(keys[i - 1], nb);
-    const int64_t cur = i == E ? (int64_t)nb : (int64_t)min(keys[i], nb);
+    const int64_t prev = i == 0 ? -1 : (int64_t)bucket_of(keys[i - 1], c, groups, nb);
+    const int64_t cur = i == E ? (int64_t)nb : (int64_t)bucket_of(keys[i], c, groups, nb);
     for (int64_t b = prev + 1; b <= cur; b++) start[b] = (uint32_t)i;
 }
 
@@ -159,7 +174,8 @@ __global__ void k_chunk_count(const uint32_t* start, uint32_t nb, uint32_t log_c
 #endif
 __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum(const uint32_t* keys, const uint32_t* vals, const uint32_t* start,
                             const uint32_t* piece_off, uint32_t n_pairs, uint32_t log_chunk,
-                            const G1Affine* pts, G1Xyzz* piece_sums) {
+                            uint32_t c, uint32_t groups, uint32_t nb, const G1Affine* pts,
+                            G1Xyzz* piece_sums) {
     // grid-stride over chunks: a capped grid (EON_PIECE_WAVES) leaves wave slots for the
     // concurrent digit sort of the next batch
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; ((uint64_t)t << log_chunk) < n_pairs;
@@ -171,7 +187,8 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum(const uint
     for (uint32_t e = e0; e < e1; e++) {
         const uint32_t k = keys[e];
         if (k != b) {
-            st_xyzz(piece_sums + piece_off[b] + t - (start[b] >> log_chunk), acc);
+            const uint32_t bb = bucket_of(b, c, groups, nb);
+            st_xyzz(piece_sums + piece_off[bb] + t - (start[bb] >> log_chunk), acc);
             acc = xyzz_inf();
             b = k;
         }
@@ -180,7 +197,8 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum(const uint
         if (v >> 31) a = affine_neg(a);
         acc = xyzz_add_affine(acc, a);
     }
-    st_xyzz(piece_sums + piece_off[b] + t - (start[b] >> log_chunk), acc);
+    const uint32_t bb = bucket_of(b, c, groups, nb);
+    st_xyzz(piece_sums + piece_off[bb] + t - (start[bb] >> log_chunk), acc);
     }
 }
 
@@ -208,11 +226,13 @@ __global__ void k_level_count(const uint32_t* off, uint32_t nb, uint32_t* count)
 }
 
 // every bucket holds at most one partial: bucket_sums[b] = it, or the identity
-__global__ void k_bucket_final(const uint32_t* off, uint32_t nb, const G1Xyzz* partials,
-                               G1Xyzz* bucket_sums) {
+__global__ void k_bucket_final(const uint32_t* off, uint32_t B, uint32_t groups,
+                               const G1Xyzz* partials, G1Xyzz* bucket_sums) {
+    // bucket_sums is column-major (group * B + m) for the reduction; partials follow b' order
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
-    st_xyzz(bucket_sums + b, off[b + 1] > off[b] ? ld_xyzz(partials + off[b]) : xyzz_inf());
+    if (b >= B * groups) return;
+    const uint32_t bp = (b % B) * groups + b / B;
+    st_xyzz(bucket_sums + b, off[bp + 1] > off[bp] ? ld_xyzz(partials + off[bp]) : xyzz_inf());
 }
 
 // Segment s of group g covers buckets [lo, lo + SEG) (bucket b holds digit b + 1):
@@ -470,8 +490,10 @@ static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint6
     bt.nb = bt.groups * bt.B;
     bt.E = n * bt.W * bt.cols;
     if (bt.E >= (1ull << 32)) return Status::err(EON_E_SHAPE, "MSM too large for 32-bit pair indices");
-    bt.key_bits = 1;
-    while ((1ull << bt.key_bits) <= bt.nb) bt.key_bits++;
+    // keys are (group << c) | (|digit| - 1); only the low c bits are sorted
+    if (((uint64_t)bt.groups << bt.c) > 0xFFFFFFFFull)
+        return Status::err(EON_E_SHAPE, "too many MSM groups for 32-bit digit keys");
+    bt.key_bits = bt.c;
     const uint64_t E = bt.E;
     const uint32_t nb = bt.nb;
 
@@ -500,9 +522,12 @@ static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint6
 
     Profiler* prof = &ctx->prof;
     prof->begin("k_msm_digits", n * bt.cols * 32 + E * 8, st);
-    hipLaunchKernelGGL(k_msm_digits, dim3(blocks_for(n * bt.cols, 256)), dim3(256), 0, st, bt.scalars,
-                       n, ld, bt.cols, bt.c, bt.W, (uint32_t)b->precomputed, wk.keys.as<uint32_t>(),
-                       wk.vals.as<uint32_t>());
+    const uint32_t tile_cols = bt.cols >= DIGIT_COLS ? DIGIT_COLS : (bt.cols >= 2 ? 2 : 1);
+    const uint32_t tile_rows = 256 / tile_cols;
+    hipLaunchKernelGGL(k_msm_digits, dim3((unsigned)((n + tile_rows - 1) / tile_rows),
+                                          (bt.cols + tile_cols - 1) / tile_cols),
+                       dim3(256), 0, st, bt.scalars, n, ld, bt.cols, bt.c, bt.W, (uint32_t)b->precomputed,
+                       tile_cols, wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>());
     prof->end(st);
     EON_HIP(hipGetLastError());
     prof->begin("radix_sort_pairs", E * 16, st);
@@ -511,7 +536,7 @@ static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint6
                                                wk.vals2.as<uint32_t>(), (int)E, 0, bt.key_bits, st));
     prof->end(st);
     hipLaunchKernelGGL(k_bucket_start, dim3(blocks_for(E + 1, 256)), dim3(256), 0, st,
-                       wk.keys2.as<uint32_t>(), E, nb, wk.start.as<uint32_t>());
+                       wk.keys2.as<uint32_t>(), E, bt.c, bt.groups, nb, wk.start.as<uint32_t>());
     hipLaunchKernelGGL(k_chunk_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st,
                        wk.start.as<uint32_t>(), nb, bt.log_chunk, wk.count.as<uint32_t>());
     EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, bt.scan_bytes, wk.count.as<uint32_t>(),
@@ -543,7 +568,7 @@ static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt
         hipLaunchKernelGGL(k_piece_sum, dim3(blocks),
                            dim3(64), 0, st, wk.keys2.as<uint32_t>(), wk.vals2.as<uint32_t>(),
                            wk.start.as<uint32_t>(), wk.piece_off.as<uint32_t>(), bt.n_pairs,
-                           bt.log_chunk, pts, wk.piece_sums.as<G1Xyzz>());
+                           bt.log_chunk, bt.c, bt.groups, bt.nb, pts, wk.piece_sums.as<G1Xyzz>());
     ctx->prof.end(st);
     EON_HIP(hipGetLastError());
     return Status::ok();
@@ -620,7 +645,7 @@ static Status batch_reduce(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, MsmW
         std::swap(part_cur, part_nxt);
         n_pieces = n_new;
     }
-    hipLaunchKernelGGL(k_bucket_final, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_cur, nb,
+    hipLaunchKernelGGL(k_bucket_final, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_cur, B, groups,
                        part_cur, wk.bucket_sums.as<G1Xyzz>());
     if (groups < 64) return reduce_segments(ctx, b, bt, wk, st);
     // sum_d d * B_d = W(S) + T(S) per group (bucket b holds digit b + 1), level by level

@@ -143,14 +143,27 @@ __global__ void k_window_horner(const G1Xyzz* gs, uint32_t cols, uint32_t W, uin
     st_xyzz(out + col, acc);
 }
 
-// start[b'] = index of the first sorted pair in bucket >= b', for b' in [0, nb]
+// start[b'] = index of the first sorted pair in bucket >= b', for b' in [0, nb]; each thread
+// handles 4 consecutive pairs with one 16-byte load (E is a multiple of 4 or handled per element)
 __global__ void k_bucket_start(const uint32_t* keys, uint64_t E, uint32_t c, uint32_t groups,
                                uint32_t nb, uint32_t* start) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > E) return;
-    const int64_t prev = i == 0 ? -1 : (int64_t)bucket_of(keys[i - 1], c, groups, nb);
-    const int64_t cur = i == E ? (int64_t)nb : (int64_t)bucket_of(keys[i], c, groups, nb);
-    for (int64_t b = prev + 1; b <= cur; b++) start[b] = (uint32_t)i;
+    const uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i0 > E) return;
+    uint32_t k[4];
+    if (i0 + 4 <= E && (E & 3) == 0) {
+        const uint4 q = *reinterpret_cast<const uint4*>(keys + i0);
+        k[0] = q.x; k[1] = q.y; k[2] = q.z; k[3] = q.w;
+    } else {
+        for (int j = 0; j < 4; j++) k[j] = i0 + j < E ? keys[i0 + j] : 0u;
+    }
+    int64_t prev = i0 == 0 ? -1 : (int64_t)bucket_of(keys[i0 - 1], c, groups, nb);
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint64_t i = i0 + j;
+        if (i > E) break;
+        const int64_t cur = i == E ? (int64_t)nb : (int64_t)bucket_of(k[j], c, groups, nb);
+        for (int64_t b = prev + 1; b <= cur; b++) start[b] = (uint32_t)i;
+        prev = cur;
+    }
 }
 
 __global__ void k_piece_owner(const uint32_t* piece_off, uint32_t nb, uint32_t* owner) {
@@ -535,7 +548,7 @@ static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint6
                                                wk.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
                                                wk.vals2.as<uint32_t>(), (int)E, 0, bt.key_bits, st));
     prof->end(st);
-    hipLaunchKernelGGL(k_bucket_start, dim3(blocks_for(E + 1, 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_bucket_start, dim3(blocks_for(E / 4 + 1, 256)), dim3(256), 0, st,
                        wk.keys2.as<uint32_t>(), E, bt.c, bt.groups, nb, wk.start.as<uint32_t>());
     hipLaunchKernelGGL(k_chunk_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st,
                        wk.start.as<uint32_t>(), nb, bt.log_chunk, wk.count.as<uint32_t>());

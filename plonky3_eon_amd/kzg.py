@@ -132,28 +132,51 @@ class GpuKzgPcs:
         return self.commit(list(zip(quotient_domain.split_domains(num_chunks), chunks)))
 
     def open(self, rounds):
-        """rounds: [(prover_data, points_per_matrix)] -> (opened values, witnesses) per round."""
+        """rounds: [(prover_data, points_per_matrix)] -> (opened values, witnesses) per round.
+
+        pcs.rs:289-335 computes, per (matrix, point), every column's synthetic-division quotient
+        and commits each one.  All quotients of one height share the SRS prefix, so they are
+        gathered into one matrix and committed by ONE batched column MSM (one pipeline fill and
+        drain instead of one per (matrix, point))."""
         import torch
 
-        out = []
-        for prover_data, points_per_matrix in rounds:
+        jobs = []  # (round, matrix, point index, height n, width w)
+        for ri, (prover_data, points_per_matrix) in enumerate(rounds):
             if len(prover_data) != len(points_per_matrix):
                 raise _lib.EonError(_lib.EON_E_SHAPE, "one point list per matrix")
-            r = Opened()
-            for m, points in zip(prover_data, points_per_matrix):
-                n, w = int(m.coeffs.shape[0]), int(m.coeffs.shape[1])
-                vals, wits = [], []
-                for z in points:
-                    quo = torch.empty((max(n - 1, 1), w, 4), dtype=torch.int64, device=m.coeffs.device)
-                    v = torch.empty((w, 4), dtype=torch.int64, device=m.coeffs.device)
-                    pz = fr_to_abi(z)
-                    self.ctx.set_stream(torch.cuda.current_stream(m.coeffs.device).cuda_stream)
-                    self.ctx.check(self.ctx.lib.eon_quotient_and_eval_columns_dev(
-                        self.ctx.handle, ctypes.c_void_p(m.coeffs.data_ptr()), n, w, ctypes.byref(pz),
-                        ctypes.c_void_p(quo.data_ptr()), ctypes.c_void_p(v.data_ptr())))
-                    wits.append(self.bases.msm_columns(quo[:n - 1]))
-                    vals.append(v.cpu().numpy().view(np.uint64))
-                r.values.append(vals)
-                r.witnesses.append(wits)
-            out.append(r)
+            for mi, (m, points) in enumerate(zip(prover_data, points_per_matrix)):
+                for pi in range(len(points)):
+                    jobs.append((ri, mi, pi, int(m.coeffs.shape[0]), int(m.coeffs.shape[1])))
+        # one witness matrix per quotient height n - 1, columns in job order
+        groups = {}
+        for j in jobs:
+            groups.setdefault(j[3], []).append(j)
+        mats, col0 = {}, {}
+        for n, js in groups.items():
+            dev = rounds[js[0][0]][0][js[0][1]].coeffs.device
+            mats[n] = torch.empty((max(n - 1, 1), sum(j[4] for j in js), 4), dtype=torch.int64, device=dev)
+            c = 0
+            for j in js:
+                col0[j[:3]] = c
+                c += j[4]
+        out = [Opened(values=[[None] * len(pts) for pts in p], witnesses=[[None] * len(pts) for pts in p])
+               for _, p in rounds]
+        for ri, mi, pi, n, w in jobs:
+            m = rounds[ri][0][mi]
+            z = rounds[ri][1][mi][pi]
+            quo = torch.empty((max(n - 1, 1), w, 4), dtype=torch.int64, device=m.coeffs.device)
+            v = torch.empty((w, 4), dtype=torch.int64, device=m.coeffs.device)
+            pz = fr_to_abi(z)
+            self.ctx.set_stream(torch.cuda.current_stream(m.coeffs.device).cuda_stream)
+            self.ctx.check(self.ctx.lib.eon_quotient_and_eval_columns_dev(
+                self.ctx.handle, ctypes.c_void_p(m.coeffs.data_ptr()), n, w, ctypes.byref(pz),
+                ctypes.c_void_p(quo.data_ptr()), ctypes.c_void_p(v.data_ptr())))
+            c = col0[(ri, mi, pi)]
+            mats[n][:, c:c + w] = quo
+            out[ri].values[mi][pi] = v.cpu().numpy().view(np.uint64)
+        for n, js in groups.items():
+            wits = self.bases.msm_columns(mats[n][:n - 1])
+            for ri, mi, pi, _, w in js:
+                c = col0[(ri, mi, pi)]
+                out[ri].witnesses[mi][pi] = wits[c:c + w]
         return out

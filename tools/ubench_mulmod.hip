@@ -24,6 +24,39 @@ __global__ void __launch_bounds__(256) k_mul(const Fe<M>* in, Fe<M>* out, int it
     out[tid] = acc;
 }
 
+// the FIPS product followed by 64 extra s_nop 0: prices one s_nop in the mulmod stream
+template <class M>
+__global__ void __launch_bounds__(256) k_mul_nops(const Fe<M>* in, Fe<M>* out, int iters) {
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    Fe<M> y = in[(tid + 7) & 1023];
+    Fe<M> x0 = in[tid & 1023], x1 = in[(tid + 1) & 1023];
+    for (int it = 0; it < iters; it++) {
+        x0 = mul_fips(x0, y);
+        asm volatile(".rept 32\n\ts_nop 0\n\t.endr");
+        x1 = mul_fips(x1, y);
+        asm volatile(".rept 32\n\ts_nop 0\n\t.endr");
+    }
+    out[tid] = add(x0, x1);
+}
+
+template <class M>
+void run_nops(const char* name, Fe<M>* d_in, Fe<M>* d_out, int blocks, int iters) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    k_mul_nops<M><<<blocks, 256>>>(d_in, d_out, 16);
+    hipDeviceSynchronize();
+    hipEventRecord(a);
+    k_mul_nops<M><<<blocks, 256>>>(d_in, d_out, iters);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    double n = (double)blocks * 256 * iters * 2;
+    printf("{\"field\":\"%s\",\"fips\":\"+64nops\",\"chains\":2,\"blocks\":%d,\"ms\":%.3f,\"mulmod_per_s\":%.4e}\n", name,
+           blocks, ms, n / (ms * 1e-3));
+}
+
 template <class M>
 __global__ void k_check(const Fe<M>* a, const Fe<M>* b, int n, unsigned* bad, Fe<M>* out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -96,6 +129,7 @@ int main() {
         run<FrP, 1, true>("Fr", d_in, d_out, blocks, 4096);
         run<FrP, 2, true>("Fr", d_in, d_out, blocks, 2048);
         run<FrP, 4, true>("Fr", d_in, d_out, blocks, 1024);
+        run_nops<FrP>("Fr", d_in, d_out, blocks, 2048);
     }
     return 0;
 }

@@ -144,6 +144,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         f.load_scale = table;
         a.max_stages_per_pass = f.max_stages_per_pass = ctx->ntt_max_stages;
         a.max_threads = f.max_threads = ctx->ntt_tpb;
+        a.log_tile = f.log_tile = ctx->ntt_log_tile;
         a.log_cb_override = f.log_cb_override = ctx->ntt_log_cb;
         EON_HIP(run_network(a, st, &ctx->prof));
         EON_HIP(run_network(f, st, &ctx->prof));
@@ -176,6 +177,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         }
         f.max_stages_per_pass = ctx->ntt_max_stages;
         f.max_threads = ctx->ntt_tpb;
+        f.log_tile = ctx->ntt_log_tile;
         f.log_cb_override = ctx->ntt_log_cb;
         EON_HIP(run_network(f, st, &ctx->prof));
         return Status::ok();
@@ -215,6 +217,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
     }
     s.max_stages_per_pass = ctx->ntt_max_stages;
     s.max_threads = ctx->ntt_tpb;
+    s.log_tile = ctx->ntt_log_tile;
     s.log_cb_override = ctx->ntt_log_cb;
     EON_HIP(run_network(s, st, &ctx->prof));
     return Status::ok();
@@ -309,6 +312,7 @@ int eon_ctx_create(int device_ordinal, eon_ctx** out) {
     }
     if (const char* e = getenv("EON_NTT_MAX_STAGES")) c->ntt_max_stages = (uint32_t)atoi(e);
     if (const char* e = getenv("EON_NTT_TPB")) c->ntt_tpb = (uint32_t)atoi(e);
+    if (const char* e = getenv("EON_NTT_TILE")) c->ntt_log_tile = (uint32_t)atoi(e);
     if (const char* e = getenv("EON_NTT_LOG_CB")) c->ntt_log_cb = atoi(e) > 3 ? 3 : atoi(e);
     *out = c;
     return EON_OK;

@@ -95,6 +95,7 @@ struct eon_ctx {
     uint32_t ntt_max_stages = 0;
     // EON_NTT_TPB / EON_NTT_LOG_CB: tuning knobs (threads per block cap, columns per tile)
     uint32_t ntt_tpb = 0;
+    uint32_t ntt_log_tile = 0;  // EON_NTT_TILE: log2 elements per LDS tile (0 = 10)
     int ntt_log_cb = -1;
 
     // per-launch HIP-event timing (eon_ctx_profile_*)

@@ -39,7 +39,8 @@ struct NetworkSpec {
     Fr load_const = Fr::one();
     const Fr* store_scale = nullptr;
     uint32_t max_stages_per_pass = 0;  // 0 = tile limit; tests force multi-pass plans with it
-    uint32_t max_threads = 0;          // 0 = default (512); tuning knob
+    uint32_t max_threads = 0;          // 0 = default (512, 1024 for 2048-element tiles); tuning knob
+    uint32_t log_tile = 0;             // log2 elements per LDS tile (0 = 10); tuning knob
     int log_cb_override = -1;          // columns per tile = 2^log_cb; -1 = by width
 };
 

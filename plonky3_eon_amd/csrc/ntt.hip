@@ -34,6 +34,7 @@ struct PassArgs {
     uint32_t load_mode;
     uint32_t load_param;
     uint32_t has_load_const;
+    uint32_t col_tiles;
 };
 
 __device__ __forceinline__ void lds_put(uint4* lo, uint4* hi, uint32_t i, const Fr& x) {
@@ -65,7 +66,7 @@ __device__ __forceinline__ void gstore(Fr* p, const Fr& x) {
 }
 
 template <bool DIF, int LOG_CB>
-__global__ void __launch_bounds__(512) k_ntt_pass(PassArgs a) {
+__global__ void __launch_bounds__(1024) k_ntt_pass(PassArgs a) {
     constexpr uint32_t CB = 1u << LOG_CB;
     extern __shared__ __attribute__((aligned(16))) uint4 lds[];
     const uint32_t k = a.k;
@@ -75,10 +76,12 @@ __global__ void __launch_bounds__(512) k_ntt_pass(PassArgs a) {
     Fr* twl = reinterpret_cast<Fr*>(lds + 2 * ne);
 
     const uint32_t s0 = a.s0;
-    const uint64_t g = blockIdx.x;
+    // one-dimensional grid, column tile fastest: the tiles sharing a row segment's cache lines
+    // run together
+    const uint64_t g = blockIdx.x / a.col_tiles;
     const uint64_t low = g & ((1ull << s0) - 1);
     const uint64_t base_row = low + ((g >> s0) << (s0 + k));
-    const uint64_t col0 = (uint64_t)blockIdx.y * CB;
+    const uint64_t col0 = (uint64_t)(blockIdx.x % a.col_tiles) * CB;
     const uint64_t width = a.width;
     const uint32_t T = blockDim.x;
 
@@ -214,7 +217,7 @@ static hipError_t launch_pass(bool dif, uint32_t log_cb, const PassArgs& a, uint
     if (threads > max_threads) threads = max_threads;
     if (threads < 64) threads = 64;
     const size_t lds = (size_t)ne * 32 + ((size_t)1 << a.k) * 32;
-    dim3 grid((unsigned)groups, (unsigned)col_tiles);
+    dim3 grid((unsigned)(groups * col_tiles));
 #define EON_LAUNCH(D, C) \
     hipLaunchKernelGGL((k_ntt_pass<D, C>), grid, dim3(threads), lds, st, a)
     switch ((dif ? 4 : 0) + log_cb) {
@@ -262,7 +265,8 @@ static uint32_t pick_log_cb(uint64_t width) {
 
 hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
     const uint32_t log_cb = s.log_cb_override >= 0 ? (uint32_t)s.log_cb_override : pick_log_cb(s.width);
-    uint32_t kmax = 10 - log_cb;  // 1024 elements per tile (32 KiB of LDS)
+    const uint32_t log_tile = s.log_tile ? s.log_tile : 10;  // 2^10 elements per tile: 32 KiB of LDS
+    uint32_t kmax = log_tile > log_cb ? log_tile - log_cb : 1;
     if (s.max_stages_per_pass && s.max_stages_per_pass < kmax) kmax = s.max_stages_per_pass;
     const uint32_t lo_stage = s.first_stage;
     const uint32_t n_st = s.log_m > lo_stage ? s.log_m - lo_stage : 0;
@@ -307,7 +311,9 @@ hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
         const uint64_t mm = elems / 2 * a.k + (a.load_scale ? elems : 0) + (a.has_load_const ? elems : 0) +
                             (a.store_scale ? elems : 0);
         if (prof) prof->begin(names[(s.dif ? 4 : 0) + log_cb], 64ull * elems, st, mm);
-        hipError_t e = launch_pass(s.dif, log_cb, a, groups, col_tiles, s.max_threads ? s.max_threads : 512, st);
+        a.col_tiles = (uint32_t)col_tiles;
+        const uint32_t tpb = s.max_threads ? s.max_threads : (log_tile > 10 ? 1024 : 512);
+        hipError_t e = launch_pass(s.dif, log_cb, a, groups, col_tiles, tpb, st);
         if (prof) prof->end(st);
         if (e != hipSuccess) return e;
     }

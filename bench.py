@@ -262,7 +262,10 @@ class ProveWorkload:
     """configs[3]: eon-uni-stark prove of the vectorized Poseidon2-AIR (VECTOR_LEN 8, 2^(log_n+3)
     permutations, log-trace-length log_n) with KzgPcs over BN254 (SRS max_degree 2^log_n,
     alpha 12345); alpha / zeta fixed (transcript out of scope).  At N > 1 the ONE proof is split
-    by vector lane over the ranks (plonky3_eon_amd/distributed.py): strong scaling."""
+    by vector lane over the ranks (plonky3_eon_amd/distributed.py): strong scaling.
+
+    --host native (default) runs the C++ prove driver (libeonprove.so, include/eon_prove.h; at N > 1
+    its own RCCL all-gathers); --host python the Python mirror (prover.py).  Same proof."""
 
     scaling = "strong"
 
@@ -281,7 +284,21 @@ class ProveWorkload:
         l0, l1 = self.shard.lanes if self.shard else (0, self.vl)
         self.consts = p2_constants_limbs(99)
         self.air = Poseidon2Air(*self.consts, l1 - l0, ctx)
-        self.pcs = GpuKzgPcs(n, 12345, ctx)
+        self.native = args.host == "native"
+        if self.native:
+            from plonky3_eon_amd.native import NativeKzgPcs, RcclCollective
+
+            from plonky3_eon_amd.native import TorchCollective
+
+            self.pcs = NativeKzgPcs(n, 12345, ctx)
+            self.coll = None
+            if world > 1:
+                # torch's RCCL process group (all_gather_into_tensor on device) by default; the
+                # driver's own communicator with --collective rccl
+                self.coll = (RcclCollective(rank, world) if args.collective == "rccl"
+                             else TorchCollective(rank, world, None, device=dev.index))
+        else:
+            self.pcs = GpuKzgPcs(n, 12345, ctx)
         # the same 2^(log_n) x VECTOR_LEN permutation inputs on every rank; rank g takes its lanes
         # (permutation j sits at row j / VECTOR_LEN, lane j % VECTOR_LEN)
         inputs = synthetic_fr(n * self.vl, 3, 5).reshape(n, self.vl, 3, 4)[:, l0:l1]
@@ -294,7 +311,12 @@ class ProveWorkload:
     def step(self):
         from plonky3_eon_amd.prover import prove
 
-        p = prove(self.air, self.pcs, self.trace, self.alpha, self.zeta, shard=self.shard)
+        if self.native:
+            from plonky3_eon_amd.native import prove_native
+
+            p = prove_native(self.air, self.pcs, self.trace, self.alpha, self.zeta, collective=self.coll)
+        else:
+            p = prove(self.air, self.pcs, self.trace, self.alpha, self.zeta, shard=self.shard)
         self.timings.append(p.timings_ms)
 
     def describe(self, world):
@@ -451,6 +473,11 @@ def main() -> int:
     ap.add_argument("--log-msm", type=int, default=20)
     ap.add_argument("--cpu-sample-cols", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host", choices=["native", "python"], default="native",
+                    help="prove: C++ driver (libeonprove.so) or the Python mirror")
+    ap.add_argument("--collective", choices=["torch", "rccl"], default="torch",
+                    help="prove --host native at N > 1: all-gathers through torch.distributed (RCCL "
+                         "process group) or the driver's own RCCL communicator")
     args = ap.parse_args()
     if args.steps is None:
         args.steps = 3 if args.workload == "prove" else 10

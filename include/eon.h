@@ -67,6 +67,8 @@ const char* eon_last_error(const eon_ctx* ctx);
 /* Stream (a hipStream_t) for all subsequent work of this context, used verbatim: NULL selects
  * the HIP null (default) stream.  Until the first call the context uses a stream of its own. */
 int eon_ctx_set_stream(eon_ctx* ctx, void* hip_stream);
+/* The stream the context currently enqueues on (as set, or its own). */
+void* eon_ctx_stream(eon_ctx* ctx);
 int eon_ctx_synchronize(eon_ctx* ctx);
 /* Per-launch kernel timing with HIP events on the launch stream (the analogue of the
  * reference's tracing spans, e.g. dft/src/radix_2_dit_parallel.rs:168).  eon_ctx_profile(ctx, 1)
@@ -190,6 +192,10 @@ int eon_p2air_create(eon_ctx* ctx, const eon_poseidon2_constants* constants, uin
 void eon_p2air_destroy(eon_p2air* air);
 /* trace width: (4 + 12 * half_full_rounds + 2 * partial_rounds) * vector_len (164 * vector_len) */
 uint32_t eon_p2air_width(const eon_p2air* air);
+/* VECTOR_LEN, and the constraints of one permutation: 12 * half_full_rounds + 2 * partial_rounds
+ * (160; the folder's per-lane block, eon-uni-stark/src/folder.rs:81-85) */
+uint32_t eon_p2air_vector_len(const eon_p2air* air);
+uint32_t eon_p2air_constraints_per_perm(const eon_p2air* air);
 /* generate_vectorized_trace_rows (poseidon2-air/src/generation.rs:14-72): inputs n_perms x 3 Fr
  * (device), trace (n_perms / vector_len) x width (device); n_perms = vector_len * 2^k. */
 int eon_p2air_generate_trace_dev(eon_ctx* ctx, const eon_p2air* air, const eon_fr* inputs,

@@ -1,0 +1,90 @@
+/*
+ * eon_prove.h -- C ABI of the native prove driver (libeonprove.so), the host side ABOVE eon.h.
+ *
+ * The reference's prover is compiled Rust; its toolchain is absent here, so the orchestration is
+ * C++ (plonky3_eon_amd/host/) calling only the eon.h entry points, with the reference's shapes:
+ *   eon_kzg_pcs      KzgPcs (kzg/src/pcs.rs:143-402) with the test SRS init_srs_unsafe
+ *                    (kzg/src/params.rs:123-139): commit / get_evaluations_on_domain /
+ *                    commit_quotient / open of the Pcs trait (commit/src/pcs.rs:21-187)
+ *   eon_prove_p2air  prove_with_preprocessed (eon-uni-stark/src/prover.rs:28-512) for the
+ *                    Poseidon2-AIR: no preprocessed columns, no lookups,
+ *                    ZK off, Challenge = Fr.  alpha and zeta are inputs (the DuplexChallenger
+ *                    transcript is SURVEY.md 8(f) N2, not built).
+ * Conventions are eon.h's: 0 / negative EON_E_* codes (the reference panics), host outputs,
+ * device inputs, work on the context's stream.
+ */
+#ifndef EON_PROVE_H
+#define EON_PROVE_H
+
+#include <stdint.h>
+
+#include "eon.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct eon_kzg_pcs eon_kzg_pcs;
+
+/* KzgPcs::new(max_degree, alpha): SRS g1_powers[0..=max_degree] generated and kept on device as
+ * fixed-base MSM bases (alpha is a host pointer). */
+int eon_kzg_pcs_create(eon_ctx* ctx, uint64_t max_degree, const eon_fr* srs_alpha, eon_kzg_pcs** out);
+void eon_kzg_pcs_destroy(eon_kzg_pcs* pcs);
+/* message of the last failing call on this pcs (driver-side errors and eon.h errors) */
+const char* eon_kzg_pcs_last_error(const eon_kzg_pcs* pcs);
+
+/* Lane-sharded prove: this rank's share of VECTOR_LEN and an all-gather over
+ * DEVICE buffers -- recv receives `world` blocks of `bytes`, in rank order.  The driver calls it
+ * with the context's stream; it must leave recv complete and ordered before that stream's later
+ * work (an RCCL all-gather enqueued on `hip_stream` does; a host-staged one synchronizes). */
+typedef struct {
+    uint32_t rank;
+    uint32_t world;
+    int (*all_gather)(void* user, const void* send, void* recv, uint64_t bytes, void* hip_stream);
+    void* user;
+} eon_collective;
+
+/* An RCCL (NCCL API over xGMI) all-gather for eon_collective: rank 0 creates the unique id
+ * (128 bytes), every rank receives it out of band (e.g. torch.distributed) and initialises its
+ * communicator on the current HIP device (the context's). */
+int eon_rccl_unique_id(uint8_t id[128]);
+int eon_rccl_collective_init(uint32_t rank, uint32_t world, const uint8_t id[128], eon_collective* out);
+void eon_rccl_collective_finalize(eon_collective* coll);
+
+enum {
+    EON_STAGE_COMMIT_TRACE = 0,    /* "commit to trace data" (prover.rs:186-187) */
+    EON_STAGE_TRACE_LDE = 1,       /* get_evaluations_on_domain (prover.rs:315) */
+    EON_STAGE_QUOTIENT = 2,        /* quotient_values (prover.rs:328-342) */
+    EON_STAGE_EXCHANGE = 3,        /* sharded: all-gather + combine of partial quotients */
+    EON_STAGE_COMMIT_QUOTIENT = 4, /* "commit to quotient poly chunks" (prover.rs:371-372) */
+    EON_STAGE_OPEN = 5,            /* "open" (prover.rs:424-442) */
+    EON_STAGE_ASSEMBLE = 6,        /* sharded: all-gather of per-column results */
+    EON_STAGES = 8
+};
+
+/* Proof fields (eon-uni-stark/src/proof.rs:19-44), caller-allocated host arrays; W is the FULL
+ * trace width (164 * VECTOR_LEN over all ranks), C = 2^log_qd quotient chunks (2 for degree 3). */
+typedef struct {
+    eon_g1_affine* trace_commit;       /* [W] */
+    eon_g1_affine* quotient_commit;    /* [C] */
+    eon_fr* trace_opened;              /* [2][W]: values at zeta, zeta * h */
+    eon_g1_affine* trace_witnesses;    /* [2][W] */
+    eon_fr* quotient_opened;           /* [C]: chunk c at zeta */
+    eon_g1_affine* quotient_witnesses; /* [C] */
+    uint32_t degree_bits;              /* out: log2 of the trace height */
+    double stage_ms[EON_STAGES];       /* out: host clock around each stage (device synchronized) */
+} eon_proof;
+
+/* prove: `trace` is this rank's (height x width(air)) trace on device; `alpha`, `zeta` host.
+ * `shard` NULL = the whole AIR on this device.  max_constraint_degree = 3 for the Poseidon2-AIR
+ * (log_qd = 1, get_log_quotient_degree, symbolic_builder.rs:15-43). */
+int eon_prove_p2air(eon_kzg_pcs* pcs, const eon_p2air* air, const eon_fr* trace, uint64_t height,
+                    const eon_fr* alpha, const eon_fr* zeta, uint32_t max_constraint_degree,
+                    const eon_collective* shard, eon_proof* out);
+
+uint32_t eon_prove_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EON_PROVE_H */

@@ -1,7 +1,12 @@
-"""Builds libeonhip.so (the C-ABI shared library, include/eon.h) in-tree for gfx950.
+"""Builds the two in-tree shared libraries for gfx950:
 
-Each translation unit is compiled with hipcc --offload-arch=gfx950 into build/, then linked
-into plonky3_eon_amd/libeonhip.so.  Objects are rebuilt only when a source or header is newer.
+* libeonhip.so   -- the C-ABI hot path (include/eon.h): the HIP kernels in csrc/*.hip;
+* libeonprove.so -- the native prove driver above it (include/eon_prove.h): host C++ in
+                    host/*.cpp that calls only eon.h (linked against libeonhip.so, $ORIGIN rpath)
+                    and RCCL for the sharded prove's all-gathers.
+
+Each translation unit is compiled with hipcc into build/, then linked.  Objects are rebuilt only
+when a source or header is newer.
 """
 
 from __future__ import annotations
@@ -16,6 +21,9 @@ ROOT = PKG.parent
 CSRC = PKG / "csrc"
 BUILD = ROOT / "build" / "eonhip"
 LIB = PKG / "libeonhip.so"
+HOST = PKG / "host"
+BUILD_HOST = ROOT / "build" / "eonprove"
+PROVE_LIB = PKG / "libeonprove.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
@@ -27,15 +35,15 @@ def sources():
 
 
 def _headers_mtime() -> float:
-    hs = list(CSRC.glob("*.h")) + list((ROOT / "include").glob("*.h"))
+    hs = list(CSRC.glob("*.h")) + list(HOST.glob("*.h")) + list((ROOT / "include").glob("*.h"))
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
-def _compile(src: Path) -> Path:
-    obj = BUILD / (src.stem + ".o")
+def _compile(src: Path, out_dir: Path = BUILD, extra=()) -> Path:
+    obj = out_dir / (src.stem + ".o")
     if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
         return obj
-    cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *FLAGS, *extra, "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")
@@ -53,9 +61,26 @@ def build(verbose: bool = False) -> Path:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    _build_prove_driver()
     if verbose:
-        print(f"built {LIB}")
+        print(f"built {LIB} and {PROVE_LIB}")
     return LIB
+
+
+def _build_prove_driver() -> Path:
+    """libeonprove.so: host C++ only (no kernels); hipcc supplies the HIP runtime headers."""
+    BUILD_HOST.mkdir(parents=True, exist_ok=True)
+    srcs = sorted(HOST.glob("*.cpp"))
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(lambda p: _compile(p, BUILD_HOST, ("-I" + str(HOST),)), srcs))
+    newest = max([o.stat().st_mtime for o in objs] + [LIB.stat().st_mtime])
+    if not PROVE_LIB.exists() or PROVE_LIB.stat().st_mtime < newest:
+        cmd = [HIPCC, "-shared", "-fPIC", *map(str, objs), "-o", str(PROVE_LIB), "-L" + str(PKG), "-leonhip",
+               "-lrccl", "-Wl,-rpath,$ORIGIN"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed (libeonprove.so):\n{r.stderr[-6000:]}")
+    return PROVE_LIB
 
 
 def build_variant(name: str, defines: list[str]) -> Path:

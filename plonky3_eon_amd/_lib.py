@@ -64,6 +64,7 @@ SIGNATURES = {
     "eon_ctx_destroy": (None, [_P]),
     "eon_last_error": (ctypes.c_char_p, [_P]),
     "eon_ctx_set_stream": (_INT, [_P, _P]),
+    "eon_ctx_stream": (_P, [_P]),
     "eon_ctx_synchronize": (_INT, [_P]),
     "eon_ctx_profile": (_INT, [_P, _INT]),
     "eon_ctx_profile_report": (_INT, [_P, ctypes.c_char_p, _U64]),
@@ -95,6 +96,8 @@ SIGNATURES = {
     "eon_p2air_create": (_INT, [_P, _P, _U32, ctypes.POINTER(_P)]),
     "eon_p2air_destroy": (None, [_P]),
     "eon_p2air_width": (_U32, [_P]),
+    "eon_p2air_vector_len": (_U32, [_P]),
+    "eon_p2air_constraints_per_perm": (_U32, [_P]),
     "eon_p2air_generate_trace_dev": (_INT, [_P, _P, _P, _U64, _P]),
     "eon_p2air_quotient_values_dev": (_INT, [_P, _P, _P, _U32, _U32, _P, _P]),
     "eon_fr_lincomb_dev": (_INT, [_P, _P, _U32, _U64, _P, _P]),

@@ -363,6 +363,12 @@ int eon_ctx_set_stream(eon_ctx* ctx, void* hip_stream) {
     return EON_OK;
 }
 
+void* eon_ctx_stream(eon_ctx* ctx) {
+    if (!ctx) return nullptr;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return reinterpret_cast<void*>(ctx->stream);
+}
+
 int eon_ctx_synchronize(eon_ctx* ctx) {
     if (!ctx) return EON_E_ARG;
     std::lock_guard<std::mutex> lk(ctx->mu);

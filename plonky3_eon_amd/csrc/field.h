@@ -231,6 +231,9 @@ EON_HD Fe<M> mul(const Fe<M>& a, const Fe<M>& b) {
 #endif
 }
 
+// A dedicated square (36 + 64 products instead of 128) measured slower than mul(a, a) on gfx950:
+// the doubling adds VOP3 instructions that cost what the saved products did
+// (tools/ubench_mulmod.hip, profiles/r01_ubench_isa.txt).
 template <class M>
 EON_HD Fe<M> sqr(const Fe<M>& a) {
     return mul(a, a);

@@ -348,6 +348,12 @@ uint32_t eon_p2air_width(const eon_p2air* air) {
     return air ? (1 + 3 + 12 * air->hf + 2 * air->pr) * air->vl : 0;
 }
 
+uint32_t eon_p2air_vector_len(const eon_p2air* air) { return air ? air->vl : 0; }
+
+uint32_t eon_p2air_constraints_per_perm(const eon_p2air* air) {
+    return air ? 12 * air->hf + 2 * air->pr : 0;
+}
+
 int eon_p2air_generate_trace_dev(eon_ctx* ctx, const eon_p2air* air, const eon_fr* inputs,
                                  uint64_t n_perms, eon_fr* trace) {
     if (!ctx || !air) return EON_E_ARG;

@@ -1,0 +1,231 @@
+// KzgPcs over eon.h (see pcs.h).  Reference: kzg/src/pcs.rs, commit/src/{pcs,domain}.rs.
+#include "pcs.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <map>
+
+namespace eon_host {
+
+void check(eon_ctx* ctx, int rc, const char* what) {
+    if (rc == EON_OK) return;
+    const char* msg = ctx ? eon_last_error(ctx) : nullptr;
+    throw Error(rc, std::string(what) + ": " + (msg ? msg : "error"));
+}
+
+static void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw Error(e == hipErrorOutOfMemory ? EON_E_OOM : EON_E_DEVICE,
+                                     std::string(what) + ": " + hipGetErrorString(e));
+}
+
+DeviceBuffer::DeviceBuffer(uint64_t bytes) : bytes_(bytes) {
+    if (bytes) hip_check(hipMalloc(&p_, bytes), "hipMalloc");
+}
+
+DeviceBuffer::~DeviceBuffer() {
+    if (p_) (void)hipFree(p_);
+}
+
+DeviceBuffer& DeviceBuffer::operator=(DeviceBuffer&& o) noexcept {
+    if (this != &o) {
+        if (p_) (void)hipFree(p_);
+        p_ = o.p_;
+        bytes_ = o.bytes_;
+        o.p_ = nullptr;
+        o.bytes_ = 0;
+    }
+    return *this;
+}
+
+DeviceMatrix DeviceMatrix::alloc(uint64_t height, uint32_t width) {
+    DeviceMatrix m;
+    m.owned = DeviceBuffer(std::max<uint64_t>(height * width, 1) * sizeof(eon_fr));
+    m.height = height;
+    m.width = width;
+    return m;
+}
+
+DeviceMatrix DeviceMatrix::borrow(const eon_fr* p, uint64_t height, uint32_t width) {
+    DeviceMatrix m;
+    m.view = p;
+    m.height = height;
+    m.width = width;
+    return m;
+}
+
+static uint32_t log2_ceil(uint64_t n) {
+    uint32_t b = 0;
+    while ((1ull << b) < n) b++;
+    return b;
+}
+
+Domain Domain::create_disjoint_domain(uint64_t min_size) const {
+    // shift * GENERATOR keeps the coset disjoint from the subgroup (domain.rs:155-168)
+    return Domain{fr_mul(shift, fr_from_u64(5)), log2_ceil(min_size)};
+}
+
+std::vector<Domain> Domain::split_domains(uint32_t num_chunks) const {
+    const uint32_t lc = log2_ceil(num_chunks);
+    const Fr g = generator();
+    std::vector<Domain> out;
+    Fr s = shift;
+    for (uint32_t i = 0; i < num_chunks; i++) {
+        out.push_back(Domain{s, log_size - lc});
+        s = fr_mul(s, g);
+    }
+    return out;
+}
+
+KzgPcs::KzgPcs(eon_ctx* ctx, uint64_t max_degree, const Fr& srs_alpha) : ctx_(ctx), max_degree_(max_degree) {
+    // init_srs_unsafe (params.rs:123-139): g1_powers[i] = alpha^i * G for i <= max_degree, made on
+    // device and turned into fixed-base MSM bases without a host round trip
+    const uint64_t n = max_degree + 1;
+    DeviceBuffer pts(n * sizeof(eon_g1_affine));
+    const eon_fr a = srs_alpha.abi();
+    check(ctx_, eon_g1_srs_powers_dev(ctx_, &a, n, pts.as<eon_g1_affine>()), "eon_g1_srs_powers_dev");
+    check(ctx_, eon_msm_bases_create_dev(ctx_, pts.as<eon_g1_affine>(), n, EON_MSM_PRECOMPUTE, &bases_),
+          "eon_msm_bases_create_dev");
+    check(ctx_, eon_ctx_synchronize(ctx_), "eon_ctx_synchronize");
+}
+
+KzgPcs::~KzgPcs() {
+    if (bases_) eon_msm_bases_destroy(bases_);
+}
+
+Domain KzgPcs::natural_domain_for_degree(uint64_t degree) const {
+    return Domain{Fr::one(), degree > 1 ? log2_ceil(degree) : 0};
+}
+
+void KzgPcs::ensure_supported(uint64_t degree) const {
+    if (degree > max_degree_)
+        throw Error(EON_E_DEGREE_TOO_LARGE,
+                    "degree " + std::to_string(degree) + " > max " + std::to_string(max_degree_));
+}
+
+void KzgPcs::commit(std::vector<std::pair<Domain, DeviceMatrix>> evaluations,
+                    std::vector<std::vector<eon_g1_affine>>& commitments, std::vector<MatrixProverData>& data) {
+    for (auto& [domain, evals] : evaluations) {
+        const uint64_t h = evals.height;
+        const uint32_t w = evals.width;
+        if (h != domain.size()) throw Error(EON_E_SHAPE, "evaluation height must match domain size");
+        ensure_supported(h > 0 ? h - 1 : 0);
+        MatrixProverData d{domain, std::move(evals), DeviceMatrix::alloc(h, w)};
+        const eon_fr s = domain.shift.abi();
+        check(ctx_, eon_coset_idft_batch_dev(ctx_, d.evals.data(), d.coeffs.mutable_data(), h, w, &s),
+              "coset_idft_batch");
+        std::vector<eon_g1_affine> cm(w);
+        check(ctx_, eon_msm_g1_columns_dev(ctx_, bases_, d.coeffs.data(), h, w, cm.data()), "commit_column");
+        commitments.push_back(std::move(cm));
+        data.push_back(std::move(d));
+    }
+}
+
+DeviceMatrix KzgPcs::get_evaluations_on_domain(const std::vector<MatrixProverData>& data, size_t idx,
+                                               const Domain& domain) {
+    const MatrixProverData& m = data.at(idx);
+    if (m.domain == domain) return DeviceMatrix::borrow(m.evals.data(), m.evals.height, m.evals.width);
+    if (domain.log_size < m.domain.log_size)
+        throw Error(EON_E_SHAPE, "evaluation domain smaller than the committed domain");
+    const uint32_t added = domain.log_size - m.domain.log_size;
+    DeviceMatrix out = DeviceMatrix::alloc(m.coeffs.height << added, m.coeffs.width);
+    const eon_fr s = domain.shift.abi();
+    check(ctx_,
+          eon_coset_dft_padded_batch_dev(ctx_, m.coeffs.data(), out.mutable_data(), m.coeffs.height, m.coeffs.width,
+                                         added, &s, EON_ORDER_NATURAL),
+          "get_evaluations_on_domain");
+    return out;
+}
+
+void KzgPcs::commit_quotient(const Domain& quotient_domain, const DeviceMatrix& quotient_evals, uint32_t num_chunks,
+                             std::vector<std::vector<eon_g1_affine>>& commitments,
+                             std::vector<MatrixProverData>& data) {
+    // split_evals: chunk c holds rows {i * num_chunks + c} (a strided column gather on device)
+    if (quotient_evals.width != 1 || quotient_evals.height != quotient_domain.size() || num_chunks == 0 ||
+        quotient_evals.height % num_chunks)
+        throw Error(EON_E_SHAPE, "quotient evaluations must be one column over the quotient domain");
+    const uint64_t rows = quotient_evals.height / num_chunks;
+    hipStream_t st = static_cast<hipStream_t>(eon_ctx_stream(ctx_));
+    std::vector<std::pair<Domain, DeviceMatrix>> chunks;
+    const std::vector<Domain> doms = quotient_domain.split_domains(num_chunks);
+    for (uint32_t c = 0; c < num_chunks; c++) {
+        DeviceMatrix m = DeviceMatrix::alloc(rows, 1);
+        hip_check(hipMemcpy2DAsync(m.mutable_data(), sizeof(eon_fr), quotient_evals.data() + c,
+                                   sizeof(eon_fr) * num_chunks, sizeof(eon_fr), rows, hipMemcpyDeviceToDevice, st),
+                  "split_evals");
+        chunks.emplace_back(doms[c], std::move(m));
+    }
+    commit(std::move(chunks), commitments, data);
+}
+
+std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
+    struct Job {
+        size_t round, matrix, point;
+        uint64_t n;
+        uint32_t w;
+        uint32_t col0 = 0;
+    };
+    std::vector<Job> jobs;
+    std::vector<Opened> out(rounds.size());
+    for (size_t r = 0; r < rounds.size(); r++) {
+        const auto& data = *rounds[r].data;
+        if (data.size() != rounds[r].points.size()) throw Error(EON_E_SHAPE, "one point list per matrix");
+        out[r].values.resize(data.size());
+        out[r].witnesses.resize(data.size());
+        for (size_t m = 0; m < data.size(); m++) {
+            const size_t np = rounds[r].points[m].size();
+            out[r].values[m].resize(np);
+            out[r].witnesses[m].resize(np);
+            for (size_t p = 0; p < np; p++) jobs.push_back(Job{r, m, p, data[m].coeffs.height, data[m].coeffs.width});
+        }
+    }
+    // one witness matrix per quotient height n - 1, columns in job order
+    std::map<uint64_t, uint32_t> group_width;
+    for (Job& j : jobs) {
+        j.col0 = group_width[j.n];
+        group_width[j.n] += j.w;
+    }
+    std::map<uint64_t, DeviceMatrix> mats;
+    uint64_t tmp_elems = 1;
+    for (const auto& [n, w] : group_width) {
+        mats.emplace(n, DeviceMatrix::alloc(std::max<uint64_t>(n, 2) - 1, w));
+        (void)w;
+    }
+    for (const Job& j : jobs) tmp_elems = std::max<uint64_t>(tmp_elems, (std::max<uint64_t>(j.n, 2) - 1) * j.w);
+    uint32_t max_w = 1;
+    for (const Job& j : jobs) max_w = std::max(max_w, j.w);
+    DeviceBuffer quo(tmp_elems * sizeof(eon_fr));
+    DeviceBuffer vals(max_w * sizeof(eon_fr));
+    hipStream_t st = static_cast<hipStream_t>(eon_ctx_stream(ctx_));
+    for (const Job& j : jobs) {
+        const MatrixProverData& m = (*rounds[j.round].data)[j.matrix];
+        const eon_fr z = rounds[j.round].points[j.matrix][j.point].abi();
+        // quotient_and_eval (util.rs:100-111) for every column of the matrix
+        check(ctx_,
+              eon_quotient_and_eval_columns_dev(ctx_, m.coeffs.data(), j.n, j.w, &z, quo.as<eon_fr>(),
+                                                vals.as<eon_fr>()),
+              "quotient_and_eval");
+        DeviceMatrix& dst = mats.at(j.n);
+        if (j.n > 1)
+            hip_check(hipMemcpy2DAsync(dst.mutable_data() + j.col0, sizeof(eon_fr) * dst.width, quo.get(),
+                                       sizeof(eon_fr) * j.w, sizeof(eon_fr) * j.w, j.n - 1, hipMemcpyDeviceToDevice,
+                                       st),
+                      "witness matrix");
+        std::vector<eon_fr>& v = out[j.round].values[j.matrix][j.point];
+        v.resize(j.w);
+        hip_check(hipMemcpyAsync(v.data(), vals.get(), sizeof(eon_fr) * j.w, hipMemcpyDeviceToHost, st),
+                  "opened values");
+        hip_check(hipStreamSynchronize(st), "opened values");
+    }
+    for (auto& [n, mat] : mats) {
+        std::vector<eon_g1_affine> wits(mat.width);
+        check(ctx_, eon_msm_g1_columns_dev(ctx_, bases_, mat.data(), n - 1, mat.width, wits.data()), "witnesses");
+        for (const Job& j : jobs) {
+            if (j.n != n) continue;
+            out[j.round].witnesses[j.matrix][j.point].assign(wits.begin() + j.col0, wits.begin() + j.col0 + j.w);
+        }
+    }
+    return out;
+}
+
+}  // namespace eon_host

@@ -1,0 +1,179 @@
+// See prover.h.  Stage order and span names follow prove_with_preprocessed
+// (eon-uni-stark/src/prover.rs): commit (186-187) -> quotient domain (307-308) -> LDE (315) ->
+// quotient_values (328-342) -> commit_quotient (371-372) -> open at [zeta, zeta h] and [zeta] per
+// chunk (416-442).
+//
+// Lane sharding: the vectorized AIR evaluates its lanes one after another
+// (poseidon2-air/src/vectorized.rs:259-274), so lane v owns columns [164 v, 164 v + 164) and
+// constraints [K v, K v + K), K = 160.  A rank proving lanes [l0, l1) commits, extends and opens
+// its own columns, and its folder accumulator times alpha^(K (VL - l1)) is its exact share of the
+// full one (folder.rs:81-85).  The partials are all-gathered (Q x 32 B, the one data-path
+// exchange) and combined on device; the per-column results are all-gathered at the end.
+#include "prover.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <chrono>
+#include <cstring>
+
+namespace eon_host {
+
+uint32_t log_quotient_degree(uint32_t max_constraint_degree) {
+    const uint32_t d = (max_constraint_degree > 2 ? max_constraint_degree : 2) - 1;
+    uint32_t b = 0;
+    while ((1u << b) < d) b++;
+    return b;
+}
+
+namespace {
+
+// per-column record of the final all-gather: commitment (8) | value at zeta (4) | value at zeta h
+// (4) | witness at zeta (8) | witness at zeta h (8), in u64
+constexpr uint32_t RECORD = 32;
+
+void all_gather(eon_ctx* ctx, const eon_collective* coll, const void* send, void* recv, uint64_t bytes) {
+    const int rc = coll->all_gather(coll->user, send, recv, bytes, eon_ctx_stream(ctx));
+    if (rc != 0) throw Error(EON_E_DEVICE, "collective all_gather failed (" + std::to_string(rc) + ")");
+}
+
+void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw Error(EON_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t height, const Fr& alpha,
+            const Fr& zeta, uint32_t max_constraint_degree, const eon_collective* shard) {
+    eon_ctx* ctx = pcs.ctx();
+    using clock = std::chrono::steady_clock;
+    auto tick = [&] {
+        check(ctx, eon_ctx_synchronize(ctx), "eon_ctx_synchronize");
+        return clock::now();
+    };
+    auto ms = [](clock::time_point a, clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    if (height == 0 || (height & (height - 1))) throw Error(EON_E_SHAPE, "trace height must be a power of two");
+    const uint32_t width = eon_p2air_width(air);
+    const uint32_t local_vl = eon_p2air_vector_len(air);
+    const uint32_t k_lane = eon_p2air_constraints_per_perm(air);
+    if (shard && shard->world <= 1) shard = nullptr;
+    if (shard && (!shard->all_gather || shard->rank >= shard->world))
+        throw Error(EON_E_ARG, "invalid collective");
+    const uint32_t world = shard ? shard->world : 1, rank = shard ? shard->rank : 0;
+    const uint32_t vector_len = local_vl * world;
+    const uint32_t log_n = 63 - __builtin_clzll(height);
+    const uint32_t log_qd = log_quotient_degree(max_constraint_degree);
+    const uint32_t num_chunks = 1u << log_qd;
+    hipStream_t st = static_cast<hipStream_t>(eon_ctx_stream(ctx));
+
+    Proof proof;
+    proof.degree_bits = log_n;
+    const Domain trace_domain = pcs.natural_domain_for_degree(height);
+
+    auto t0 = tick();
+    std::vector<std::vector<eon_g1_affine>> trace_commit;
+    std::vector<MatrixProverData> trace_data;
+    {
+        std::vector<std::pair<Domain, DeviceMatrix>> ev;
+        ev.emplace_back(trace_domain, DeviceMatrix::borrow(trace, height, width));
+        pcs.commit(std::move(ev), trace_commit, trace_data);  // prover.rs:186-187
+    }
+    auto t1 = tick();
+    const Domain quotient_domain = trace_domain.create_disjoint_domain(1ull << (log_n + log_qd));
+    const uint64_t q_rows = quotient_domain.size();
+    DeviceMatrix qv = DeviceMatrix::alloc(q_rows, 1);
+    clock::time_point t2;
+    {
+        DeviceMatrix lde = pcs.get_evaluations_on_domain(trace_data, 0, quotient_domain);  // prover.rs:315
+        t2 = tick();
+        const eon_fr a = alpha.abi();
+        check(ctx, eon_p2air_quotient_values_dev(ctx, air, lde.data(), log_n, log_qd, &a, qv.mutable_data()),
+              "quotient_values");
+    }
+    auto t3 = tick();
+    if (shard) {
+        DeviceBuffer parts(sizeof(eon_fr) * q_rows * world);
+        all_gather(ctx, shard, qv.data(), parts.get(), sizeof(eon_fr) * q_rows);
+        std::vector<eon_fr> w(world);
+        for (uint32_t g = 0; g < world; g++)
+            w[g] = fr_pow(alpha, (uint64_t)k_lane * (vector_len - (g + 1) * local_vl)).abi();
+        check(ctx, eon_fr_lincomb_dev(ctx, parts.as<eon_fr>(), world, q_rows, w.data(), qv.mutable_data()),
+              "combine partial quotients");
+        (void)tick();
+    }
+    auto t3x = tick();
+    std::vector<std::vector<eon_g1_affine>> quotient_commit;
+    std::vector<MatrixProverData> quotient_data;
+    pcs.commit_quotient(quotient_domain, qv, num_chunks, quotient_commit, quotient_data);  // :371-372
+    auto t4 = tick();
+    const Fr zeta_next = trace_domain.next_point(zeta);  // prover.rs:416-419
+    std::vector<OpenRound> rounds(2);
+    rounds[0].data = &trace_data;
+    rounds[0].points = {{zeta, zeta_next}};
+    rounds[1].data = &quotient_data;
+    rounds[1].points.assign(num_chunks, std::vector<Fr>{zeta});
+    std::vector<Opened> opened = pcs.open(rounds);  // prover.rs:424-442
+    auto t5 = tick();
+
+    proof.quotient_commit.resize(num_chunks);
+    proof.quotient_opened.resize(num_chunks);
+    proof.quotient_witnesses.resize(num_chunks);
+    for (uint32_t c = 0; c < num_chunks; c++) {
+        proof.quotient_commit[c] = quotient_commit[c][0];
+        proof.quotient_opened[c] = opened[1].values[c][0][0];
+        proof.quotient_witnesses[c] = opened[1].witnesses[c][0][0];
+    }
+    const Opened& tr = opened[0];
+    if (!shard) {
+        proof.trace_commit = trace_commit[0];
+        for (int p = 0; p < 2; p++) {
+            proof.trace_opened[p] = tr.values[0][p];
+            proof.trace_witnesses[p] = tr.witnesses[0][p];
+        }
+    } else {
+        // every rank's columns land at their global positions (rank order = lane order)
+        std::vector<uint64_t> rec((uint64_t)width * RECORD);
+        for (uint32_t c = 0; c < width; c++) {
+            uint64_t* r = rec.data() + (uint64_t)c * RECORD;
+            std::memcpy(r, &trace_commit[0][c], 64);
+            std::memcpy(r + 8, &tr.values[0][0][c], 32);
+            std::memcpy(r + 12, &tr.values[0][1][c], 32);
+            std::memcpy(r + 16, &tr.witnesses[0][0][c], 64);
+            std::memcpy(r + 24, &tr.witnesses[0][1][c], 64);
+        }
+        const uint64_t bytes = rec.size() * sizeof(uint64_t);
+        DeviceBuffer send(bytes), recv(bytes * world);
+        hip_ok(hipMemcpyAsync(send.get(), rec.data(), bytes, hipMemcpyHostToDevice, st), "records");
+        all_gather(ctx, shard, send.get(), recv.get(), bytes);
+        std::vector<uint64_t> all(rec.size() * world);
+        hip_ok(hipMemcpyAsync(all.data(), recv.get(), bytes * world, hipMemcpyDeviceToHost, st), "records");
+        hip_ok(hipStreamSynchronize(st), "records");
+        const uint64_t full = (uint64_t)width * world;
+        proof.trace_commit.resize(full);
+        for (int p = 0; p < 2; p++) {
+            proof.trace_opened[p].resize(full);
+            proof.trace_witnesses[p].resize(full);
+        }
+        for (uint64_t c = 0; c < full; c++) {
+            const uint64_t* r = all.data() + c * RECORD;
+            std::memcpy(&proof.trace_commit[c], r, 64);
+            std::memcpy(&proof.trace_opened[0][c], r + 8, 32);
+            std::memcpy(&proof.trace_opened[1][c], r + 12, 32);
+            std::memcpy(&proof.trace_witnesses[0][c], r + 16, 64);
+            std::memcpy(&proof.trace_witnesses[1][c], r + 24, 64);
+        }
+    }
+    auto t6 = tick();
+    proof.stage_ms[EON_STAGE_COMMIT_TRACE] = ms(t0, t1);
+    proof.stage_ms[EON_STAGE_TRACE_LDE] = ms(t1, t2);
+    proof.stage_ms[EON_STAGE_QUOTIENT] = ms(t2, t3);
+    proof.stage_ms[EON_STAGE_EXCHANGE] = ms(t3, t3x);
+    proof.stage_ms[EON_STAGE_COMMIT_QUOTIENT] = ms(t3x, t4);
+    proof.stage_ms[EON_STAGE_OPEN] = ms(t4, t5);
+    proof.stage_ms[EON_STAGE_ASSEMBLE] = ms(t5, t6);
+    (void)rank;
+    return proof;
+}
+
+}  // namespace eon_host

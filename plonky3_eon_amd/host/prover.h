@@ -1,0 +1,30 @@
+// prove_with_preprocessed (eon-uni-stark/src/prover.rs:28-512) for the Poseidon2-AIR over KzgPcs,
+// as a C++ driver above eon.h.  Specialised to what the benchmark AIR exercises:
+// no preprocessed columns, no lookups, ZK off (KzgPcs::ZK = false, kzg/src/pcs.rs:216),
+// Challenge = Fr; alpha and zeta are inputs (transcript: SURVEY.md 8(f) N2).
+#pragma once
+#include "eon_prove.h"
+#include "pcs.h"
+
+namespace eon_host {
+
+// get_log_quotient_degree (eon-uni-stark/src/symbolic_builder.rs:15-43), ZK off
+uint32_t log_quotient_degree(uint32_t max_constraint_degree);
+
+struct Proof {
+    std::vector<eon_g1_affine> trace_commit;        // [W]
+    std::vector<eon_g1_affine> quotient_commit;     // [C]
+    std::vector<eon_fr> trace_opened[2];            // at zeta, zeta * h: [W] each
+    std::vector<eon_g1_affine> trace_witnesses[2];  // [W] each
+    std::vector<eon_fr> quotient_opened;            // [C]
+    std::vector<eon_g1_affine> quotient_witnesses;  // [C]
+    uint32_t degree_bits = 0;
+    double stage_ms[EON_STAGES] = {};
+};
+
+// `trace`: this rank's height x width(air) device trace.  With `shard` (world > 1) the AIR is the
+// rank's lane range; every rank returns the full proof.
+Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t height, const Fr& alpha,
+            const Fr& zeta, uint32_t max_constraint_degree, const eon_collective* shard);
+
+}  // namespace eon_host

@@ -1,0 +1,218 @@
+"""ctypes binding of the native prove driver libeonprove.so (include/eon_prove.h).
+
+The driver is the C++ host side above eon.h (plonky3_eon_amd/host/): KzgPcs + prove for the
+Poseidon2-AIR, the same orchestration as prover.py/kzg.py but without the Python interpreter in the
+loop.  Its Proof has prover.Proof's shape, so the two are compared field by field in the tests.
+
+Sharded prove: an eon_collective is either
+* ``TorchCollective(group)`` -- a ctypes callback over torch.distributed (gloo stages through host
+  memory; used by the CPU-hosted multi-rank tests), or
+* ``RcclCollective(rank, world, group)`` -- the driver's own RCCL communicator (ncclAllGather on
+  device buffers over xGMI); the 128-byte unique id is broadcast with torch.distributed.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+from . import _lib
+from .dft import Context, default_context
+from .field import fr_to_abi
+from .kzg import Opened
+from .prover import Proof, log_quotient_degree
+
+PROVE_LIB_PATH = Path(__file__).resolve().parent / "libeonprove.so"
+
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_INT = ctypes.c_int
+
+STAGES = ["commit to trace data", "trace LDE (get_evaluations_on_domain)", "quotient_values",
+          "exchange partial quotients", "commit to quotient poly chunks", "open", "assemble columns"]
+EON_STAGES = 8
+
+ALL_GATHER_FN = ctypes.CFUNCTYPE(_INT, _P, _P, _P, _U64, _P)
+
+
+class eon_collective(ctypes.Structure):
+    _fields_ = [("rank", _U32), ("world", _U32), ("all_gather", ALL_GATHER_FN), ("user", _P)]
+
+
+class eon_proof(ctypes.Structure):
+    _fields_ = [("trace_commit", _P), ("quotient_commit", _P), ("trace_opened", _P), ("trace_witnesses", _P),
+                ("quotient_opened", _P), ("quotient_witnesses", _P), ("degree_bits", _U32),
+                ("stage_ms", ctypes.c_double * EON_STAGES)]
+
+
+# name -> (restype, argtypes): every entry point of include/eon_prove.h
+SIGNATURES = {
+    "eon_prove_abi_version": (_U32, []),
+    "eon_kzg_pcs_create": (_INT, [_P, _U64, _P, ctypes.POINTER(_P)]),
+    "eon_kzg_pcs_destroy": (None, [_P]),
+    "eon_kzg_pcs_last_error": (ctypes.c_char_p, [_P]),
+    "eon_rccl_unique_id": (_INT, [_P]),
+    "eon_rccl_collective_init": (_INT, [_U32, _U32, _P, ctypes.POINTER(eon_collective)]),
+    "eon_rccl_collective_finalize": (None, [ctypes.POINTER(eon_collective)]),
+    "eon_prove_p2air": (_INT, [_P, _P, _P, _U64, _P, _P, _U32, ctypes.POINTER(eon_collective),
+                               ctypes.POINTER(eon_proof)]),
+}
+
+_plib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libeonprove.so (after libeonhip.so, which it links).  Raises if it is absent."""
+    global _plib
+    if _plib is not None:
+        return _plib
+    _lib.load()
+    path = Path(os.environ["EON_PROVE_LIB"]) if os.environ.get("EON_PROVE_LIB") else PROVE_LIB_PATH
+    if not path.exists():
+        raise ImportError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(os.fspath(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _plib = lib
+    return lib
+
+
+class NativeKzgPcs:
+    """KzgPcs::new(max_degree, alpha) inside the native driver (SRS and bases on device)."""
+
+    def __init__(self, max_degree: int, alpha: int, ctx: Context | None = None):
+        self.ctx = ctx or default_context(0)
+        self.lib = load()
+        self.max_degree = max_degree
+        h = ctypes.c_void_p()
+        a = fr_to_abi(alpha)
+        self.ctx.check(self.lib.eon_kzg_pcs_create(self.ctx.handle, max_degree, ctypes.byref(a), ctypes.byref(h)))
+        self._h = h
+
+    def check(self, rc: int):
+        if rc != 0:
+            raise _lib.EonError(rc, self.lib.eon_kzg_pcs_last_error(self._h).decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.eon_kzg_pcs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _DevBytes:
+    """A raw device allocation seen as a uint8 torch tensor (zero-copy, __cuda_array_interface__)."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 2}
+
+
+class TorchCollective:
+    """eon_collective whose all-gather is torch.distributed over `group` (any backend)."""
+
+    def __init__(self, rank: int, world: int, group=None, device=0):
+        self.group = group
+        self.device = device
+
+        def all_gather(user, send, recv, nbytes, stream):
+            try:
+                import torch
+
+                from .distributed import all_gather_rows
+
+                torch.cuda.synchronize(self.device)  # the driver's stream has produced `send`
+                s = torch.as_tensor(_DevBytes(send, nbytes), device=f"cuda:{self.device}")
+                r = torch.as_tensor(_DevBytes(recv, nbytes * world), device=f"cuda:{self.device}")
+                r.copy_(all_gather_rows(s, self.group).reshape(-1))
+                torch.cuda.synchronize(self.device)
+                return 0
+            except Exception:  # a Python exception must not unwind through the C caller
+                import traceback
+
+                traceback.print_exc()
+                return 1
+
+        self._fn = ALL_GATHER_FN(all_gather)  # keep the thunk alive
+        self.c = eon_collective(rank, world, self._fn, None)
+
+
+class RcclCollective:
+    """eon_collective backed by the driver's RCCL communicator."""
+
+    def __init__(self, rank: int, world: int, group=None):
+        import torch.distributed as dist
+
+        self.lib = load()
+        self.c = None
+        idbuf = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            rc = self.lib.eon_rccl_unique_id(idbuf)
+            if rc != 0:
+                raise _lib.EonError(rc, "eon_rccl_unique_id")
+        if world > 1:
+            obj = [bytes(idbuf)]
+            dist.broadcast_object_list(obj, src=0, group=group)
+            idbuf = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
+        self.c = eon_collective()
+        rc = self.lib.eon_rccl_collective_init(rank, world, idbuf, ctypes.byref(self.c))
+        if rc != 0:
+            raise _lib.EonError(rc, "eon_rccl_collective_init")
+
+    def close(self):
+        if getattr(self, "c", None) is not None and self.c.user:
+            self.lib.eon_rccl_collective_finalize(ctypes.byref(self.c))
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def prove_native(air, pcs: NativeKzgPcs, trace, alpha: int, zeta: int, max_constraint_degree: int = 3,
+                 collective=None) -> Proof:
+    """prover.prove through the C++ driver.  `trace`: (N, width, 4) device tensor; with a
+    collective (world > 1) `air`/`trace` are this rank's lanes and the proof is the full one."""
+    world = collective.c.world if collective is not None else 1
+    w = air.width * world
+    chunks = 1 << log_quotient_degree(max_constraint_degree)
+    tc = np.zeros((w, 8), np.uint64)
+    qc = np.zeros((chunks, 8), np.uint64)
+    to = np.zeros((2, w, 4), np.uint64)
+    tw = np.zeros((2, w, 8), np.uint64)
+    qo = np.zeros((chunks, 4), np.uint64)
+    qw = np.zeros((chunks, 8), np.uint64)
+    out = eon_proof(_p(tc), _p(qc), _p(to), _p(tw), _p(qo), _p(qw), 0)
+    a, z = fr_to_abi(alpha), fr_to_abi(zeta)
+    t = trace.contiguous()
+    import torch
+
+    torch.cuda.synchronize(t.device)  # the trace was produced on torch's stream
+    pcs.ctx.set_stream(None)
+    coll = ctypes.byref(collective.c) if collective is not None else None
+    pcs.check(pcs.lib.eon_prove_p2air(pcs._h, air.handle, ctypes.c_void_p(t.data_ptr()), int(t.shape[0]),
+                                      ctypes.byref(a), ctypes.byref(z), max_constraint_degree, coll,
+                                      ctypes.byref(out)))
+    opened_trace = Opened(values=[[to[0], to[1]]], witnesses=[[tw[0], tw[1]]])
+    opened_quot = Opened(values=[[qo[c:c + 1]] for c in range(chunks)], witnesses=[[qw[c:c + 1]] for c in range(chunks)])
+    timings = {name: out.stage_ms[i] for i, name in enumerate(STAGES)}
+    if collective is None:
+        timings.pop("exchange partial quotients")
+        timings.pop("assemble columns")
+    return Proof([tc], [qc[c:c + 1] for c in range(chunks)], [opened_trace, opened_quot], out.degree_bits, timings)

@@ -10,6 +10,9 @@ RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment, backend gloo).
           for the kernels (CPU).
   fourstep / msmshard -- the product four-step DFT and the point-range-sharded MSM on cuda:0,
           against the oracle's full-length DFT / MSM.
+  native -- the C++ prove driver (libeonprove.so) sharded over the ranks with a torch.distributed
+          eon_collective; rank 0 compares it with the driver's unsharded prove and the Python
+          prover's.
 
 Writes {"ok": true} or {"ok": false, "why": ...} as JSON to argv[2].
 """
@@ -130,6 +133,53 @@ def run_gpu(rank, world, group):
     return None
 
 
+def _proof_fields(p):
+    out = [("trace_commit", p.trace_commit[0])]
+    out += [(f"quotient_commit[{c}]", p.quotient_commit[c]) for c in range(len(p.quotient_commit))]
+    for r in range(2):
+        for m in range(len(p.opened[r].values)):
+            for pt in range(len(p.opened[r].values[m])):
+                out.append((f"opened[{r}].values[{m}][{pt}]", p.opened[r].values[m][pt]))
+                out.append((f"opened[{r}].witnesses[{m}][{pt}]", p.opened[r].witnesses[m][pt]))
+    return out
+
+
+def run_native(rank, world, group):
+    import torch
+
+    from plonky3_eon_amd import Context
+    from plonky3_eon_amd import distributed as D
+    from plonky3_eon_amd.air import Poseidon2Air
+    from plonky3_eon_amd.kzg import GpuKzgPcs
+    from plonky3_eon_amd.native import NativeKzgPcs, TorchCollective, prove_native
+    from plonky3_eon_amd.prover import prove
+
+    log_n, vl = int(os.environ.get("EON_T_LOG_N", "5")), int(os.environ.get("EON_T_VL", "4"))
+    n = 1 << log_n
+    k = consts()
+    ctx = Context(0)
+    dev = torch.device("cuda:0")
+    inputs = C.random_fr(98, n * vl * 3).reshape(n * vl, 3, 4)
+    alpha, zeta = 0x1234567890ABCDEF1234, 0xFEDCBA0987654321
+    npcs = NativeKzgPcs(n, 12345, ctx)
+    l0, l1 = D.lane_range(rank, world, vl)
+    air = Poseidon2Air(k.begin, k.partial, k.end, l1 - l0, ctx)
+    trace = air.generate_trace(torch.from_numpy(lane_inputs(inputs, n, vl, l0, l1).view(np.int64)).to(dev))
+    p = prove_native(air, npcs, trace, alpha, zeta, collective=TorchCollective(rank, world, group))
+    if rank != 0:
+        return None
+    full_air = Poseidon2Air(k.begin, k.partial, k.end, vl, ctx)
+    full = full_air.generate_trace(torch.from_numpy(inputs.view(np.int64)).to(dev))
+    q = prove_native(full_air, npcs, full, alpha, zeta)
+    r = prove(full_air, GpuKzgPcs(n, 12345, ctx), full, alpha, zeta)
+    for (name, a), (_, b), (_, c) in zip(_proof_fields(p), _proof_fields(q), _proof_fields(r)):
+        if not np.array_equal(np.asarray(a), np.asarray(b)):
+            return f"{name}: sharded native prove differs from the unsharded one"
+        if not np.array_equal(np.asarray(b), np.asarray(c)):
+            return f"{name}: native prove differs from the Python prover"
+    return None
+
+
 def _tw_pack(y, log_n, log_n1, col0, parts):
     """The documented contract of eon_fourstep_twiddle_pack_dev, in Python ints (test only)."""
     n1, cols = y.shape[0], y.shape[1]
@@ -215,7 +265,7 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         fn = {"cpu": run_cpu, "gpu": run_gpu, "a2a": run_a2a, "fourstep": run_fourstep,
-              "msmshard": run_msmshard}[mode]
+              "msmshard": run_msmshard, "native": run_native}[mode]
         why = fn(rank, world, None)
     except Exception:
         why = traceback.format_exc()

@@ -9,8 +9,8 @@ import pytest
 ROOT = Path(__file__).resolve().parent.parent
 
 
-def declared_functions():
-    text = (ROOT / "include" / "eon.h").read_text()
+def declared_functions(header="eon.h"):
+    text = (ROOT / "include" / header).read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(eon_[a-z0-9_]+)\s*\(", text)))
 
@@ -58,3 +58,26 @@ def test_no_oracle_in_product_path():
     for p in (ROOT / "plonky3_eon_amd").rglob("*"):
         if p.suffix in (".py", ".hip", ".h", ".cpp"):
             assert "oracle" not in p.read_text().replace("no CPU fallback", ""), p
+
+
+def test_prove_driver_exports_every_declared_symbol():
+    """libeonprove.so (the C++ host side above eon.h) loads without a GPU and exports
+    include/eon_prove.h; the ctypes table covers the header."""
+    from plonky3_eon_amd import _lib, native
+
+    if not _lib.LIB_PATH.exists() or not native.PROVE_LIB_PATH.exists():
+        pytest.skip("libraries not built (run __graft_entry__.build())")
+    lib = native.load()
+    names = declared_functions("eon_prove.h")
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert sorted(native.SIGNATURES) == names
+    assert lib.eon_prove_abi_version() >= 1
+
+
+def test_prove_driver_calls_only_the_c_abi():
+    """The driver is above the boundary: it includes eon.h / eon_prove.h and its own headers,
+    never the kernel sources."""
+    for p in (ROOT / "plonky3_eon_amd" / "host").glob("*"):
+        text = p.read_text()
+        assert "csrc/" not in text and '#include "field.h"' not in text and '#include "context.h"' not in text, p

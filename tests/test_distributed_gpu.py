@@ -14,6 +14,14 @@ def test_sharded_prove_matches_single(world, log_n, vl):
     assert all(r["ok"] for r in res), [r["why"] for r in res]
 
 
+@pytest.mark.parametrize("world,log_n,vl", [(2, 5, 4), (4, 3, 8)])
+def test_native_sharded_prove_matches_single(world, log_n, vl):
+    """The C++ driver's lane-sharded prove (torch.distributed eon_collective) == its unsharded
+    prove == the Python prover."""
+    res = run_world("native", world, timeout=900, extra_env={"EON_T_LOG_N": str(log_n), "EON_T_VL": str(vl)})
+    assert all(r["ok"] for r in res), [r["why"] for r in res]
+
+
 @pytest.mark.parametrize("world", [1, 2, 4])
 def test_fourstep_dft_matches_oracle(world):
     res = run_world("fourstep", world, timeout=900)

@@ -73,3 +73,78 @@ def test_prove_vs_oracle(gpu_ctx, consts, log_n, vl):
     for c in range(2):
         np.testing.assert_array_equal(qo.values[c][0], want["quotient_open"][c][0][0])
         np.testing.assert_array_equal(qo.witnesses[c][0], want["quotient_open"][c][1][0])
+
+
+@pytest.mark.parametrize("log_n,vl", [(3, 1), (5, 8)])
+def test_native_prove_vs_oracle(gpu_ctx, consts, log_n, vl):
+    """The C++ prove driver (libeonprove.so, include/eon_prove.h) against the same restatement."""
+    import torch
+
+    from plonky3_eon_amd.air import Poseidon2Air
+    from plonky3_eon_amd.native import NativeKzgPcs, prove_native
+
+    n = 1 << log_n
+    alpha_srs = 12345
+    pcs = NativeKzgPcs(n, alpha_srs, gpu_ctx)
+    air = Poseidon2Air(consts.begin, consts.partial, consts.end, vl, gpu_ctx)
+    inputs = C.random_fr(log_n * 3 + vl, n * vl * 3).reshape(n * vl, 3, 4)
+    trace = air.generate_trace(torch.from_numpy(inputs.view(np.int64)).to("cuda:0"))
+    alpha, zeta = 0x1234567890ABCDEF1234, 0xFEDCBA0987654321
+    proof = prove_native(air, pcs, trace, alpha, zeta)
+    assert proof.degree_bits == log_n
+
+    srs = C.g1_srs(n + 1, C.fr_from_u64(alpha_srs))
+    want = prove_oracle.prove(C.p2_generate_trace(inputs, vl, consts), srs, consts, vl, alpha, zeta)
+    np.testing.assert_array_equal(proof.trace_commit[0], want["trace_commit"])
+    np.testing.assert_array_equal(np.stack([c[0] for c in proof.quotient_commit]), want["quotient_commit"])
+    tr = proof.opened[0]
+    for p in range(2):
+        np.testing.assert_array_equal(tr.values[0][p], want["trace_open"][0][p])
+        np.testing.assert_array_equal(tr.witnesses[0][p], want["trace_open"][1][p])
+    qo = proof.opened[1]
+    for c in range(2):
+        np.testing.assert_array_equal(qo.values[c][0], want["quotient_open"][c][0][0])
+        np.testing.assert_array_equal(qo.witnesses[c][0], want["quotient_open"][c][1][0])
+
+
+def test_native_errors(gpu_ctx, consts):
+    """Reference panics -> EonError: degree above the SRS (KzgError::DegreeTooLarge), a
+    non-power-of-two height."""
+    import torch
+
+    from plonky3_eon_amd import _lib
+    from plonky3_eon_amd.air import Poseidon2Air
+    from plonky3_eon_amd.native import NativeKzgPcs, prove_native
+
+    air = Poseidon2Air(consts.begin, consts.partial, consts.end, 1, gpu_ctx)
+    inputs = C.random_fr(3, 16 * 3).reshape(16, 3, 4)
+    trace = air.generate_trace(torch.from_numpy(inputs.view(np.int64)).to("cuda:0"))
+    small = NativeKzgPcs(8, 12345, gpu_ctx)
+    with pytest.raises(_lib.EonError) as e:
+        prove_native(air, small, trace, 3, 5)
+    assert e.value.code == _lib.EON_E_DEGREE_TOO_LARGE
+    pcs = NativeKzgPcs(16, 12345, gpu_ctx)
+    with pytest.raises(_lib.EonError) as e:
+        prove_native(air, pcs, trace[:12], 3, 5)
+    assert e.value.code == _lib.EON_E_SHAPE
+
+
+def test_native_rccl_collective_single_rank(gpu_ctx):
+    """The driver's RCCL eon_collective (used at N > 1 GPUs) initialises and all-gathers on device
+    with one rank (RCCL allows one rank per GPU, so this is all one box can run)."""
+    import ctypes
+
+    import torch
+
+    from plonky3_eon_amd.native import RcclCollective
+
+    coll = RcclCollective(0, 1)
+    src = torch.arange(1000, dtype=torch.uint8, device="cuda:0")
+    dst = torch.zeros_like(src)
+    stream = torch.cuda.current_stream().cuda_stream
+    rc = coll.c.all_gather(None if coll.c.user is None else coll.c.user, ctypes.c_void_p(src.data_ptr()),
+                           ctypes.c_void_p(dst.data_ptr()), 1000, ctypes.c_void_p(stream))
+    torch.cuda.synchronize()
+    assert rc == 0
+    assert torch.equal(src, dst)
+    coll.close()

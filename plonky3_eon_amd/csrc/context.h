@@ -49,14 +49,14 @@ struct Status {
 // device workspace of one MSM pipeline run (msm.hip); grows on demand, reused across calls
 struct MsmWork {
     DevBuf keys, vals, keys2, vals2, start, count, piece_off, off2, owner, piece_sums,
-        piece_sums2, bucket_sums, red_a, red_b, temp, results, levels;
+        piece_sums2, bucket_sums, red_a, red_b, temp, results, levels, piece_raw;
     uint32_t* host_counts = nullptr;  // pinned read-back slots
     void release() {
         if (host_counts) (void)hipHostFree(host_counts);
         host_counts = nullptr;
         for (DevBuf* b : {&keys, &vals, &keys2, &vals2, &start, &count, &piece_off, &off2, &owner,
                           &piece_sums, &piece_sums2, &bucket_sums, &red_a, &red_b, &temp, &levels,
-                          &results})
+                          &results, &piece_raw})
             b->release();
     }
 };

@@ -1,0 +1,138 @@
+// BN254 G1 XYZZ accumulation in radix-2^29 arithmetic (field29.h) for the MSM bucket sums.
+//
+// Same formulas as ec.h (madd-2008-s, mdbl-2008-s-1, a = 0) with lazy reduction: no conditional
+// subtraction anywhere, each coordinate carries a bound in multiples of p instead:
+//   X < 8p, Y < 4p, ZZ < 2p, ZZZ < 2p        (invariant of an accumulator between additions)
+// and every product input stays below 13p (mul29's limit, field29.h).  Affine bases are read in
+// 29-Montgomery form (x 2^261 mod p, canonical, as a 256-bit integer in the 64-byte G1Affine
+// slot; see k_table_to29 in msm.hip), so a load is a bit re-split with no product.
+#pragma once
+#include "ec.h"
+#include "field29.h"
+
+namespace eon {
+
+struct G1X29 {
+    F29 X, Y, ZZ, ZZZ;
+};
+
+// The raw accumulator as stored by k_piece_sum: 36 words (X, Y, ZZ, ZZZ limbs), 144 bytes;
+// ZZ = 0 marks the identity.
+struct alignas(16) G1Raw29 {
+    uint32_t w[36];
+};
+
+__device__ __forceinline__ void pin29(F29& a) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) asm volatile("" : "+v"(a.l[i]));
+}
+
+// 2A for an affine A (29-Montgomery, canonical coordinates): mdbl-2008-s-1
+__device__ __forceinline__ G1X29 dbl29_affine(const F29& x, const F29& y) {
+    const F29 U = add29_norm(y, y);                   // < 2p
+    const F29 V = mul29<FqP>(U, U);                   // < 2p
+    const F29 W = mul29<FqP>(U, V);                   // < 2p
+    const F29 S = mul29<FqP>(x, V);                   // < 2p
+    const F29 X2 = mul29<FqP>(x, x);                  // < 2p
+    const F29 M = add29_norm(add29_norm(X2, X2), X2);  // < 6p
+    G1X29 r;
+    r.X = sub29<FqP, 4>(mul29<FqP>(M, M), add29_lazy(S, S));                        // < 6p
+    r.Y = sub29<FqP, 2>(mul29<FqP>(M, sub29<FqP, 6>(S, r.X)), mul29<FqP>(W, y));     // < 4p
+    r.ZZ = V;
+    r.ZZZ = W;
+    return r;
+}
+
+// acc += (ax, ay) for a non-identity accumulator and a non-identity affine base.  Returns false in
+// the exceptional case x(acc) == x(A) (then acc is left unchanged and the caller resolves it:
+// doubling or the identity).
+__device__ __forceinline__ bool madd29(G1X29& acc, const F29& ax, const F29& ay) {
+    const F29 U2 = mul29<FqP>(ax, acc.ZZ);            // < 2p
+    const F29 P = sub29<FqP, 8>(U2, acc.X);           // < 10p
+    const F29 PP = mul29<FqP>(P, P);                  // < 2p
+    if (is_zero_mod29<FqP>(PP)) return false;         // P == 0 mod p
+    const F29 PPP = mul29<FqP>(P, PP);                // < 2p
+    const F29 Q = mul29<FqP>(acc.X, PP);              // < 2p
+    const F29 S2 = mul29<FqP>(ay, acc.ZZZ);           // < 2p
+    const F29 R = sub29<FqP, 4>(S2, acc.Y);           // < 6p
+    acc.ZZ = mul29<FqP>(acc.ZZ, PP);                  // < 2p
+    acc.ZZZ = mul29<FqP>(acc.ZZZ, PPP);               // < 2p
+    const F29 YP = mul29<FqP>(acc.Y, PPP);            // < 2p
+    const F29 X3 = sub29<FqP, 4>(sub29<FqP, 2>(mul29<FqP>(R, R), PPP), add29_lazy(Q, Q));  // < 8p
+    acc.Y = sub29<FqP, 2>(mul29<FqP>(R, sub29<FqP, 8>(Q, X3)), YP);                        // < 4p
+    acc.X = X3;
+    return true;
+}
+
+// exceptional case of madd29: x(acc) == x(A); returns the sum (doubling when y(acc) == y(A))
+// and whether it is the identity.  Rare (duplicate bases, P + (-P)): one extra product.
+__device__ __forceinline__ bool madd29_exceptional(G1X29& acc, const F29& ax, const F29& ay) {
+    const F29 S2 = mul29<FqP>(ay, acc.ZZZ);
+    const F29 R = sub29<FqP, 4>(S2, acc.Y);
+    // R mod p: times the plain integer 2^261 mod p (29-Montgomery one) -> value < 2p
+    const F29 Rr = mul29<FqP>(R, const29<FqP>(R29<FqP>::ONE));
+    if (is_zero_mod29<FqP>(Rr)) {
+        acc = dbl29_affine(ax, ay);
+        return false;
+    }
+    return true;  // A = -acc: the sum is the identity
+}
+
+// 29-Montgomery coordinate (any bound < 13p) -> canonical radix-2^32 Montgomery Fq
+__device__ __forceinline__ Fq to_fq256(const F29& a) {
+    return pack29<FqP>(canon29<FqP>(mul29<FqP>(a, const29<FqP>(R29<FqP>::TO256))));
+}
+
+// canonical radix-2^32 Fq -> 29-Montgomery, canonical (x 2^256 -> x 2^261)
+__device__ __forceinline__ Fq to_fq261(const Fq& a) {
+    return pack29<FqP>(canon29<FqP>(mul29<FqP>(unpack29(a), const29<FqP>(R29<FqP>::TO261))));
+}
+
+__device__ __forceinline__ void st_raw29(G1Raw29* p, const G1X29& a) {
+    uint32_t w[36];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        w[i] = a.X.l[i];
+        w[9 + i] = a.Y.l[i];
+        w[18 + i] = a.ZZ.l[i];
+        w[27 + i] = a.ZZZ.l[i];
+    }
+    uint4* q = reinterpret_cast<uint4*>(p->w);
+#pragma unroll
+    for (int k = 0; k < 9; k++) q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+}
+
+__device__ __forceinline__ void st_raw29_inf(G1Raw29* p) {
+    uint4* q = reinterpret_cast<uint4*>(p->w);
+#pragma unroll
+    for (int k = 0; k < 9; k++) q[k] = make_uint4(0, 0, 0, 0);
+}
+
+__device__ __forceinline__ G1Xyzz raw29_to_xyzz(const G1Raw29* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p->w);
+    uint32_t w[36];
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        const uint4 v = q[k];
+        w[4 * k] = v.x;
+        w[4 * k + 1] = v.y;
+        w[4 * k + 2] = v.z;
+        w[4 * k + 3] = v.w;
+    }
+    F29 c[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+#pragma unroll
+        for (int i = 0; i < 9; i++) c[j].l[i] = w[9 * j + i];
+        pin29(c[j]);
+    }
+    if (is_zero29_raw(c[2])) return xyzz_inf();
+    G1Xyzz r;
+    r.X = to_fq256(c[0]);
+    r.Y = to_fq256(c[1]);
+    r.ZZ = to_fq256(c[2]);
+    r.ZZZ = to_fq256(c[3]);
+    return r;
+}
+
+}  // namespace eon

@@ -1,0 +1,268 @@
+// BN254 field arithmetic in radix 2^29 (9 limbs in VGPRs, Montgomery R = 2^261) for the MSM's
+// register-resident bucket accumulators.
+//
+// Why a second representation: in radix 2^32 (field.h) every 32x32 multiply-add into a column
+// accumulator can carry out of 64 bits, so each v_mad_u64_u32 is followed by a v_addc carry
+// capture -- half the issue slots of the product.  With 29-bit limbs a column holds at most 18
+// products < 2^60 (both operands' limbs < 2^30), which together with the incoming carry stay below
+// 2^64: the product is 162 bare multiply-adds plus a few shifts per column.
+//
+// Value conventions (p = the modulus, < 2^254):
+//   * an element is 9 limbs l[i] with value sum l[i] 2^(29 i); "normalised" = every limb < 2^29;
+//   * mul29(a, b) returns a b 2^-261 mod p, normalised, value < 2p, for any inputs whose limbs are
+//     < 2^30 and whose values satisfy a b < p 2^261 (e.g. both < 13p);
+//   * add29_lazy (no carry propagation: limbs < 2^30) feeds a product only; sub29<K> returns
+//     a - b + K p normalised (b < K p) -- no conditional subtraction anywhere on the hot path;
+//   * canon29 brings a value < 2p to [0, p).
+// An element x of the field is held as x 2^261 mod p ("29-Montgomery"); the radix-2^32 ABI form is
+// x 2^256 mod p, and to256 / to261 convert with one product each.  unpack29 / pack29 only re-split
+// the bits of an integer < 2^256.
+#pragma once
+#include "field.h"
+
+namespace eon {
+
+constexpr uint32_t M29 = (1u << 29) - 1;
+
+struct F29 {
+    uint32_t l[9];
+};
+
+template <class M>
+struct R29;
+
+template <>
+struct R29<FqP> {
+    static constexpr uint32_t P[9] = {0x187cfd47u, 0x10460b6u, 0x1c72a34fu, 0x2d522d0u, 0x1585d978u,
+                                      0x2db40c0u,  0xa6e141u,  0xe5c2634u,  0x30644eu};
+    static constexpr uint32_t INV = 0xe4866389u;  // -p^-1 mod 2^32 (only the low 29 bits are used)
+    // 2^261 mod p (the 29-Montgomery one), 2^256 mod p and 2^266 mod p as plain integers
+    static constexpr uint32_t ONE[9] = {0x157ccc21u, 0x141c2758u, 0x185230d3u, 0x14c0419u, 0xaa36fb9u,
+                                        0x1d4240ceu, 0x11d54c07u, 0x52ac7a8u,  0xdc836u};
+    static constexpr uint32_t TO256[9] = {0x58f0d9du,  0x1aea1c6eu, 0x11c2cf74u, 0x11d651ebu, 0x1462c0a7u,
+                                          0x11b7bc3cu, 0x1cbd99bau, 0x183340fbu, 0xe0a77u};
+    static constexpr uint32_t TO261[9] = {0x13349ca1u, 0x1a5d84a8u, 0xa3e5cacu,  0x100249e0u, 0x12b951e8u,
+                                          0xe92d304u,  0x14cb95b3u, 0x41b9d3du,  0x58003u};
+};
+
+template <>
+struct R29<FrP> {
+    static constexpr uint32_t P[9] = {0x10000001u, 0x1f0fac9fu, 0xe5c2450u, 0x7d090f3u, 0x1585d283u,
+                                      0x2db40c0u,  0xa6e141u,   0xe5c2634u, 0x30644eu};
+    static constexpr uint32_t INV = 0xefffffffu;
+    static constexpr uint32_t ONE[9] = {0xfffff57u,  0x1ea70ab4u, 0x52c068bu, 0x17504f49u, 0xaa8075bu,
+                                        0x1d4240ceu, 0x11d54c07u, 0x52ac7a8u, 0xdc836u};
+    static constexpr uint32_t TO256[9] = {0xffffffbu,  0x4b1a0e2u,  0x18334a6bu, 0x18ed2b3eu, 0x1462e36fu,
+                                          0x11b7bc3cu, 0x1cbd99bau, 0x183340fbu, 0xe0a77u};
+    static constexpr uint32_t TO261[9] = {0xfffead7u, 0x1d5444f4u, 0x4438aa5u,  0x3b4d096u, 0x134c84dau,
+                                          0xe92d304u, 0x14cb95b3u, 0x41b9d3du,  0x58003u};
+};
+
+// K p as normalised limbs (compile-time)
+template <class M, uint32_t K>
+struct KP29 {
+    uint32_t l[9];
+    constexpr KP29() : l{} {
+        uint64_t c = 0;
+        for (int i = 0; i < 9; i++) {
+            c += (uint64_t)R29<M>::P[i] * K;
+            l[i] = (uint32_t)(c & M29);
+            c >>= 29;
+        }
+    }
+};
+
+template <class M>
+EON_HD F29 const29(const uint32_t (&c)[9]) {
+    F29 r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.l[i] = c[i];
+    return r;
+}
+
+// integer < 2^256 in 8 x 32-bit limbs <-> 9 x 29-bit limbs (bit re-split only)
+template <class M>
+EON_HD F29 unpack29(const Fe<M>& a) {
+    F29 r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        const int bit = 29 * i, w = bit >> 5, s = bit & 31;
+        uint64_t v = a.v[w];
+        if (w + 1 < 8) v |= (uint64_t)a.v[w + 1] << 32;
+        r.l[i] = (uint32_t)(v >> s) & M29;
+    }
+    return r;
+}
+
+template <class M = FqP>
+EON_HD Fe<M> pack29(const F29& a) {
+    // a normalised, value < 2^256
+    Fe<M> r;
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+        const int bit = 32 * w, i = bit / 29, s = bit % 29;
+        uint64_t v = (uint64_t)a.l[i] >> s;
+        if (i + 1 < 9) v |= (uint64_t)a.l[i + 1] << (29 - s);
+        if (i + 2 < 9 && 58 - s < 32) v |= (uint64_t)a.l[i + 2] << (58 - s);
+        r.v[w] = (uint32_t)v;
+    }
+    return r;
+}
+
+EON_HD bool limbs_ok29(const F29& a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) o |= a.l[i];
+    return (o >> 29) == 0;
+}
+
+EON_HD bool is_zero29_raw(const F29& a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) o |= a.l[i];
+    return o == 0;
+}
+
+// limb-wise a + b, no carry propagation (a, b normalised -> limbs < 2^30): a product input only
+EON_HD F29 add29_lazy(const F29& a, const F29& b) {
+    F29 r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.l[i] = a.l[i] + b.l[i];
+    return r;
+}
+
+// a + b with carry propagation (normalised result; value a + b < 2^261)
+EON_HD F29 add29_norm(const F29& a, const F29& b) {
+    F29 r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        const uint32_t t = a.l[i] + b.l[i] + c;
+        r.l[i] = t & M29;
+        c = t >> 29;
+    }
+    return r;
+}
+
+// a - b + K p, normalised (requires b < K p; a, b limbs < 2^30)
+template <class M, uint32_t K>
+EON_HD F29 sub29(const F29& a, const F29& b) {
+    constexpr KP29<M, K> kp{};
+    F29 r;
+    int32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        const int32_t t = (int32_t)(a.l[i] + kp.l[i]) - (int32_t)b.l[i] + c;
+        r.l[i] = (uint32_t)t & M29;
+        c = t >> 29;  // arithmetic: -1, 0 or 1
+    }
+    return r;
+}
+
+template <class M>
+EON_HD F29 mulp29(uint32_t k) {
+    F29 r;
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        c += (uint64_t)R29<M>::P[i] * k;
+        r.l[i] = (uint32_t)(c & M29);
+        c >>= 29;
+    }
+    return r;
+}
+
+// a - p if a >= p (a normalised, a < 2p) -> [0, p)
+template <class M>
+EON_HD F29 canon29(const F29& a) {
+    F29 d;
+    int32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        const int32_t t = (int32_t)a.l[i] - (int32_t)R29<M>::P[i] + c;
+        d.l[i] = (uint32_t)t & M29;
+        c = t >> 29;
+    }
+    return c < 0 ? a : d;
+}
+
+// value in {0, p} (a normalised, < 2p): "zero mod p" for a product output
+template <class M>
+EON_HD bool is_zero_mod29(const F29& a) {
+    uint32_t z = 0, e = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        z |= a.l[i];
+        e |= a.l[i] ^ R29<M>::P[i];
+    }
+    return z == 0 || e == 0;
+}
+
+// Montgomery product a b 2^-261 mod p (product scanning; see the header comment for the bounds)
+template <class M>
+EON_HD F29 mul29(const F29& a, const F29& b) {
+    uint32_t m[9];
+    F29 r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+#pragma unroll
+        for (int i = 0; i <= k; i++) acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+        for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * R29<M>::P[k - i];
+        m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
+        acc += (uint64_t)m[k] * R29<M>::P[0];
+        acc >>= 29;
+    }
+#pragma unroll
+    for (int k = 9; k < 17; k++) {
+#pragma unroll
+        for (int i = k - 8; i < 9; i++) {
+            acc += (uint64_t)a.l[i] * b.l[k - i];
+            acc += (uint64_t)m[i] * R29<M>::P[k - i];
+        }
+        r.l[k - 9] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
+    r.l[8] = (uint32_t)acc;
+    return r;
+}
+
+// Same with the product and reduction terms of a column in two accumulators (shorter dependency
+// chains), merged once per column.
+template <class M>
+EON_HD F29 mul29_2acc(const F29& a, const F29& b) {
+    uint32_t m[9];
+    F29 r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        uint64_t pa = 0, pb = 0;
+#pragma unroll
+        for (int i = 0; i <= k; i += 2) pa += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+        for (int i = 1; i <= k; i += 2) pb += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+        for (int i = 0; i < k; i++) pb += (uint64_t)m[i] * R29<M>::P[k - i];
+        acc += pa + pb;
+        m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
+        acc += (uint64_t)m[k] * R29<M>::P[0];
+        acc >>= 29;
+    }
+#pragma unroll
+    for (int k = 9; k < 17; k++) {
+        uint64_t pa = 0, pb = 0;
+#pragma unroll
+        for (int i = k - 8; i < 9; i++) {
+            pa += (uint64_t)a.l[i] * b.l[k - i];
+            pb += (uint64_t)m[i] * R29<M>::P[k - i];
+        }
+        acc += pa + pb;
+        r.l[k - 9] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
+    r.l[8] = (uint32_t)acc;
+    return r;
+}
+
+}  // namespace eon

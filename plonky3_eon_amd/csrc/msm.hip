@@ -42,6 +42,7 @@
 
 #include "context.h"
 #include "ec.h"
+#include "ec29.h"
 #include "msm.h"
 
 using namespace eon;
@@ -53,6 +54,9 @@ struct eon_msm_bases {
     bool precomputed = false;
     uint32_t c = 0, windows = 0;
     DevBuf table;  // precomputed: n * windows affine points, entry i * windows + w = 2^(c*w) P_i
+    // the piece sums' source (table if precomputed, else points) holds 29-Montgomery coordinates
+    // and k_piece_sum29 runs (EON_MSM_R32=1 keeps radix-2^32 bases and k_piece_sum)
+    bool r29 = false;
 };
 
 namespace eon {
@@ -213,6 +217,71 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum(const uint
     const uint32_t bb = bucket_of(b, c, groups, nb);
     st_xyzz(piece_sums + piece_off[bb] + t - (start[bb] >> log_chunk), acc);
     }
+}
+
+// Radix-2^29 form of k_piece_sum (ec29.h): the same chunk walk, with the XYZZ accumulator in
+// 29-bit limbs (lazy bounds, no carry captures in the products) and the bases read in
+// 29-Montgomery form (k_table_to29).  Each bucket run stores its raw accumulator (144 bytes,
+// ZZ = 0 for the identity); k_raw29_to_xyzz converts the pieces for the combine levels.
+__global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
+    const uint32_t* keys, const uint32_t* vals, const uint32_t* start, const uint32_t* piece_off,
+    uint32_t n_pairs, uint32_t log_chunk, uint32_t c, uint32_t groups, uint32_t nb,
+    const G1Affine* pts29, G1Raw29* piece_raw) {
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; ((uint64_t)t << log_chunk) < n_pairs;
+         t += gridDim.x * blockDim.x) {
+        const uint32_t e0 = t << log_chunk;
+        const uint32_t e1 = min(e0 + (1u << log_chunk), n_pairs);
+        uint32_t b = keys[e0];
+        G1X29 acc;
+        bool inf = true;
+        auto flush = [&]() {
+            const uint32_t bb = bucket_of(b, c, groups, nb);
+            G1Raw29* dst = piece_raw + piece_off[bb] + t - (start[bb] >> log_chunk);
+            if (inf)
+                st_raw29_inf(dst);
+            else
+                st_raw29(dst, acc);
+        };
+        for (uint32_t e = e0; e < e1; e++) {
+            const uint32_t k = keys[e];
+            if (k != b) {
+                flush();
+                inf = true;
+                b = k;
+            }
+            const uint32_t v = vals[e];
+            G1Affine a = ld_affine(pts29 + (v & 0x7fffffffu));
+            if (is_inf(a)) continue;
+            if (v >> 31) a.y = neg(a.y);
+            const F29 ax = unpack29(a.x), ay = unpack29(a.y);
+            if (inf) {
+                acc.X = ax;
+                acc.Y = ay;
+                acc.ZZ = const29<FqP>(R29<FqP>::ONE);
+                acc.ZZZ = acc.ZZ;
+                inf = false;
+            } else if (!madd29(acc, ax, ay)) {
+                inf = madd29_exceptional(acc, ax, ay);
+            }
+        }
+        flush();
+    }
+}
+
+__global__ void k_raw29_to_xyzz(const G1Raw29* in, uint32_t n, G1Xyzz* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    st_xyzz(out + i, raw29_to_xyzz(in + i));
+}
+
+// affine points (canonical radix-2^32 Montgomery) -> 29-Montgomery in place; (0, 0) stays
+__global__ void k_table_to29(G1Affine* pts, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    G1Affine a = ld_affine(pts + i);
+    a.x = to_fq261(a.x);
+    a.y = to_fq261(a.y);
+    st_affine(pts + i, a);
 }
 
 // One combine level: new partial p of bucket b sums old partials
@@ -465,6 +534,14 @@ Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32
         tmp.release();
         if (e != hipSuccess) return fail(Status::err(EON_E_DEVICE, hipGetErrorString(e)));
     }
+    b->r29 = getenv("EON_MSM_R32") == nullptr;
+    if (b->r29 && n) {
+        const uint64_t m = b->precomputed ? n * b->windows : n;
+        G1Affine* src = b->precomputed ? b->table.as<G1Affine>() : b->points.as<G1Affine>();
+        hipLaunchKernelGGL(k_table_to29, dim3(blocks_for(m, 256)), dim3(256), 0, st, src, m);
+        e = hipGetLastError();
+        if (e != hipSuccess) return fail(Status::err(EON_E_DEVICE, hipGetErrorString(e)));
+    }
     e = hipStreamSynchronize(st);
     if (e != hipSuccess) return fail(Status::err(EON_E_DEVICE, hipGetErrorString(e)));
     *out = b;
@@ -529,6 +606,7 @@ static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint6
     EON_HIP(wk.owner.ensure(bt.max_pieces * 4));
     EON_HIP(wk.piece_sums.ensure(bt.max_pieces * sizeof(G1Xyzz)));
     EON_HIP(wk.piece_sums2.ensure(bt.max_pieces * sizeof(G1Xyzz)));
+    if (b->r29) EON_HIP(wk.piece_raw.ensure(bt.max_pieces * sizeof(G1Raw29)));
     EON_HIP(wk.bucket_sums.ensure((uint64_t)nb * sizeof(G1Xyzz)));
     EON_HIP(wk.off2.ensure((nb + 1) * 4ull));
     if (!wk.host_counts) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&wk.host_counts), 64));
@@ -577,12 +655,19 @@ static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt
                     (uint64_t)bt.n_pairs * 10);
     uint32_t blocks = blocks_for(((uint64_t)bt.n_pairs + (1u << bt.log_chunk) - 1) >> bt.log_chunk, 64);
     if (ctx->piece_block_cap) blocks = std::min(blocks, ctx->piece_block_cap);
-    if (bt.n_pairs)
+    if (bt.n_pairs && b->r29)
+        hipLaunchKernelGGL(k_piece_sum29, dim3(blocks), dim3(64), 0, st, wk.keys2.as<uint32_t>(),
+                           wk.vals2.as<uint32_t>(), wk.start.as<uint32_t>(), wk.piece_off.as<uint32_t>(),
+                           bt.n_pairs, bt.log_chunk, bt.c, bt.groups, bt.nb, pts, wk.piece_raw.as<G1Raw29>());
+    else if (bt.n_pairs)
         hipLaunchKernelGGL(k_piece_sum, dim3(blocks),
                            dim3(64), 0, st, wk.keys2.as<uint32_t>(), wk.vals2.as<uint32_t>(),
                            wk.start.as<uint32_t>(), wk.piece_off.as<uint32_t>(), bt.n_pairs,
                            bt.log_chunk, bt.c, bt.groups, bt.nb, pts, wk.piece_sums.as<G1Xyzz>());
     ctx->prof.end(st);
+    if (bt.n_pieces && b->r29)
+        hipLaunchKernelGGL(k_raw29_to_xyzz, dim3(blocks_for(bt.n_pieces, 128)), dim3(128), 0, st,
+                           wk.piece_raw.as<G1Raw29>(), bt.n_pieces, wk.piece_sums.as<G1Xyzz>());
     EON_HIP(hipGetLastError());
     return Status::ok();
 }

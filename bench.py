@@ -45,8 +45,10 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "eon-uni-stark prove ms, Poseidon2-AIR 2^20 rows KZG/BN254, at 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# measured 256-bit Montgomery multiply peak (tools/ubench_mulmod.hip, MI355X, FIPS variant)
-MULMOD_PEAK_PER_S = 1.29e11
+# measured 256-bit Montgomery multiply peak on MI355X: the radix-2^29 carry-free product
+# (tools/ubench_r29.hip, profiles/r01_ubench_r29.txt: 1.73e11/s; the radix-2^32 FIPS product of
+# the NTT/quotient kernels peaks at 1.29e11/s, tools/ubench_mulmod.hip)
+MULMOD_PEAK_PER_S = 1.73e11
 FR_P = [0x43E1F593F0000001, 0x2833E84879B97091, 0xB85045B68181585D, 0x30644E72E131A029]
 
 
@@ -328,7 +330,7 @@ class ProveWorkload:
     def throughput(self, world, ms):
         n = 1 << self.log_n
         st = {}
-        for k in self.timings[-self.args.steps:]:
+        for k in self.timings[self.args.warmup:self.args.warmup + self.args.steps]:  # the timed steps
             for a, b in k.items():
                 st[a] = st.get(a, 0.0) + b / self.args.steps
         return {
@@ -456,7 +458,7 @@ class MsmShardWorkload:
                       f"2^{self.args.log_shard_msm}",
         }
 
-def main() -> int:
+def make_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default: 3 (prove), 10 (lde, msm)")
@@ -478,7 +480,11 @@ def main() -> int:
     ap.add_argument("--collective", choices=["torch", "rccl"], default="torch",
                     help="prove --host native at N > 1: all-gathers through torch.distributed (RCCL "
                          "process group) or the driver's own RCCL communicator")
-    args = ap.parse_args()
+    return ap
+
+
+def main() -> int:
+    args = make_parser().parse_args()
     if args.steps is None:
         args.steps = 3 if args.workload == "prove" else 10
     if args.warmup is None:
@@ -510,16 +516,26 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ctx.profile(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         wl.step()
+        print(f"step {i}: {(time.perf_counter() - t0) * 1e3:.1f} ms since start", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
+    # per-launch HIP-event timings come from extra steps after the timed region: recording two
+    # events around every launch on three streams perturbs the stream overlap of the MSM pipeline,
+    # so the timed steps above run without them
+    prof_steps = max(1, min(args.steps, 2))
+    ctx.profile(True)
+    for _ in range(prof_steps):
+        wl.step()
+    torch.cuda.synchronize()
     prof = ctx.profile_report()
     ctx.profile(False)
+    if world > 1:
+        dist.barrier()
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -531,7 +547,7 @@ def main() -> int:
     avg_ms = kst["total_ms"] / kst["launches"]
     bytes_per_launch = kst["alg_bytes"] / kst["launches"]
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    gpu_total_ms = sum(v["total_ms"] for v in prof.values()) / args.steps
+    gpu_total_ms = sum(v["total_ms"] for v in prof.values()) / prof_steps
     workload, gbatch, seq, par = wl.describe(world)
     thr, mulmods = wl.throughput(world, ms_per_step)
 
@@ -573,7 +589,7 @@ def main() -> int:
         "higher_is_better": False,
         "scaling": getattr(wl, "scaling", "weak"),
         "vs_baseline": None,
-        "dtype": "bn254-fr (u32x8 Montgomery)",
+        "dtype": "bn254 Fr/Fq (256-bit Montgomery: u32x8 in HBM, u29x9 MSM accumulators)",
         "data": "synthetic uniform Fr, resident in HBM",
         "config": {"workload": workload, "global_batch": gbatch, "seq_len": seq, "parallelism": par},
         "throughput": thr,

@@ -95,6 +95,12 @@ __global__ void k_check(const Fe<M>* a, const Fe<M>* b, int n, unsigned* bad) {
     Fe<M> c4 = pack29<M>(canon29<M>(r4));
     for (int k = 0; k < 5; k++) c4 = add(c4, c4);
     if (c4 != want || !limbs_ok29(lx)) atomicAdd(bad + 4, 1u);
+    // sum of two products with one reduction: x y + (x - y + 8p) (2p - y)
+    const F29 d = sub29<M, 8>(x, y), e = sub29<M, 2>(F29{}, y);
+    const Fe<M> want5 = add(want, mul_fips(sub(ai, bi), neg(bi)));
+    Fe<M> c5 = pack29<M>(canon29<M>(mul29_sum2<M>(x, y, d, e)));
+    for (int k = 0; k < 5; k++) c5 = add(c5, c5);
+    if (c5 != want5) atomicAdd(bad + 5, 1u);
 }
 
 template <class M, int CH, int V>
@@ -183,8 +189,8 @@ int main() {
     k_check<FrP><<<n / 256, 256>>>((const Fr*)da, (const Fr*)db, n, dbad + 8);
     unsigned bad[16];
     hipMemcpy(bad, dbad, 64, hipMemcpyDeviceToHost);
-    printf("{\"fq_mismatch\":[%u,%u,%u,%u,%u],\"fr_mismatch\":[%u,%u,%u,%u,%u]}\n", bad[0], bad[1], bad[2], bad[3], bad[4],
-           bad[8], bad[9], bad[10], bad[11], bad[12]);
+    printf("{\"fq_mismatch\":[%u,%u,%u,%u,%u,%u],\"fr_mismatch\":[%u,%u,%u,%u,%u,%u]}\n", bad[0], bad[1], bad[2], bad[3], bad[4],
+           bad[5], bad[8], bad[9], bad[10], bad[11], bad[12], bad[13]);
     for (int blocks : {256 * 4, 256 * 8, 256 * 16}) {
         run_fips<FqP>("Fq", da, dout, blocks, 2048);
         run<FqP, 1, 0>("Fq", da, dout, blocks, 4096);

@@ -43,6 +43,7 @@ typedef struct {
 
 typedef struct eon_ctx eon_ctx;
 typedef struct eon_msm_bases eon_msm_bases;
+typedef struct eon_msm_scalars eon_msm_scalars;
 
 enum {
     EON_OK = 0,
@@ -69,6 +70,8 @@ const char* eon_last_error(const eon_ctx* ctx);
 int eon_ctx_set_stream(eon_ctx* ctx, void* hip_stream);
 /* The stream the context currently enqueues on (as set, or its own). */
 void* eon_ctx_stream(eon_ctx* ctx);
+/* The device ordinal the context was created on. */
+int eon_ctx_device(const eon_ctx* ctx);
 int eon_ctx_synchronize(eon_ctx* ctx);
 /* Per-launch kernel timing with HIP events on the launch stream (the analogue of the
  * reference's tracing spans, e.g. dft/src/radix_2_dit_parallel.rs:168).  eon_ctx_profile(ctx, 1)
@@ -155,7 +158,8 @@ int eon_msm_g1_columns_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_f
 /* quotient_and_eval (kzg/src/util.rs:100-111) for every column of a row-major rows x width
  * coefficient matrix (device) at `point` (host): quotient (device) receives the (rows-1) x width
  * synthetic-division quotients, values (device) the width evaluations f_j(point), as
- * KzgPcs::open computes per (matrix, point, column) (kzg/src/pcs.rs:297-330). */
+ * KzgPcs::open computes per (matrix, point, column) (kzg/src/pcs.rs:297-330).  quotient NULL:
+ * values only. */
 int eon_quotient_and_eval_columns_dev(eon_ctx* ctx, const eon_fr* coeffs, uint64_t rows,
                                       uint32_t width, const eon_fr* point, eon_fr* quotient,
                                       eon_fr* values);
@@ -165,6 +169,33 @@ int eon_msm_bases_create_dev(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t 
 /* One-shot G1::multi_exp(points, scalars) on host arrays (bases uploaded for this call only). */
 int eon_g1_multi_exp(eon_ctx* ctx, const eon_g1_affine* points, const eon_fr* scalars, uint64_t n,
                      eon_g1_affine* out);
+
+/* Prepared scalar columns.  eon_msm_g1_columns_prepare_dev is eon_msm_g1_columns_dev (out may be
+ * NULL) that also keeps every column's sorted bucket digits on device in *prepared
+ * (~8 bytes x rows x ceil(255/c) per column), so that MSMs of the SAME columns against other
+ * bases of the same window layout skip the digit extraction and sort:
+ * eon_msm_g1_columns_prepared writes out[t * width + j] = sum_i mat[i][j] * bases[t][i].  KzgPcs
+ * commits a matrix with the first (kzg/src/pcs.rs:244-251) and opens it with the second against
+ * eon_kzg_opening_bases_create bases (pcs.rs:305-316).  `mat` need not outlive the prepare call;
+ * every bases[t] must hold >= rows points with the window layout of the prepare call's bases
+ * (EON_E_SHAPE otherwise). */
+int eon_msm_g1_columns_prepare_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* mat,
+                                   uint64_t rows, uint32_t width, eon_g1_affine* out,
+                                   eon_msm_scalars** prepared);
+int eon_msm_g1_columns_prepared(eon_ctx* ctx, const eon_msm_bases* const* bases, uint32_t nbases,
+                                const eon_msm_scalars* prepared, eon_g1_affine* out);
+void eon_msm_scalars_destroy(eon_msm_scalars* prepared);
+/* KZG opening bases for `point` z (host) over the first n-1 points G_i of `srs`:
+ * H_j = sum_{i<j} z^(j-1-i) G_i, j < n (H_0 = identity), in the window layout of `srs`.  For any
+ * coefficient column c of length n, sum_j c_j H_j = commit_column(quotient_and_eval(c, z).0)
+ * (kzg/src/util.rs:37-40,100-111): the opening witness of KzgPcs::open (kzg/src/pcs.rs:305-316)
+ * as an MSM of the committed coefficients themselves. */
+int eon_kzg_opening_bases_create(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
+                                 const eon_fr* point, eon_msm_bases** out);
+/* The same for npoints points (host array) at once (the points' constructions overlap on the
+ * device): outs[t] = the opening bases of points[t]. */
+int eon_kzg_opening_bases_create_many(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
+                                      const eon_fr* points, uint32_t npoints, eon_msm_bases** outs);
 
 /* ---- eon-uni-stark quotient on the Poseidon2-AIR --------------------------------------------
  * selectors_on_coset (commit/src/domain.rs:252-292): for the trace domain H (shift 1, 2^log_n) on

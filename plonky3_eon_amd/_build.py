@@ -76,7 +76,7 @@ def _build_prove_driver() -> Path:
     newest = max([o.stat().st_mtime for o in objs] + [LIB.stat().st_mtime])
     if not PROVE_LIB.exists() or PROVE_LIB.stat().st_mtime < newest:
         cmd = [HIPCC, "-shared", "-fPIC", *map(str, objs), "-o", str(PROVE_LIB), "-L" + str(PKG), "-leonhip",
-               "-lrccl", "-Wl,-rpath,$ORIGIN"]
+               "-lrccl", "-pthread", "-Wl,-rpath,$ORIGIN"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed (libeonprove.so):\n{r.stderr[-6000:]}")

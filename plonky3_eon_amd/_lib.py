@@ -65,6 +65,7 @@ SIGNATURES = {
     "eon_last_error": (ctypes.c_char_p, [_P]),
     "eon_ctx_set_stream": (_INT, [_P, _P]),
     "eon_ctx_stream": (_P, [_P]),
+    "eon_ctx_device": (_INT, [_P]),
     "eon_ctx_synchronize": (_INT, [_P]),
     "eon_ctx_profile": (_INT, [_P, _INT]),
     "eon_ctx_profile_report": (_INT, [_P, ctypes.c_char_p, _U64]),
@@ -89,6 +90,11 @@ SIGNATURES = {
     "eon_msm_g1_columns": (_INT, [_P, _P, _P, _U64, _U32, _P]),
     "eon_msm_g1_columns_dev": (_INT, [_P, _P, _P, _U64, _U32, _P]),
     "eon_quotient_and_eval_columns_dev": (_INT, [_P, _P, _U64, _U32, _P, _P, _P]),
+    "eon_msm_g1_columns_prepare_dev": (_INT, [_P, _P, _P, _U64, _U32, _P, ctypes.POINTER(_P)]),
+    "eon_msm_g1_columns_prepared": (_INT, [_P, _P, _U32, _P, _P]),
+    "eon_msm_scalars_destroy": (None, [_P]),
+    "eon_kzg_opening_bases_create": (_INT, [_P, _P, _U64, _P, ctypes.POINTER(_P)]),
+    "eon_kzg_opening_bases_create_many": (_INT, [_P, _P, _U64, _P, _U32, _P]),
     "eon_msm_bases_create_dev": (_INT, [_P, _P, _U64, _U32, ctypes.POINTER(_P)]),
     "eon_g1_srs_powers": (_INT, [_P, _P, _U64, _P]),
     "eon_g1_srs_powers_dev": (_INT, [_P, _P, _U64, _P]),

@@ -259,7 +259,7 @@ int entry(eon_ctx* ctx, bool dev, Op op, const eon_fr* in, eon_fr* out, uint64_t
 
 extern "C" {
 
-uint32_t eon_abi_version(void) { return 1; }
+uint32_t eon_abi_version(void) { return 2; }
 
 int eon_ctx_create(int device_ordinal, eon_ctx** out) {
     if (!out) return EON_E_ARG;
@@ -280,7 +280,8 @@ int eon_ctx_create(int device_ordinal, eon_ctx** out) {
     // sort stream at the highest priority
     int prio_least = 0, prio_greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
-    bool ok = hipStreamCreateWithFlags(&c->msm_side, hipStreamNonBlocking) == hipSuccess;
+    bool ok = hipStreamCreateWithFlags(&c->msm_side, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->msm_side2, hipStreamNonBlocking) == hipSuccess;
     if (const char* e = getenv("EON_MSM_SORT_CUS")) c->msm_sort_cus = (uint32_t)atoi(e);
     hipDeviceProp_t prop{};
     int ncu = 0;
@@ -323,6 +324,7 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamSynchronize(ctx->msm_side);
+    (void)hipStreamSynchronize(ctx->msm_side2);
     (void)hipStreamSynchronize(ctx->msm_sort);
     for (hipStream_t st : ctx->msm_comp)
         if (st) (void)hipStreamSynchronize(st);
@@ -337,6 +339,8 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     ctx->msm.release();
     ctx->msm_b.release();
     ctx->msm_c.release();
+    for (auto& sb : ctx->sorted_cache) sb.release();
+    ctx->sorted_cache.clear();
     ctx->sel_tab.release();
     ctx->kzg_tmp.release();
     ctx->scratch.release();
@@ -344,6 +348,7 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     ctx->stage_out.release();
     (void)hipStreamDestroy(ctx->own_stream);
     (void)hipStreamDestroy(ctx->msm_side);
+    (void)hipStreamDestroy(ctx->msm_side2);
     (void)hipStreamDestroy(ctx->msm_sort);
     for (hipStream_t st : ctx->msm_comp)
         if (st) (void)hipStreamDestroy(st);
@@ -362,6 +367,8 @@ int eon_ctx_set_stream(eon_ctx* ctx, void* hip_stream) {
     ctx->stream = reinterpret_cast<hipStream_t>(hip_stream);
     return EON_OK;
 }
+
+int eon_ctx_device(const eon_ctx* ctx) { return ctx ? ctx->device : -1; }
 
 void* eon_ctx_stream(eon_ctx* ctx) {
     if (!ctx) return nullptr;

@@ -47,17 +47,32 @@ struct Status {
 };
 
 // device workspace of one MSM pipeline run (msm.hip); grows on demand, reused across calls
+// A batch's sorted digit pairs: keys / values by bucket, bucket starts, piece offsets.  Owned by
+// a workspace (streaming path) or by an eon_msm_scalars cache (prepared path, reused by every MSM
+// of the same scalars against other bases).
+struct SortedBufs {
+    DevBuf keys2, vals2, start, piece_off;
+    size_t bytes() const { return keys2.bytes + vals2.bytes + start.bytes + piece_off.bytes; }
+    void release() {
+        keys2.release();
+        vals2.release();
+        start.release();
+        piece_off.release();
+    }
+};
+
 struct MsmWork {
-    DevBuf keys, vals, keys2, vals2, start, count, piece_off, off2, owner, piece_sums,
-        piece_sums2, bucket_sums, red_a, red_b, temp, results, levels, piece_raw;
+    DevBuf keys, vals, count, off2, off3, owner, piece_sums, piece_sums2, bucket_sums, red_a, red_b,
+        temp, results, levels, piece_raw, stat;
+    SortedBufs sorted;
     uint32_t* host_counts = nullptr;  // pinned read-back slots
     void release() {
         if (host_counts) (void)hipHostFree(host_counts);
         host_counts = nullptr;
-        for (DevBuf* b : {&keys, &vals, &keys2, &vals2, &start, &count, &piece_off, &off2, &owner,
-                          &piece_sums, &piece_sums2, &bucket_sums, &red_a, &red_b, &temp, &levels,
-                          &results, &piece_raw})
+        for (DevBuf* b : {&keys, &vals, &count, &off2, &off3, &owner, &piece_sums, &piece_sums2,
+                          &bucket_sums, &red_a, &red_b, &temp, &levels, &results, &piece_raw, &stat})
             b->release();
+        sorted.release();
     }
 };
 
@@ -105,6 +120,8 @@ struct eon_ctx {
     // `stream` / msm_side, digit sorts on the high-priority msm_sort (msm.hip: msm_run_columns)
     eon::MsmWork msm, msm_b, msm_c;
     hipStream_t msm_side = nullptr, msm_sort = nullptr;
+    // third compute stream of the prepared path (jobs round-robin over stream / msm_side / msm_side2)
+    hipStream_t msm_side2 = nullptr;
     // EON_MSM_SORT_CUS > 0: piece sums on msm_comp[2] (CU-masked to all but those CUs), sorts
     // on msm_sort masked to them -- a full piece-sum launch leaves no room for a sort workgroup
     uint32_t msm_sort_cus = 0;
@@ -114,6 +131,11 @@ struct eon_ctx {
     hipStream_t msm_comp[2] = {nullptr, nullptr};
     hipEvent_t msm_ev[3] = {nullptr, nullptr, nullptr};
     hipEvent_t msm_sorted[3] = {nullptr, nullptr, nullptr}, msm_reduced[3] = {nullptr, nullptr, nullptr};
+
+    // sorted-digit buffers of destroyed eon_msm_scalars, reused by the next prepared MSM (the
+    // prover commits matrices of the same shape every proof: keeping ~22 GB resident beats a
+    // hipMalloc/hipFree of it per proof); trimmed past MSM_SORTED_CACHE_CAP bytes
+    std::vector<eon::SortedBufs> sorted_cache;
 
     // quotient: vanishing-polynomial table; KZG opening scan workspace
     eon::DevBuf sel_tab, kzg_tmp;

@@ -30,13 +30,13 @@ __device__ __forceinline__ void pin29(F29& a) {
 // 2A for an affine A (29-Montgomery, canonical coordinates): mdbl-2008-s-1
 __device__ __forceinline__ G1X29 dbl29_affine(const F29& x, const F29& y) {
     const F29 U = add29_norm(y, y);                   // < 2p
-    const F29 V = mul29<FqP>(U, U);                   // < 2p
+    const F29 V = sqr29<FqP>(U);                       // < 2p
     const F29 W = mul29<FqP>(U, V);                   // < 2p
     const F29 S = mul29<FqP>(x, V);                   // < 2p
-    const F29 X2 = mul29<FqP>(x, x);                  // < 2p
+    const F29 X2 = sqr29<FqP>(x);                      // < 2p
     const F29 M = add29_norm(add29_norm(X2, X2), X2);  // < 6p
     G1X29 r;
-    r.X = sub29<FqP, 4>(mul29<FqP>(M, M), add29_lazy(S, S));                        // < 6p
+    r.X = sub29<FqP, 4>(sqr29<FqP>(M), add29_lazy(S, S));                        // < 6p
     r.Y = sub29<FqP, 2>(mul29<FqP>(M, sub29<FqP, 6>(S, r.X)), mul29<FqP>(W, y));     // < 4p
     r.ZZ = V;
     r.ZZZ = W;
@@ -49,7 +49,7 @@ __device__ __forceinline__ G1X29 dbl29_affine(const F29& x, const F29& y) {
 __device__ __forceinline__ bool madd29(G1X29& acc, const F29& ax, const F29& ay) {
     const F29 U2 = mul29<FqP>(ax, acc.ZZ);            // < 2p
     const F29 P = sub29<FqP, 8>(U2, acc.X);           // < 10p
-    const F29 PP = mul29<FqP>(P, P);                  // < 2p
+    const F29 PP = sqr29<FqP>(P);                      // < 2p
     if (is_zero_mod29<FqP>(PP)) return false;         // P == 0 mod p
     const F29 PPP = mul29<FqP>(P, PP);                // < 2p
     const F29 Q = mul29<FqP>(acc.X, PP);              // < 2p
@@ -57,9 +57,9 @@ __device__ __forceinline__ bool madd29(G1X29& acc, const F29& ax, const F29& ay)
     const F29 R = sub29<FqP, 4>(S2, acc.Y);           // < 6p
     acc.ZZ = mul29<FqP>(acc.ZZ, PP);                  // < 2p
     acc.ZZZ = mul29<FqP>(acc.ZZZ, PPP);               // < 2p
-    const F29 YP = mul29<FqP>(acc.Y, PPP);            // < 2p
-    const F29 X3 = sub29<FqP, 4>(sub29<FqP, 2>(mul29<FqP>(R, R), PPP), add29_lazy(Q, Q));  // < 8p
-    acc.Y = sub29<FqP, 2>(mul29<FqP>(R, sub29<FqP, 8>(Q, X3)), YP);                        // < 4p
+    const F29 X3 = sub29<FqP, 4>(sub29<FqP, 2>(sqr29<FqP>(R), PPP), add29_lazy(Q, Q));  // < 8p
+    // Y3 = R (Q - X3) - Y PPP = R (Q - X3 + 8p) + Y (2p - PPP): one shared reduction, < 2p
+    acc.Y = mul29_sum2<FqP>(R, sub29<FqP, 8>(Q, X3), acc.Y, sub29<FqP, 2>(F29{}, PPP));
     acc.X = X3;
     return true;
 }
@@ -76,6 +76,88 @@ __device__ __forceinline__ bool madd29_exceptional(G1X29& acc, const F29& ax, co
         return false;
     }
     return true;  // A = -acc: the sum is the identity
+}
+
+// 2P for an accumulator under the invariant bounds: dbl-2008-s-1 (a = 0), lazy
+__device__ __forceinline__ void dbl29(G1X29& p) {
+    const F29 U = add29_norm(p.Y, p.Y);                // < 8p
+    const F29 V = sqr29<FqP>(U);                       // < 2p
+    const F29 W = mul29<FqP>(U, V);                    // < 2p
+    const F29 S = mul29<FqP>(p.X, V);                  // < 2p
+    const F29 X2 = sqr29<FqP>(p.X);                    // < 2p
+    const F29 M = add29_norm(add29_norm(X2, X2), X2);  // < 6p
+    const F29 X3 = sub29<FqP, 4>(sqr29<FqP>(M), add29_lazy(S, S));  // < 6p
+    // Y3 = M (S - X3) - W Y = M (S - X3 + 6p) + W (4p - Y), one shared reduction, < 2p
+    const F29 Y3 = mul29_sum2<FqP>(M, sub29<FqP, 6>(S, X3), W, sub29<FqP, 4>(F29{}, p.Y));
+    p.ZZ = mul29<FqP>(V, p.ZZ);
+    p.ZZZ = mul29<FqP>(W, p.ZZZ);
+    p.X = X3;
+    p.Y = Y3;
+}
+
+// p += q for two non-identity accumulators under the invariant bounds: add-2008-s, lazy
+// (12M + 2S).  Returns 0, or in the exceptional case x(p) == x(q) (p unchanged) 1 when p == q
+// (the caller doubles) and 2 when p == -q (the sum is the identity).
+__device__ __forceinline__ int add29(G1X29& p, const G1X29& q) {
+    const F29 U1 = mul29<FqP>(p.X, q.ZZ);    // < 2p
+    const F29 U2 = mul29<FqP>(q.X, p.ZZ);    // < 2p
+    const F29 S1 = mul29<FqP>(p.Y, q.ZZZ);   // < 2p
+    const F29 S2 = mul29<FqP>(q.Y, p.ZZZ);   // < 2p
+    const F29 P = sub29<FqP, 2>(U2, U1);     // < 4p
+    const F29 R = sub29<FqP, 2>(S2, S1);     // < 4p
+    const F29 PP = sqr29<FqP>(P);            // < 2p
+    if (is_zero_mod29<FqP>(PP)) {
+        const F29 Rr = mul29<FqP>(R, const29<FqP>(R29<FqP>::ONE));  // R mod p, < 2p
+        return is_zero_mod29<FqP>(Rr) ? 1 : 2;
+    }
+    const F29 PPP = mul29<FqP>(P, PP);       // < 2p
+    const F29 Q = mul29<FqP>(U1, PP);        // < 2p
+    const F29 X3 = sub29<FqP, 4>(sub29<FqP, 2>(sqr29<FqP>(R), PPP), add29_lazy(Q, Q));  // < 8p
+    // Y3 = R (Q - X3) - S1 PPP = R (Q - X3 + 8p) + S1 (2p - PPP), < 2p
+    p.Y = mul29_sum2<FqP>(R, sub29<FqP, 8>(Q, X3), S1, sub29<FqP, 2>(F29{}, PPP));
+    p.ZZ = mul29<FqP>(mul29<FqP>(p.ZZ, q.ZZ), PP);
+    p.ZZZ = mul29<FqP>(mul29<FqP>(p.ZZZ, q.ZZZ), PPP);
+    p.X = X3;
+    return 0;
+}
+
+// p += q with identity flags
+__device__ __forceinline__ void acc29(G1X29& p, bool& p_inf, const G1X29& q, bool q_inf) {
+    if (q_inf) return;
+    if (p_inf) {
+        p = q;
+        p_inf = false;
+        return;
+    }
+    const int e = add29(p, q);
+    if (e == 1) dbl29(p);
+    if (e == 2) p_inf = true;
+}
+
+// a raw accumulator (k_piece_sum29's partial); returns whether it is the identity
+__device__ __forceinline__ bool ld_raw29(const G1Raw29* p, G1X29& a) {
+    const uint4* q = reinterpret_cast<const uint4*>(p->w);
+    uint32_t w[36];
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        const uint4 v = q[k];
+        w[4 * k] = v.x;
+        w[4 * k + 1] = v.y;
+        w[4 * k + 2] = v.z;
+        w[4 * k + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        a.X.l[i] = w[i];
+        a.Y.l[i] = w[9 + i];
+        a.ZZ.l[i] = w[18 + i];
+        a.ZZZ.l[i] = w[27 + i];
+    }
+    pin29(a.X);
+    pin29(a.Y);
+    pin29(a.ZZ);
+    pin29(a.ZZZ);
+    return is_zero29_raw(a.ZZ);
 }
 
 // 29-Montgomery coordinate (any bound < 13p) -> canonical radix-2^32 Montgomery Fq
@@ -106,6 +188,16 @@ __device__ __forceinline__ void st_raw29_inf(G1Raw29* p) {
     uint4* q = reinterpret_cast<uint4*>(p->w);
 #pragma unroll
     for (int k = 0; k < 9; k++) q[k] = make_uint4(0, 0, 0, 0);
+}
+
+__device__ __forceinline__ G1Xyzz x29_to_xyzz(const G1X29& a, bool inf) {
+    if (inf) return xyzz_inf();
+    G1Xyzz r;
+    r.X = to_fq256(a.X);
+    r.Y = to_fq256(a.Y);
+    r.ZZ = to_fq256(a.ZZ);
+    r.ZZZ = to_fq256(a.ZZZ);
+    return r;
 }
 
 __device__ __forceinline__ G1Xyzz raw29_to_xyzz(const G1Raw29* p) {

@@ -228,6 +228,77 @@ EON_HD F29 mul29(const F29& a, const F29& b) {
     return r;
 }
 
+// a^2 2^-261 mod p for a NORMALISED a (limbs < 2^29; value < 13p): each column's cross products
+// once, summed apart and doubled by a shift (45 instead of 81 limb products; sums < 2^63)
+template <class M>
+EON_HD F29 sqr29(const F29& a) {
+    uint32_t m[9];
+    F29 r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        uint64_t cross = 0;
+#pragma unroll
+        for (int i = 0; 2 * i < k; i++) cross += (uint64_t)a.l[i] * a.l[k - i];
+        acc += cross << 1;
+        if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+#pragma unroll
+        for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * R29<M>::P[k - i];
+        m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
+        acc += (uint64_t)m[k] * R29<M>::P[0];
+        acc >>= 29;
+    }
+#pragma unroll
+    for (int k = 9; k < 17; k++) {
+        uint64_t cross = 0;
+#pragma unroll
+        for (int i = k - 8; 2 * i < k; i++) cross += (uint64_t)a.l[i] * a.l[k - i];
+        acc += cross << 1;
+        if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+#pragma unroll
+        for (int i = k - 8; i < 9; i++) acc += (uint64_t)m[i] * R29<M>::P[k - i];
+        r.l[k - 9] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
+    r.l[8] = (uint32_t)acc;
+    return r;
+}
+
+// (a b + c d) 2^-261 mod p with one reduction: 27 terms per column, so all four inputs must be
+// normalised (limbs < 2^29); a b + c d < p 2^261 gives an output < 2p.
+template <class M>
+EON_HD F29 mul29_sum2(const F29& a, const F29& b, const F29& c, const F29& d) {
+    uint32_t m[9];
+    F29 r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+#pragma unroll
+        for (int i = 0; i <= k; i++) {
+            acc += (uint64_t)a.l[i] * b.l[k - i];
+            acc += (uint64_t)c.l[i] * d.l[k - i];
+        }
+#pragma unroll
+        for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * R29<M>::P[k - i];
+        m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
+        acc += (uint64_t)m[k] * R29<M>::P[0];
+        acc >>= 29;
+    }
+#pragma unroll
+    for (int k = 9; k < 17; k++) {
+#pragma unroll
+        for (int i = k - 8; i < 9; i++) {
+            acc += (uint64_t)a.l[i] * b.l[k - i];
+            acc += (uint64_t)c.l[i] * d.l[k - i];
+            acc += (uint64_t)m[i] * R29<M>::P[k - i];
+        }
+        r.l[k - 9] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
+    r.l[8] = (uint32_t)acc;
+    return r;
+}
+
 // Same with the product and reduction terms of a column in two accumulators (shorter dependency
 // chains), merged once per column.
 template <class M>

@@ -89,7 +89,7 @@ int eon_quotient_and_eval_columns_dev(eon_ctx* ctx, const eon_fr* coeffs, uint64
             EON_HIP(hipMemsetAsync(values, 0, (size_t)width * sizeof(Fr), ctx->stream));
             return Status::ok();
         }
-        if (!coeffs || (rows > 1 && !quotient)) return Status::err(EON_E_ARG, "null argument");
+        if (!coeffs) return Status::err(EON_E_ARG, "null argument");
         const Fr z = fr_from_abi(point);
         if (!fr_is_canonical(z)) return Status::err(EON_E_ARG, "point is not a canonical Fr");
         const uint64_t nblk = (rows + BL - 1) / BL;
@@ -104,6 +104,7 @@ int eon_quotient_and_eval_columns_dev(eon_ctx* ctx, const eon_fr* coeffs, uint64
         ctx->prof.end(ctx->stream);
         hipLaunchKernelGGL(k_horner_carry, dim3((width + 63) / 64), dim3(64), 0, ctx->stream, totals, nblk,
                            width, pow_u64(z, BL), carries, reinterpret_cast<Fr*>(values));
+        if (!quotient || rows < 2) return Status::ok();  // values only
         ctx->prof.begin("k_horner_apply", rows * width * 64ull, ctx->stream);
         hipLaunchKernelGGL(k_horner_apply, dim3(grid), dim3(128), 0, ctx->stream, c, rows, width, z, carries,
                            reinterpret_cast<Fr*>(quotient));

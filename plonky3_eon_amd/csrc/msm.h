@@ -8,9 +8,24 @@ namespace eon {
 // sum_i scalars[i] * bases[i] for i < n; `scalars` is a device pointer (Fr Montgomery).
 Status msm_run(eon_ctx* ctx, const eon_msm_bases* bases, const Fr* scalars, uint64_t n,
                G1Affine* result);
-// one MSM per column of the row-major rows x width device matrix `scalars` (result on host)
+// one MSM per column of the row-major rows x width device matrix `scalars` (result on host,
+// unless out_host is null); with `keep`, the sorted digit pairs of every batch stay in it
 Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* bases, const Fr* scalars, uint64_t rows,
-                       uint32_t width, G1Affine* out_host);
+                       uint32_t width, G1Affine* out_host, eon_msm_scalars* keep);
+// out_host[t * width + j] = MSM of prepared column j against bases[t] (same window layout)
+Status msm_run_prepared(eon_ctx* ctx, const eon_msm_bases* const* bases, uint32_t nbases,
+                        const eon_msm_scalars* s, G1Affine* out_host);
+// bases from n device (or host) affine points; force_c != 0 fixes the window size (a bases
+// object whose MSMs reuse scalars prepared against another of that window size)
+Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32_t flags,
+                    bool device_ptr, eon_msm_bases** out, uint32_t force_c = 0,
+                    hipStream_t stream = nullptr, DevBuf* async_tmp = nullptr);
+// the bases' affine points on device, ABI form (radix-2^32 Montgomery, (0,0) = identity)
+const G1Affine* bases_points(const eon_msm_bases* b);
+uint32_t bases_window(const eon_msm_bases* b);
+bool bases_precomputed(const eon_msm_bases* b);
+// release a bases object (caller holds ctx->mu and has synchronised its work)
+void bases_free(eon_msm_bases* b);
 
 constexpr uint32_t BATCH = 32;  // points per thread in batched XYZZ -> affine conversion
 hipError_t launch_batch_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out, hipStream_t st);

@@ -54,9 +54,15 @@ struct eon_msm_bases {
     bool precomputed = false;
     uint32_t c = 0, windows = 0;
     DevBuf table;  // precomputed: n * windows affine points, entry i * windows + w = 2^(c*w) P_i
-    // the piece sums' source (table if precomputed, else points) holds 29-Montgomery coordinates
-    // and k_piece_sum29 runs (EON_MSM_R32=1 keeps radix-2^32 bases and k_piece_sum)
+    // radix-2^29 piece sums (EON_MSM_R32=1 keeps radix-2^32 bases and k_piece_sum): the piece
+    // sums read 29-Montgomery coordinates from `table` (precomputed) or `points29`; `points` stays
+    // in the ABI form (the KZG opening bases are derived from it)
     bool r29 = false;
+    DevBuf points29;
+    const G1Affine* piece_source() const {
+        if (precomputed) return table.as<G1Affine>();
+        return r29 ? points29.as<G1Affine>() : points.as<G1Affine>();
+    }
 };
 
 namespace eon {
@@ -168,6 +174,15 @@ __global__ void k_bucket_start(const uint32_t* keys, uint64_t E, uint32_t c, uin
         for (int64_t b = prev + 1; b <= cur; b++) start[b] = (uint32_t)i;
         prev = cur;
     }
+}
+
+// stat[0] = max over buckets of the pieces a bucket holds (atomicMax; stat[0] zeroed before)
+__global__ void k_max_pieces(const uint32_t* piece_off, uint32_t nb, uint32_t* stat) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t v = b < nb ? piece_off[b + 1] - piece_off[b] : 0u;
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o));
+    // one atomic per wave, and only while it can raise the maximum (~all waves see 2 or 3)
+    if ((threadIdx.x & 63) == 0 && v > 1 && v > __atomic_load_n(stat, __ATOMIC_RELAXED)) atomicMax(stat, v);
 }
 
 __global__ void k_piece_owner(const uint32_t* piece_off, uint32_t nb, uint32_t* owner) {
@@ -286,11 +301,12 @@ __global__ void k_table_to29(G1Affine* pts, uint64_t n) {
 
 // One combine level: new partial p of bucket b sums old partials
 // [off_old[b] + PIECE*j, min(+PIECE, off_old[b+1])), j = p - off_new[b].
+// The launch covers an upper bound of the new partial count; the count itself is off_new[nb].
 __global__ void k_partial_combine(const uint32_t* off_old, const uint32_t* off_new,
-                                  const uint32_t* owner, uint32_t n_new, const G1Xyzz* in,
+                                  const uint32_t* owner, uint32_t nb, const G1Xyzz* in,
                                   G1Xyzz* out) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_new) return;
+    if (p >= off_new[nb]) return;
     const uint32_t b = owner[p];
     const uint32_t j = p - off_new[b];
     const uint32_t e0 = off_old[b] + j * PIECE;
@@ -353,6 +369,34 @@ __global__ void __launch_bounds__(64) k_seg_level(const G1Xyzz* X, uint32_t L, u
     run = xyzz_add(run, ld_xyzz(x));
     st_xyzz(T + t, run);
     st_xyzz(U + t, acc);
+}
+
+// The first level of the weighted bucket sum fused with the bucket sums, straight from
+// k_piece_sum29's raw partials (radix 2^29, lazy): segment s of group g covers magnitudes
+// [s seg, s seg + seg); bucket m is the sum of its pieces [piece_off[b'], piece_off[b' + 1]),
+// b' = m groups + g (<= PIECE of them: used when no combine level is needed).  Same T / U as
+// k_seg_level over the bucket sums, at T[g nseg + s] / U[g nseg + s]; a wave covers consecutive
+// groups of one segment, so its piece reads are adjacent.
+__global__ void __launch_bounds__(64) k_bucket_reduce29(const G1Raw29* pieces, const uint32_t* piece_off,
+                                                        uint32_t B, uint32_t seg, uint32_t groups, G1Xyzz* T,
+                                                        G1Xyzz* U) {
+    const uint32_t nseg = B / seg;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nseg * groups) return;
+    const uint32_t g = t % groups, s = t / groups;
+    G1X29 run, acc, x;
+    bool run_inf = true, acc_inf = true;
+    for (int k = (int)seg - 1; k >= 0; k--) {
+        const uint32_t bp = (s * seg + (uint32_t)k) * groups + g;
+        const uint32_t e1 = piece_off[bp + 1];
+        for (uint32_t e = piece_off[bp]; e < e1; e++) {
+            const bool inf = ld_raw29(pieces + e, x);
+            acc29(run, run_inf, x, inf);
+        }
+        if (k >= 1) acc29(acc, acc_inf, run, run_inf);
+    }
+    st_xyzz(T + (uint64_t)g * nseg + s, x29_to_xyzz(run, run_inf));
+    st_xyzz(U + (uint64_t)g * nseg + s, x29_to_xyzz(acc, acc_inf));
 }
 
 constexpr uint32_t MAX_SEG_LEVELS = 24;
@@ -488,7 +532,8 @@ hipError_t launch_batch_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out, h
 }
 
 Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32_t flags,
-                    bool device_ptr, eon_msm_bases** out) {
+                    bool device_ptr, eon_msm_bases** out, uint32_t force_c, hipStream_t stream,
+                    DevBuf* async_tmp) {
     if (!out) return Status::err(EON_E_ARG, "null output handle");
     if (n && !bases) return Status::err(EON_E_ARG, "null bases");
     if (n > (1ull << 27)) return Status::err(EON_E_SHAPE, "at most 2^27 bases");
@@ -502,10 +547,13 @@ Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32
     eon_msm_bases* b = new eon_msm_bases();
     b->ctx = ctx;
     b->n = n;
-    hipStream_t st = ctx->stream;
+    // async_tmp: enqueue on `stream` and return without a sync, the precompute scratch parked in
+    // *async_tmp until the caller has synchronised the stream
+    hipStream_t st = async_tmp ? stream : ctx->stream;
     auto fail = [&](Status s) {
         b->points.release();
         b->table.release();
+        b->points29.release();
         delete b;
         return s;
     };
@@ -517,11 +565,12 @@ Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32
         if (e != hipSuccess) return fail(Status::err(EON_E_DEVICE, hipGetErrorString(e)));
     }
     b->precomputed = (flags & EON_MSM_PRECOMPUTE) != 0 && n > 0;
-    b->c = choose_c(n ? n : 1, b->precomputed);
+    b->c = force_c ? force_c : choose_c(n ? n : 1, b->precomputed);
     b->windows = (255 + b->c - 1) / b->c;
     if (b->precomputed) {
         const uint64_t m = n * b->windows;
-        DevBuf tmp;
+        DevBuf tmp_local;
+        DevBuf& tmp = async_tmp ? *async_tmp : tmp_local;
         if (tmp.ensure(m * sizeof(G1Xyzz)) != hipSuccess ||
             b->table.ensure(m * sizeof(G1Affine)) != hipSuccess) {
             tmp.release();
@@ -530,19 +579,27 @@ Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32
         hipLaunchKernelGGL(k_precompute_windows, dim3(blocks_for(n, 128)), dim3(128), 0, st,
                            b->points.as<G1Affine>(), n, b->c, b->windows, tmp.as<G1Xyzz>());
         e = launch_batch_to_affine(tmp.as<G1Xyzz>(), m, b->table.as<G1Affine>(), st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        tmp.release();
+        if (!async_tmp) {
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            tmp.release();
+        }
         if (e != hipSuccess) return fail(Status::err(EON_E_DEVICE, hipGetErrorString(e)));
     }
     b->r29 = getenv("EON_MSM_R32") == nullptr;
     if (b->r29 && n) {
         const uint64_t m = b->precomputed ? n * b->windows : n;
-        G1Affine* src = b->precomputed ? b->table.as<G1Affine>() : b->points.as<G1Affine>();
+        if (!b->precomputed) {
+            e = b->points29.ensure(n * sizeof(G1Affine));
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(b->points29.p, b->points.p, n * sizeof(G1Affine), hipMemcpyDeviceToDevice, st);
+            if (e != hipSuccess) return fail(Status::err(EON_E_OOM, "bases allocation failed"));
+        }
+        G1Affine* src = b->precomputed ? b->table.as<G1Affine>() : b->points29.as<G1Affine>();
         hipLaunchKernelGGL(k_table_to29, dim3(blocks_for(m, 256)), dim3(256), 0, st, src, m);
         e = hipGetLastError();
         if (e != hipSuccess) return fail(Status::err(EON_E_DEVICE, hipGetErrorString(e)));
     }
-    e = hipStreamSynchronize(st);
+    if (!async_tmp) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return fail(Status::err(EON_E_DEVICE, hipGetErrorString(e)));
     *out = b;
     return Status::ok();
@@ -558,12 +615,17 @@ Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32
 //                 leaves one XYZZ point per column in `out_dev`
 struct Batch {
     const Fr* scalars = nullptr;
-    uint32_t cols = 0;
+    uint32_t cols = 0, col0 = 0;
     G1Xyzz* out = nullptr;
     uint32_t c = 0, W = 0, B = 0, groups = 0, nb = 0, key_bits = 0, log_chunk = 0;
     uint64_t E = 0, max_pieces = 0;
     size_t sort_bytes = 0, scan_bytes = 0;
     uint32_t n_pieces = 0, n_pairs = 0;
+    uint32_t levels = 0;  // PIECE-way combine levels until every bucket holds <= 1 partial
+};
+
+struct SortedRef {
+    const uint32_t *keys, *vals, *start, *piece_off;
 };
 
 static bool msm_debug() {
@@ -571,12 +633,50 @@ static bool msm_debug() {
     return d;
 }
 
-static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint64_t ld, Batch& bt,
-                         MsmWork& wk, hipStream_t st) {
-    bt.c = b->precomputed ? b->c : choose_c(n, false);
-    bt.W = b->precomputed ? b->windows : (255 + bt.c - 1) / bt.c;
+// Layout of a batched column MSM of n-row columns against bases with this window layout: the
+// window size, window count and columns per batch (<= 2^28 digit pairs per batch).
+struct MsmLayout {
+    uint32_t c = 0, W = 0;
+    bool precomputed = false;
+    uint64_t cpb = 1;
+};
+
+static MsmLayout msm_layout(const eon_msm_bases* b, uint64_t n, uint32_t width) {
+    MsmLayout L;
+    L.precomputed = b->precomputed;
+    L.c = b->precomputed ? b->c : choose_c(n, false);
+    L.W = (255 + L.c - 1) / L.c;
+    // columns per batch: keep the digit pairs of one batch at <= 2^28 (4 GiB of sort buffers)
+    uint64_t cpb = (1ull << 28) / (n * L.W);
+    if (cpb < 1) cpb = 1;
+    const uint64_t max_groups = b->precomputed ? cpb : cpb * L.W;
+    if (max_groups > 65535) cpb = b->precomputed ? 65535 : 65535 / L.W;
+    // equal batches (164 columns -> 82 + 82, not 128 + 36): the two streams overlap evenly
+    const uint64_t n_batches = (width + cpb - 1) / cpb;
+    L.cpb = (width + n_batches - 1) / n_batches;
+    return L;
+}
+
+static std::vector<Batch> make_batches(const Fr* scalars, uint32_t width, uint64_t cpb) {
+    std::vector<Batch> batches;
+    for (uint32_t j0 = 0; j0 < width; j0 += (uint32_t)cpb) {
+        Batch bt;
+        bt.scalars = scalars + j0;
+        bt.col0 = j0;
+        bt.cols = (uint32_t)std::min<uint64_t>(cpb, width - j0);
+        batches.push_back(bt);
+    }
+    return batches;
+}
+
+// digits + radix sort + bucket starts + piece offsets of one batch into `out`; `wk` supplies the
+// unsorted pairs, the sort / scan scratch and the count read-back slots
+static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t ld, Batch& bt,
+                         MsmWork& wk, SortedBufs& out, hipStream_t st) {
+    bt.c = L.c;
+    bt.W = L.W;
     bt.B = 1u << (bt.c - 1);
-    bt.groups = b->precomputed ? bt.cols : bt.cols * bt.W;
+    bt.groups = L.precomputed ? bt.cols : bt.cols * bt.W;
     bt.nb = bt.groups * bt.B;
     bt.E = n * bt.W * bt.cols;
     if (bt.E >= (1ull << 32)) return Status::err(EON_E_SHAPE, "MSM too large for 32-bit pair indices");
@@ -589,26 +689,20 @@ static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint6
 
     EON_HIP(wk.keys.ensure(E * 4));
     EON_HIP(wk.vals.ensure(E * 4));
-    EON_HIP(wk.keys2.ensure(E * 4));
-    EON_HIP(wk.vals2.ensure(E * 4));
-    EON_HIP(wk.start.ensure((nb + 1) * 4ull));
+    EON_HIP(out.keys2.ensure(E * 4));
+    EON_HIP(out.vals2.ensure(E * 4));
+    EON_HIP(out.start.ensure((nb + 1) * 4ull));
+    EON_HIP(out.piece_off.ensure((nb + 1) * 4ull));
     EON_HIP(wk.count.ensure((nb + 1) * 4ull));
-    EON_HIP(wk.piece_off.ensure((nb + 1) * 4ull));
     EON_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bt.sort_bytes, wk.keys.as<uint32_t>(),
-                                               wk.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
-                                               wk.vals2.as<uint32_t>(), (int)E, 0, bt.key_bits, st));
+                                               out.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
+                                               out.vals2.as<uint32_t>(), (int)E, 0, bt.key_bits, st));
     EON_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bt.scan_bytes, wk.count.as<uint32_t>(),
-                                             wk.piece_off.as<uint32_t>(), (int)(nb + 1), st));
+                                             out.piece_off.as<uint32_t>(), (int)(nb + 1), st));
     EON_HIP(wk.temp.ensure(std::max(bt.sort_bytes, bt.scan_bytes)));
     bt.log_chunk = LOG_CHUNK_MIN;
     while (bt.log_chunk < LOG_CHUNK_MAX && (E >> (bt.log_chunk + 1)) >= (1ull << 20)) bt.log_chunk++;
     bt.max_pieces = (E >> bt.log_chunk) + nb + 1;  // >= the real piece count
-    EON_HIP(wk.owner.ensure(bt.max_pieces * 4));
-    EON_HIP(wk.piece_sums.ensure(bt.max_pieces * sizeof(G1Xyzz)));
-    EON_HIP(wk.piece_sums2.ensure(bt.max_pieces * sizeof(G1Xyzz)));
-    if (b->r29) EON_HIP(wk.piece_raw.ensure(bt.max_pieces * sizeof(G1Raw29)));
-    EON_HIP(wk.bucket_sums.ensure((uint64_t)nb * sizeof(G1Xyzz)));
-    EON_HIP(wk.off2.ensure((nb + 1) * 4ull));
     if (!wk.host_counts) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&wk.host_counts), 64));
 
     Profiler* prof = &ctx->prof;
@@ -617,27 +711,35 @@ static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint6
     const uint32_t tile_rows = 256 / tile_cols;
     hipLaunchKernelGGL(k_msm_digits, dim3((unsigned)((n + tile_rows - 1) / tile_rows),
                                           (bt.cols + tile_cols - 1) / tile_cols),
-                       dim3(256), 0, st, bt.scalars, n, ld, bt.cols, bt.c, bt.W, (uint32_t)b->precomputed,
+                       dim3(256), 0, st, bt.scalars, n, ld, bt.cols, bt.c, bt.W, (uint32_t)L.precomputed,
                        tile_cols, wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>());
     prof->end(st);
     EON_HIP(hipGetLastError());
     prof->begin("radix_sort_pairs", E * 16, st);
     EON_HIP(hipcub::DeviceRadixSort::SortPairs(wk.temp.p, bt.sort_bytes, wk.keys.as<uint32_t>(),
-                                               wk.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
-                                               wk.vals2.as<uint32_t>(), (int)E, 0, bt.key_bits, st));
+                                               out.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
+                                               out.vals2.as<uint32_t>(), (int)E, 0, bt.key_bits, st));
     prof->end(st);
     hipLaunchKernelGGL(k_bucket_start, dim3(blocks_for(E / 4 + 1, 256)), dim3(256), 0, st,
-                       wk.keys2.as<uint32_t>(), E, bt.c, bt.groups, nb, wk.start.as<uint32_t>());
+                       out.keys2.as<uint32_t>(), E, bt.c, bt.groups, nb, out.start.as<uint32_t>());
     hipLaunchKernelGGL(k_chunk_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st,
-                       wk.start.as<uint32_t>(), nb, bt.log_chunk, wk.count.as<uint32_t>());
+                       out.start.as<uint32_t>(), nb, bt.log_chunk, wk.count.as<uint32_t>());
     EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, bt.scan_bytes, wk.count.as<uint32_t>(),
-                                             wk.piece_off.as<uint32_t>(), (int)(nb + 1), st));
-    // launches are sized by the real counts (8-byte read-back: pieces, nonzero digits)
-    EON_HIP(hipMemcpyAsync(wk.host_counts, wk.piece_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
-    EON_HIP(hipMemcpyAsync(wk.host_counts + 1, wk.start.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
+                                             out.piece_off.as<uint32_t>(), (int)(nb + 1), st));
+    // the most pieces one bucket holds fixes the combine levels (no read-backs in the reduction)
+    EON_HIP(wk.stat.ensure(16));
+    EON_HIP(hipMemsetAsync(wk.stat.p, 0, 16, st));
+    hipLaunchKernelGGL(k_max_pieces, dim3(blocks_for(nb, 256)), dim3(256), 0, st, out.piece_off.as<uint32_t>(),
+                       nb, wk.stat.as<uint32_t>());
+    // launches are sized by the real counts (12-byte read-back: pieces, nonzero digits, max pieces)
+    EON_HIP(hipMemcpyAsync(wk.host_counts, out.piece_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
+    EON_HIP(hipMemcpyAsync(wk.host_counts + 1, out.start.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
+    EON_HIP(hipMemcpyAsync(wk.host_counts + 3, wk.stat.p, 4, hipMemcpyDeviceToHost, st));
     EON_HIP(hipStreamSynchronize(st));
     bt.n_pieces = wk.host_counts[0];
     bt.n_pairs = wk.host_counts[1];
+    bt.levels = 0;
+    for (uint64_t m = wk.host_counts[3]; m > 1; m = (m + PIECE - 1) / PIECE) bt.levels++;
     if (msm_debug())
         fprintf(stderr, "msm_batch n=%llu cols=%u c=%u W=%u nb=%u E=%llu pairs=%u pieces=%u\n",
                 (unsigned long long)n, bt.cols, bt.c, bt.W, nb, (unsigned long long)E, bt.n_pairs,
@@ -645,9 +747,32 @@ static Status batch_sort(eon_ctx* ctx, const eon_msm_bases* b, uint64_t n, uint6
     return Status::ok();
 }
 
-static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt, MsmWork& wk,
-                           hipStream_t st) {
-    const G1Affine* pts = b->precomputed ? b->table.as<G1Affine>() : b->points.as<G1Affine>();
+static SortedRef sorted_ref(const SortedBufs& s) {
+    return SortedRef{s.keys2.as<uint32_t>(), s.vals2.as<uint32_t>(), s.start.as<uint32_t>(),
+                     s.piece_off.as<uint32_t>()};
+}
+
+// the reduction reads k_piece_sum29's raw partials directly (k_bucket_reduce29): radix-2^29
+// pieces, no combine level needed, the many-groups weighted sum
+static bool fused_reduce(const eon_msm_bases* b, const Batch& bt) {
+    static const bool off = getenv("EON_MSM_UNFUSED") != nullptr;
+    return !off && b->r29 && bt.levels <= 1 && bt.groups >= 64 && bt.B >= SEG;
+}
+
+// piece sums of one sorted batch against bases `b` (asynchronous); wk supplies the piece buffers
+static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt, const SortedRef& sr,
+                           MsmWork& wk, hipStream_t st) {
+    EON_HIP(wk.piece_sums.ensure(bt.max_pieces * sizeof(G1Xyzz)));
+    EON_HIP(wk.piece_sums2.ensure(bt.max_pieces * sizeof(G1Xyzz)));
+    EON_HIP(wk.owner.ensure(bt.max_pieces * 4));
+    EON_HIP(wk.bucket_sums.ensure((uint64_t)bt.nb * sizeof(G1Xyzz)));
+    EON_HIP(wk.off2.ensure((bt.nb + 1) * 4ull));
+    EON_HIP(wk.off3.ensure((bt.nb + 1) * 4ull));
+    EON_HIP(wk.count.ensure((bt.nb + 1) * 4ull));
+    EON_HIP(wk.temp.ensure(bt.scan_bytes));
+    if (b->r29) EON_HIP(wk.piece_raw.ensure(bt.max_pieces * sizeof(G1Raw29)));
+    if (!wk.host_counts) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&wk.host_counts), 64));
+    const G1Affine* pts = b->piece_source();
     // algorithmic bytes: every nonzero digit reads its 4-byte key, 4-byte reference and 64-byte
     // affine base; every piece writes one 128-byte XYZZ partial
     // mulmods: one XYZZ mixed addition (madd-2008-s, 8M + 2S) per nonzero digit
@@ -656,16 +781,13 @@ static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt
     uint32_t blocks = blocks_for(((uint64_t)bt.n_pairs + (1u << bt.log_chunk) - 1) >> bt.log_chunk, 64);
     if (ctx->piece_block_cap) blocks = std::min(blocks, ctx->piece_block_cap);
     if (bt.n_pairs && b->r29)
-        hipLaunchKernelGGL(k_piece_sum29, dim3(blocks), dim3(64), 0, st, wk.keys2.as<uint32_t>(),
-                           wk.vals2.as<uint32_t>(), wk.start.as<uint32_t>(), wk.piece_off.as<uint32_t>(),
+        hipLaunchKernelGGL(k_piece_sum29, dim3(blocks), dim3(64), 0, st, sr.keys, sr.vals, sr.start, sr.piece_off,
                            bt.n_pairs, bt.log_chunk, bt.c, bt.groups, bt.nb, pts, wk.piece_raw.as<G1Raw29>());
     else if (bt.n_pairs)
-        hipLaunchKernelGGL(k_piece_sum, dim3(blocks),
-                           dim3(64), 0, st, wk.keys2.as<uint32_t>(), wk.vals2.as<uint32_t>(),
-                           wk.start.as<uint32_t>(), wk.piece_off.as<uint32_t>(), bt.n_pairs,
-                           bt.log_chunk, bt.c, bt.groups, bt.nb, pts, wk.piece_sums.as<G1Xyzz>());
+        hipLaunchKernelGGL(k_piece_sum, dim3(blocks), dim3(64), 0, st, sr.keys, sr.vals, sr.start, sr.piece_off,
+                           bt.n_pairs, bt.log_chunk, bt.c, bt.groups, bt.nb, pts, wk.piece_sums.as<G1Xyzz>());
     ctx->prof.end(st);
-    if (bt.n_pieces && b->r29)
+    if (bt.n_pieces && b->r29 && !fused_reduce(b, bt))
         hipLaunchKernelGGL(k_raw29_to_xyzz, dim3(blocks_for(bt.n_pieces, 128)), dim3(128), 0, st,
                            wk.piece_raw.as<G1Raw29>(), bt.n_pieces, wk.piece_sums.as<G1Xyzz>());
     EON_HIP(hipGetLastError());
@@ -673,11 +795,11 @@ static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt
 }
 
 // per-column output step shared by both bucket reductions
-static Status write_columns(const eon_msm_bases* b, const Batch& bt, const G1Xyzz* per_group,
+static Status write_columns(const MsmLayout& L, const Batch& bt, const G1Xyzz* per_group,
                             hipStream_t st) {
     // one point per group; per column: the group itself (fixed base) or the Horner combination of
     // its windows
-    if (!b->precomputed) {
+    if (!L.precomputed) {
         hipLaunchKernelGGL(k_window_horner, dim3(blocks_for(bt.cols, 64)), dim3(64), 0, st, per_group,
                            bt.cols, bt.W, bt.c, bt.out);
         EON_HIP(hipGetLastError());
@@ -688,7 +810,7 @@ static Status write_columns(const eon_msm_bases* b, const Batch& bt, const G1Xyz
 }
 
 // sum_d d * B_d per group, few-groups form: k_segment_sum + LDS trees (short dependency chains)
-static Status reduce_segments(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt, MsmWork& wk,
+static Status reduce_segments(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, MsmWork& wk,
                               hipStream_t st) {
     const uint32_t nseg = bt.B / SEG;  // c >= 4, so B >= SEG
     const uint32_t groups = bt.groups;
@@ -708,44 +830,48 @@ static Status reduce_segments(eon_ctx* ctx, const eon_msm_bases* b, const Batch&
         len = blk;
     }
     EON_HIP(hipGetLastError());
-    return write_columns(b, bt, cur, st);
+    return write_columns(L, bt, cur, st);
 }
 
-static Status batch_reduce(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, MsmWork& wk,
-                           hipStream_t st) {
+// combine levels, bucket sums and the weighted bucket reduction of one batch's pieces (read-back
+// of each level's count synchronises `st`); leaves one XYZZ point per column at bt.out.  The
+// sorted piece offsets are only read (a prepared batch is reduced once per bases object).
+static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, const SortedRef& sr,
+                           MsmWork& wk, hipStream_t st, bool fused) {
     Profiler* prof = &ctx->prof;
     const uint32_t nb = bt.nb, groups = bt.groups, B = bt.B;
     // combine levels until every bucket holds one partial (skewed scalars put many pieces in a
     // bucket: all-equal scalars put n pieces in one bucket per window)
-    uint32_t* off_cur = wk.piece_off.as<uint32_t>();
-    uint32_t* off_nxt = wk.off2.as<uint32_t>();
+    const uint32_t* off_cur = sr.piece_off;
+    uint32_t* off_bufs[2] = {wk.off2.as<uint32_t>(), wk.off3.as<uint32_t>()};
+    int next_off = 0;
     G1Xyzz* part_cur = wk.piece_sums.as<G1Xyzz>();
     G1Xyzz* part_nxt = wk.piece_sums2.as<G1Xyzz>();
-    uint32_t n_pieces = bt.n_pieces;
-    for (int level = 0; level < 8; level++) {
+    uint64_t bound = bt.n_pieces;  // >= the partials of the current level
+    size_t scan_bytes = bt.scan_bytes;
+    for (uint32_t level = 0; level < (fused ? 0u : bt.levels); level++) {
+        uint32_t* off_nxt = off_bufs[next_off];
         hipLaunchKernelGGL(k_level_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st, off_cur,
                            nb, wk.count.as<uint32_t>());
-        EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, bt.scan_bytes, wk.count.as<uint32_t>(),
+        EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, scan_bytes, wk.count.as<uint32_t>(),
                                                  off_nxt, (int)(nb + 1), st));
-        EON_HIP(hipMemcpyAsync(wk.host_counts + 2, off_nxt + nb, 4, hipMemcpyDeviceToHost, st));
-        EON_HIP(hipStreamSynchronize(st));
-        const uint32_t n_new = wk.host_counts[2];
-        if (msm_debug()) fprintf(stderr, "  level %d: %u -> %u partials\n", level, n_pieces, n_new);
-        if (n_new == n_pieces) break;  // every bucket already holds at most one partial
         hipLaunchKernelGGL(k_piece_owner, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_nxt, nb,
                            wk.owner.as<uint32_t>());
-        prof->begin("k_partial_combine", (uint64_t)(n_pieces + n_new) * 128, st,
-                    (uint64_t)(n_pieces - n_new) * 14);  // add-2008-s: 12M + 2S
-        hipLaunchKernelGGL(k_partial_combine, dim3(blocks_for(n_new, 64)), dim3(64), 0, st, off_cur,
-                           off_nxt, wk.owner.as<uint32_t>(), n_new, part_cur, part_nxt);
+        // sum_b ceil(p_b / PIECE) <= min(bound, nb + bound / PIECE)
+        const uint64_t nxt = std::min<uint64_t>(bound, nb + bound / PIECE);
+        prof->begin("k_partial_combine", (bound + nxt) * 128, st, (bound - std::min(bound, nxt)) * 14);
+        hipLaunchKernelGGL(k_partial_combine, dim3(blocks_for(nxt, 64)), dim3(64), 0, st, off_cur, off_nxt,
+                           wk.owner.as<uint32_t>(), nb, part_cur, part_nxt);
         prof->end(st);
-        std::swap(off_cur, off_nxt);
+        off_cur = off_nxt;
+        next_off ^= 1;
         std::swap(part_cur, part_nxt);
-        n_pieces = n_new;
+        bound = nxt;
     }
-    hipLaunchKernelGGL(k_bucket_final, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_cur, B, groups,
-                       part_cur, wk.bucket_sums.as<G1Xyzz>());
-    if (groups < 64) return reduce_segments(ctx, b, bt, wk, st);
+    if (!fused)
+        hipLaunchKernelGGL(k_bucket_final, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_cur, B, groups,
+                           part_cur, wk.bucket_sums.as<G1Xyzz>());
+    if (groups < 64) return reduce_segments(ctx, L, bt, wk, st);
     // sum_d d * B_d = W(S) + T(S) per group (bucket b holds digit b + 1), level by level
     G1Xyzz* t_buf[2] = {wk.piece_sums.as<G1Xyzz>(), wk.piece_sums.as<G1Xyzz>() + (uint64_t)groups * (B / 2)};
     G1Xyzz* u_buf = wk.piece_sums2.as<G1Xyzz>();
@@ -756,14 +882,18 @@ static Status batch_reduce(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, MsmW
     G1Xyzz* usum = wk.levels.as<G1Xyzz>();
     SegLogs logs{};
     const G1Xyzz* X = wk.bucket_sums.as<G1Xyzz>();
-    uint32_t L = B, m = 0;
+    uint32_t Lb = B, m = 0;
     prof->begin("k_seg_level", (uint64_t)nb * 128 + (uint64_t)nb / SEG * 256, st);
-    while (L > 1) {
-        const uint32_t seg = L < SEG ? L : SEG;
-        const uint32_t nseg = L / seg;
+    while (Lb > 1) {
+        const uint32_t seg = Lb < SEG ? Lb : SEG;
+        const uint32_t nseg = Lb / seg;
         G1Xyzz* T = t_buf[m & 1];
-        hipLaunchKernelGGL(k_seg_level, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
-                           X, L, seg, groups, T, u_buf);
+        if (fused && m == 0)
+            hipLaunchKernelGGL(k_bucket_reduce29, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
+                               wk.piece_raw.as<G1Raw29>(), sr.piece_off, Lb, seg, groups, T, u_buf);
+        else
+            hipLaunchKernelGGL(k_seg_level, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
+                               X, Lb, seg, groups, T, u_buf);
         // usum[m] = sum over the group's nseg U values
         const G1Xyzz* cur = u_buf;
         uint32_t len = nseg;
@@ -782,7 +912,7 @@ static Status batch_reduce(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, MsmW
                                    hipMemcpyDeviceToDevice, st));
         logs.v[m] = (uint8_t)(31 - __builtin_clz(seg));
         X = T;
-        L = nseg;
+        Lb = nseg;
         m++;
     }
     G1Xyzz* per_group = wk.red_a.as<G1Xyzz>();
@@ -790,51 +920,103 @@ static Status batch_reduce(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, MsmW
                        X, per_group);
     prof->end(st);
     EON_HIP(hipGetLastError());
-    return write_columns(b, bt, per_group, st);
+    return write_columns(L, bt, per_group, st);
+}
+
+}  // namespace eon
+
+// Prepared scalars: every batch's digit pairs sorted once and kept on device, so that MSMs of the
+// same scalar columns against other bases objects of the same window layout skip the digit
+// extraction and the sort (KzgPcs: the SRS for the commitment, then the opening bases H(z) of
+// every opening point, kzg/src/pcs.rs:244-251,297-330).  The scalars themselves are not retained.
+struct eon_msm_scalars {
+    eon_ctx* ctx = nullptr;
+    uint64_t n = 0;
+    uint32_t width = 0;
+    eon::MsmLayout layout;
+    std::vector<eon::Batch> batches;
+    std::vector<eon::SortedBufs> sorted;
+    // buffers go back to the context's cache (caller holds ctx->mu)
+    ~eon_msm_scalars() {
+        constexpr size_t CAP = 48ull << 30;  // MSM_SORTED_CACHE_CAP
+        size_t cached = 0;
+        if (ctx)
+            for (const auto& sb : ctx->sorted_cache) cached += sb.bytes();
+        for (auto& sb : sorted) {
+            if (ctx && cached + sb.bytes() <= CAP) {
+                cached += sb.bytes();
+                ctx->sorted_cache.push_back(std::move(sb));
+                sb = eon::SortedBufs{};
+            } else {
+                sb.release();
+            }
+        }
+    }
+};
+
+namespace eon {
+
+const G1Affine* bases_points(const eon_msm_bases* b) { return b->points.as<G1Affine>(); }
+
+void bases_free(eon_msm_bases* b) {
+    b->points.release();
+    b->table.release();
+    b->points29.release();
+    delete b;
+}
+
+uint32_t bases_window(const eon_msm_bases* b) { return b->c; }
+
+bool bases_precomputed(const eon_msm_bases* b) { return b->precomputed; }
+
+static SortedBufs& wks_sorted(eon_ctx* ctx, size_t w) {
+    MsmWork* wks[3] = {&ctx->msm, &ctx->msm_b, &ctx->msm_c};
+    return wks[w]->sorted;
+}
+
+static Status identity_columns(uint32_t width, G1Affine* out_host) {
+    // G1::multi_exp returns the identity for empty input (curve.rs:163-165)
+    for (uint32_t j = 0; j < width; j++) {
+        out_host[j].x = Fq::zero();
+        out_host[j].y = Fq::zero();
+    }
+    return Status::ok();
 }
 
 Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, uint64_t n,
-                       uint32_t width, G1Affine* out_host) {
+                       uint32_t width, G1Affine* out_host, eon_msm_scalars* keep) {
     if (n > b->n) return Status::err(EON_E_SHAPE, "more scalars than bases");
-    if (width == 0) return Status::ok();
-    if (n == 0) {  // G1::multi_exp returns the identity for empty input (curve.rs:163-165)
-        for (uint32_t j = 0; j < width; j++) {
-            out_host[j].x = Fq::zero();
-            out_host[j].y = Fq::zero();
-        }
-        return Status::ok();
+    if (keep) {
+        keep->ctx = ctx;
+        keep->n = n;
+        keep->width = width;
+        keep->layout = msm_layout(b, n ? n : 1, width ? width : 1);
     }
-    const uint32_t c = b->precomputed ? b->c : choose_c(n, false);
-    const uint64_t W = (255 + c - 1) / c;
-    // columns per batch: keep the digit pairs of one batch at <= 2^28 (4 GiB of sort buffers)
-    uint64_t cpb = (1ull << 28) / (n * W);
-    if (cpb < 1) cpb = 1;
-    const uint64_t max_groups = b->precomputed ? cpb : cpb * W;
-    if (max_groups > 65535) cpb = b->precomputed ? 65535 : 65535 / W;
-    // equal batches (164 columns -> 82 + 82, not 128 + 36): the two streams overlap evenly
-    const uint64_t n_batches = (width + cpb - 1) / cpb;
-    cpb = (width + n_batches - 1) / n_batches;
+    if (width == 0) return Status::ok();
+    if (n == 0) return out_host ? identity_columns(width, out_host) : Status::ok();
+    const MsmLayout L = msm_layout(b, n, width);
     // every batch leaves XYZZ results; one batched XYZZ -> affine conversion at the end (the
     // conversion is an inversion-latency-bound launch, so it is paid once per call)
     EON_HIP(ctx->msm.results.ensure(width * (sizeof(G1Affine) + sizeof(G1Xyzz))));
     G1Affine* res = ctx->msm.results.as<G1Affine>();
     G1Xyzz* res_xyzz = reinterpret_cast<G1Xyzz*>(res + width);
-
-    std::vector<Batch> batches;
-    for (uint32_t j0 = 0; j0 < width; j0 += (uint32_t)cpb) {
-        Batch bt;
-        bt.scalars = scalars + j0;
-        bt.cols = (uint32_t)std::min<uint64_t>(cpb, width - j0);
-        bt.out = res_xyzz + j0;
-        batches.push_back(bt);
+    std::vector<Batch> batches = make_batches(scalars, width, L.cpb);
+    for (Batch& bt : batches) bt.out = res_xyzz + bt.col0;
+    // sorted pairs land in the workspace of batch k % 3, or, when kept, in buffers of their own
+    if (keep) {
+        keep->sorted.resize(batches.size());
+        for (auto& sb : keep->sorted) {
+            if (ctx->sorted_cache.empty()) break;
+            sb = std::move(ctx->sorted_cache.back());
+            ctx->sorted_cache.back() = SortedBufs{};
+            ctx->sorted_cache.pop_back();
+        }
     }
-    // Three streams: every digit sort on the high-priority sort stream (so its memory-bound
-    // kernels get CU slots while a piece-sum launch fills the chip), piece sums + reductions
-    // alternating between the context stream and the side stream (batch k's reduction overlaps
-    // batch k+1's piece sums).  Three workspaces (batch k uses k % 3): sort(k+1) only waits for
-    // reduce(k-2), which finished while pieces(k-1) ran -- with two, it waited for reduce(k-1),
-    // starved by pieces(k), and the sort ended up exposed.  Events order sort(k) after
-    // reduce(k - 3) and pieces(k) after sort(k).
+    auto sorted_of = [&](size_t k) -> SortedBufs& { return keep ? keep->sorted[k] : wks_sorted(ctx, k % 3); };
+    // Three streams: every digit sort on the high-priority sort stream, piece sums + reductions
+    // alternating between the context stream and the side stream.  Three workspaces (batch k uses
+    // k % 3): sort(k+1) only waits for reduce(k-2).  Events order sort(k) after reduce(k - 3)
+    // and pieces(k) after sort(k).
     const bool masked = ctx->msm_sort_cus > 0;
     hipStream_t comp[2] = {masked ? ctx->msm_comp[0] : ctx->stream, masked ? ctx->msm_comp[1] : ctx->msm_side};
     hipStream_t sort_st = ctx->msm_sort;
@@ -846,17 +1028,24 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
     auto sort_batch = [&](size_t k) -> Status {
         const int w = (int)(k % 3);
         if (k >= 3) EON_HIP(hipStreamWaitEvent(sort_st, ctx->msm_reduced[w], 0));
-        EON_TRY(batch_sort(ctx, b, n, width, batches[k], *wks[w], sort_st));
+        EON_TRY(batch_sort(ctx, L, n, width, batches[k], *wks[w], sorted_of(k), sort_st));
         EON_HIP(hipEventRecord(ctx->msm_sorted[w], sort_st));
         return Status::ok();
+    };
+    auto pieces = [&](size_t k) -> Status {
+        const int i = (int)(k & 1), w = (int)(k % 3);
+        EON_HIP(hipStreamWaitEvent(comp[i], ctx->msm_sorted[w], 0));
+        return batch_pieces(ctx, b, batches[k], sorted_ref(sorted_of(k)), *wks[w], comp[i]);
     };
     EON_TRY(sort_batch(0));
     for (size_t k = 0; k < batches.size(); k++) {
         const int i = (int)(k & 1), w = (int)(k % 3);
-        EON_HIP(hipStreamWaitEvent(comp[i], ctx->msm_sorted[w], 0));
-        EON_TRY(batch_pieces(ctx, b, batches[k], *wks[w], comp[i]));
+        // pieces(k + 1) is enqueued only after reduce(k)'s read-backs: launched earlier it starves
+        // the latency-bound reduction (measured +20 ms per prove)
+        EON_TRY(pieces(k));
         if (k + 1 < batches.size()) EON_TRY(sort_batch(k + 1));
-        EON_TRY(batch_reduce(ctx, b, batches[k], *wks[w], comp[i]));
+        EON_TRY(batch_reduce(ctx, L, batches[k], sorted_ref(sorted_of(k)), *wks[w], comp[i],
+                             fused_reduce(b, batches[k])));
         EON_HIP(hipEventRecord(ctx->msm_reduced[w], comp[i]));
     }
     // the context stream resumes after both compute streams' last reductions
@@ -865,15 +1054,69 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
         EON_HIP(hipEventRecord(ctx->msm_ev[1 + i], comp[i]));
         EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[1 + i], 0));
     }
+    if (keep) {
+        keep->batches = batches;
+        for (Batch& bt : keep->batches) bt.scalars = nullptr;
+    }
     EON_HIP(launch_batch_to_affine(res_xyzz, width, res, ctx->stream));
-    EON_HIP(hipMemcpyAsync(out_host, res, width * sizeof(G1Affine), hipMemcpyDeviceToHost, ctx->stream));
+    if (out_host)
+        EON_HIP(hipMemcpyAsync(out_host, res, width * sizeof(G1Affine), hipMemcpyDeviceToHost, ctx->stream));
+    EON_HIP(hipStreamSynchronize(ctx->stream));
+    return Status::ok();
+}
+
+// out_host[t * width + j] = MSM of column j against bases[t]
+Status msm_run_prepared(eon_ctx* ctx, const eon_msm_bases* const* bases, uint32_t nbases,
+                        const eon_msm_scalars* s, G1Affine* out_host) {
+    const uint32_t width = s->width;
+    if (width == 0 || nbases == 0) return Status::ok();
+    for (uint32_t t = 0; t < nbases; t++) {
+        const eon_msm_bases* b = bases[t];
+        if (!b) return Status::err(EON_E_ARG, "null bases");
+        if (s->n > b->n) return Status::err(EON_E_SHAPE, "more scalars than bases");
+        const MsmLayout L = msm_layout(b, s->n ? s->n : 1, width);
+        if (L.c != s->layout.c || L.precomputed != s->layout.precomputed)
+            return Status::err(EON_E_SHAPE, "bases window layout differs from the prepared scalars'");
+    }
+    if (s->n == 0) {
+        for (uint32_t t = 0; t < nbases; t++) identity_columns(width, out_host + (uint64_t)t * width);
+        return Status::ok();
+    }
+    const uint64_t total = (uint64_t)width * nbases;
+    EON_HIP(ctx->msm.results.ensure(total * (sizeof(G1Affine) + sizeof(G1Xyzz))));
+    G1Affine* res = ctx->msm.results.as<G1Affine>();
+    G1Xyzz* res_xyzz = reinterpret_cast<G1Xyzz*>(res + total);
+    // jobs (batch k, bases t) round-robin over three streams and three workspaces, enqueued
+    // without a host wait (the reductions have no read-backs): a piece-sum launch is always
+    // queued, and each job's latency-bound reduction runs in the slots the others leave.  A
+    // workspace is reused only by its own stream, three jobs later.
+    hipStream_t comp[3] = {ctx->stream, ctx->msm_side, ctx->msm_side2};
+    MsmWork* wks[3] = {&ctx->msm, &ctx->msm_b, &ctx->msm_c};
+    EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));
+    EON_HIP(hipStreamWaitEvent(ctx->msm_side, ctx->msm_ev[0], 0));
+    EON_HIP(hipStreamWaitEvent(ctx->msm_side2, ctx->msm_ev[0], 0));
+    for (size_t k = 0; k < s->batches.size(); k++)
+        for (uint32_t t = 0; t < nbases; t++) {
+            const size_t j = k * nbases + t;
+            Batch bt = s->batches[k];
+            bt.out = res_xyzz + (uint64_t)t * width + bt.col0;
+            const SortedRef sr = sorted_ref(s->sorted[k]);
+            EON_TRY(batch_pieces(ctx, bases[t], bt, sr, *wks[j % 3], comp[j % 3]));
+            EON_TRY(batch_reduce(ctx, s->layout, bt, sr, *wks[j % 3], comp[j % 3], fused_reduce(bases[t], bt)));
+        }
+    EON_HIP(hipEventRecord(ctx->msm_ev[1], ctx->msm_side));
+    EON_HIP(hipEventRecord(ctx->msm_ev[2], ctx->msm_side2));
+    EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[1], 0));
+    EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[2], 0));
+    EON_HIP(launch_batch_to_affine(res_xyzz, total, res, ctx->stream));
+    EON_HIP(hipMemcpyAsync(out_host, res, total * sizeof(G1Affine), hipMemcpyDeviceToHost, ctx->stream));
     EON_HIP(hipStreamSynchronize(ctx->stream));
     return Status::ok();
 }
 
 Status msm_run(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, uint64_t n,
                G1Affine* result) {
-    return msm_run_columns(ctx, b, scalars, n, 1, result);
+    return msm_run_columns(ctx, b, scalars, n, 1, result, nullptr);
 }
 
 }  // namespace eon
@@ -910,9 +1153,7 @@ void eon_msm_bases_destroy(eon_msm_bases* b) {
     std::lock_guard<std::mutex> lk(b->ctx->mu);
     (void)hipSetDevice(b->ctx->device);
     (void)hipStreamSynchronize(b->ctx->stream);
-    b->points.release();
-    b->table.release();
-    delete b;
+    eon::bases_free(b);
 }
 
 uint64_t eon_msm_bases_len(const eon_msm_bases* b) { return b ? b->n : 0; }
@@ -960,7 +1201,7 @@ int eon_msm_g1_columns_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_f
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
     std::vector<G1Affine> r(width);
-    Status s = msm_run_columns(ctx, bases, reinterpret_cast<const Fr*>(mat), rows, width, r.data());
+    Status s = msm_run_columns(ctx, bases, reinterpret_cast<const Fr*>(mat), rows, width, r.data(), nullptr);
     if (!s.bad())
         for (uint32_t j = 0; j < width; j++) out[j] = g1_to_abi(r[j]);
     return finish(ctx, s);
@@ -978,10 +1219,58 @@ int eon_msm_g1_columns(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* m
         const size_t bytes = (size_t)rows * width * sizeof(Fr);
         EON_HIP(ctx->stage_in.ensure(bytes ? bytes : 32));
         if (bytes) EON_HIP(hipMemcpyAsync(ctx->stage_in.p, mat, bytes, hipMemcpyHostToDevice, ctx->stream));
-        return msm_run_columns(ctx, bases, ctx->stage_in.as<Fr>(), rows, width, r.data());
+        return msm_run_columns(ctx, bases, ctx->stage_in.as<Fr>(), rows, width, r.data(), nullptr);
     }();
     if (!s.bad())
         for (uint32_t j = 0; j < width; j++) out[j] = g1_to_abi(r[j]);
+    return finish(ctx, s);
+}
+
+int eon_msm_g1_columns_prepare_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* mat,
+                                   uint64_t rows, uint32_t width, eon_g1_affine* out,
+                                   eon_msm_scalars** prepared) {
+    if (!ctx) return EON_E_ARG;
+    if (!bases || !prepared || (rows && width && !mat)) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    auto* keep = new eon_msm_scalars();
+    std::vector<G1Affine> r(width);
+    Status s = msm_run_columns(ctx, bases, reinterpret_cast<const Fr*>(mat), rows, width,
+                               out ? r.data() : nullptr, keep);
+    if (s.bad()) {
+        delete keep;
+        return finish(ctx, s);
+    }
+    if (out)
+        for (uint32_t j = 0; j < width; j++) out[j] = g1_to_abi(r[j]);
+    *prepared = keep;
+    return EON_OK;
+}
+
+void eon_msm_scalars_destroy(eon_msm_scalars* s) {
+    if (!s) return;
+    if (s->ctx) {
+        std::lock_guard<std::mutex> lk(s->ctx->mu);
+        (void)hipSetDevice(s->ctx->device);
+        (void)hipStreamSynchronize(s->ctx->stream);
+        delete s;
+        return;
+    }
+    delete s;
+}
+
+int eon_msm_g1_columns_prepared(eon_ctx* ctx, const eon_msm_bases* const* bases, uint32_t nbases,
+                                const eon_msm_scalars* prepared, eon_g1_affine* out) {
+    if (!ctx) return EON_E_ARG;
+    if (!prepared || (nbases && !bases) || (nbases && prepared->width && !out)) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    if (prepared->ctx && prepared->ctx != ctx) return finish(ctx, Status::err(EON_E_ARG, "prepared scalars of another context"));
+    const uint64_t total = (uint64_t)nbases * prepared->width;
+    std::vector<G1Affine> r(total);
+    Status s = msm_run_prepared(ctx, bases, nbases, prepared, r.data());
+    if (!s.bad())
+        for (uint64_t j = 0; j < total; j++) out[j] = g1_to_abi(r[j]);
     return finish(ctx, s);
 }
 

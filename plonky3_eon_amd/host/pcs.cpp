@@ -4,7 +4,11 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <array>
+#include <cstdlib>
+#include <cstring>
 #include <map>
+#include <mutex>
 
 namespace eon_host {
 
@@ -19,17 +23,70 @@ static void hip_check(hipError_t e, const char* what) {
                                      std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Freed buffers are kept (per device, exact size) for the next allocation of that size: a proof
+// allocates the same matrices every time (the LDE alone is 11 GB at the headline size), and
+// hipMalloc/hipFree of them per proof costs more than keeping them resident.  Capped at
+// CACHE_CAP bytes; dropped wholesale when an allocation fails.
+namespace {
+constexpr uint64_t CACHE_CAP = 48ull << 30;
+std::mutex cache_mu;
+std::multimap<std::pair<int, uint64_t>, void*> cache;
+uint64_t cached_bytes = 0;
+
+void* cache_take(uint64_t bytes) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(cache_mu);
+    auto it = cache.find({dev, bytes});
+    if (it == cache.end()) return nullptr;
+    void* p = it->second;
+    cache.erase(it);
+    cached_bytes -= bytes;
+    return p;
+}
+
+void cache_put(void* p, uint64_t bytes) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    {
+        std::lock_guard<std::mutex> lk(cache_mu);
+        if (cached_bytes + bytes <= CACHE_CAP) {
+            cache.emplace(std::make_pair(dev, bytes), p);
+            cached_bytes += bytes;
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
+
+void cache_drop() {
+    std::lock_guard<std::mutex> lk(cache_mu);
+    for (auto& kv : cache) (void)hipFree(kv.second);
+    cache.clear();
+    cached_bytes = 0;
+}
+}  // namespace
+
 DeviceBuffer::DeviceBuffer(uint64_t bytes) : bytes_(bytes) {
-    if (bytes) hip_check(hipMalloc(&p_, bytes), "hipMalloc");
+    if (!bytes) return;
+    p_ = cache_take(bytes);
+    if (p_) return;
+    hipError_t e = hipMalloc(&p_, bytes);
+    if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        cache_drop();
+        e = hipMalloc(&p_, bytes);
+    }
+    hip_check(e, "hipMalloc");
 }
 
 DeviceBuffer::~DeviceBuffer() {
-    if (p_) (void)hipFree(p_);
+    if (p_) cache_put(p_, bytes_);
 }
 
 DeviceBuffer& DeviceBuffer::operator=(DeviceBuffer&& o) noexcept {
     if (this != &o) {
-        if (p_) (void)hipFree(p_);
+        if (p_) cache_put(p_, bytes_);
         p_ = o.p_;
         bytes_ = o.bytes_;
         o.p_ = nullptr;
@@ -87,10 +144,28 @@ KzgPcs::KzgPcs(eon_ctx* ctx, uint64_t max_degree, const Fr& srs_alpha) : ctx_(ct
     check(ctx_, eon_msm_bases_create_dev(ctx_, pts.as<eon_g1_affine>(), n, EON_MSM_PRECOMPUTE, &bases_),
           "eon_msm_bases_create_dev");
     check(ctx_, eon_ctx_synchronize(ctx_), "eon_ctx_synchronize");
+    const char* mode = getenv("EON_KZG_OPEN");
+    keep_digits_ = !(mode && std::strcmp(mode, "quotient") == 0);
+    // the auxiliary context: its own non-blocking stream, so that its work overlaps this
+    // context's even when that one runs on the legacy null stream
+    const int dev = eon_ctx_device(ctx_);
+    hipStream_t s = nullptr;
+    if (eon_ctx_create(dev, &aux_) == EON_OK) {
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+            eon_ctx_set_stream(aux_, s) == EON_OK) {
+            aux_stream_ = s;
+        } else {
+            if (s) (void)hipStreamDestroy(s);
+            eon_ctx_destroy(aux_);
+            aux_ = nullptr;
+        }
+    }
 }
 
 KzgPcs::~KzgPcs() {
     if (bases_) eon_msm_bases_destroy(bases_);
+    if (aux_) eon_ctx_destroy(aux_);
+    if (aux_stream_) (void)hipStreamDestroy(static_cast<hipStream_t>(aux_stream_));
 }
 
 Domain KzgPcs::natural_domain_for_degree(uint64_t degree) const {
@@ -103,26 +178,51 @@ void KzgPcs::ensure_supported(uint64_t degree) const {
                     "degree " + std::to_string(degree) + " > max " + std::to_string(max_degree_));
 }
 
-void KzgPcs::commit(std::vector<std::pair<Domain, DeviceMatrix>> evaluations,
-                    std::vector<std::vector<eon_g1_affine>>& commitments, std::vector<MatrixProverData>& data) {
+void KzgPcs::commit_coeffs(std::vector<std::pair<Domain, DeviceMatrix>> evaluations,
+                           std::vector<MatrixProverData>& data) {
     for (auto& [domain, evals] : evaluations) {
         const uint64_t h = evals.height;
         const uint32_t w = evals.width;
         if (h != domain.size()) throw Error(EON_E_SHAPE, "evaluation height must match domain size");
         ensure_supported(h > 0 ? h - 1 : 0);
-        MatrixProverData d{domain, std::move(evals), DeviceMatrix::alloc(h, w)};
+        MatrixProverData d{domain, std::move(evals), DeviceMatrix::alloc(h, w), nullptr};
         const eon_fr s = domain.shift.abi();
         check(ctx_, eon_coset_idft_batch_dev(ctx_, d.evals.data(), d.coeffs.mutable_data(), h, w, &s),
               "coset_idft_batch");
-        std::vector<eon_g1_affine> cm(w);
-        check(ctx_, eon_msm_g1_columns_dev(ctx_, bases_, d.coeffs.data(), h, w, cm.data()), "commit_column");
-        commitments.push_back(std::move(cm));
         data.push_back(std::move(d));
+    }
+    check(ctx_, eon_ctx_synchronize(ctx_), "coset_idft_batch");
+}
+
+void KzgPcs::commit_columns(std::vector<MatrixProverData>& data, size_t first,
+                            std::vector<std::vector<eon_g1_affine>>& commitments) {
+    for (size_t k = first; k < data.size(); k++) {
+        MatrixProverData& d = data[k];
+        const uint64_t h = d.coeffs.height;
+        const uint32_t w = d.coeffs.width;
+        std::vector<eon_g1_affine> cm(w);
+        if (keep_digits_) {
+            eon_msm_scalars* prep = nullptr;
+            check(ctx_, eon_msm_g1_columns_prepare_dev(ctx_, bases_, d.coeffs.data(), h, w, cm.data(), &prep),
+                  "commit_column");
+            d.prepared.reset(prep);
+        } else {
+            check(ctx_, eon_msm_g1_columns_dev(ctx_, bases_, d.coeffs.data(), h, w, cm.data()), "commit_column");
+        }
+        commitments.push_back(std::move(cm));
     }
 }
 
+void KzgPcs::commit(std::vector<std::pair<Domain, DeviceMatrix>> evaluations,
+                    std::vector<std::vector<eon_g1_affine>>& commitments, std::vector<MatrixProverData>& data) {
+    const size_t first = data.size();
+    commit_coeffs(std::move(evaluations), data);
+    commit_columns(data, first, commitments);
+}
+
 DeviceMatrix KzgPcs::get_evaluations_on_domain(const std::vector<MatrixProverData>& data, size_t idx,
-                                               const Domain& domain) {
+                                               const Domain& domain, bool aux) {
+    eon_ctx* ctx = aux && aux_ ? aux_ : ctx_;
     const MatrixProverData& m = data.at(idx);
     if (m.domain == domain) return DeviceMatrix::borrow(m.evals.data(), m.evals.height, m.evals.width);
     if (domain.log_size < m.domain.log_size)
@@ -130,10 +230,11 @@ DeviceMatrix KzgPcs::get_evaluations_on_domain(const std::vector<MatrixProverDat
     const uint32_t added = domain.log_size - m.domain.log_size;
     DeviceMatrix out = DeviceMatrix::alloc(m.coeffs.height << added, m.coeffs.width);
     const eon_fr s = domain.shift.abi();
-    check(ctx_,
-          eon_coset_dft_padded_batch_dev(ctx_, m.coeffs.data(), out.mutable_data(), m.coeffs.height, m.coeffs.width,
+    check(ctx,
+          eon_coset_dft_padded_batch_dev(ctx, m.coeffs.data(), out.mutable_data(), m.coeffs.height, m.coeffs.width,
                                          added, &s, EON_ORDER_NATURAL),
           "get_evaluations_on_domain");
+    if (ctx != ctx_) check(ctx, eon_ctx_synchronize(ctx), "get_evaluations_on_domain");
     return out;
 }
 
@@ -159,6 +260,92 @@ void KzgPcs::commit_quotient(const Domain& quotient_domain, const DeviceMatrix& 
 }
 
 std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
+    for (const OpenRound& r : rounds)
+        for (const MatrixProverData& m : *r.data)
+            if (!m.prepared) return open_quotients(rounds);
+    // opening bases per (height, point), shared by every matrix opened there (the trace and the
+    // quotient chunks at zeta)
+    std::map<std::pair<uint64_t, std::array<uint64_t, 4>>, eon_msm_bases*> bases_at;
+    struct BasesGuard {
+        std::map<std::pair<uint64_t, std::array<uint64_t, 4>>, eon_msm_bases*>& m;
+        ~BasesGuard() {
+            for (auto& kv : m)
+                if (kv.second) eon_msm_bases_destroy(kv.second);
+        }
+    } guard{bases_at};
+    auto key_of = [](uint64_t n, const Fr& z) {
+        const eon_fr za = z.abi();
+        return std::make_pair(n, std::array<uint64_t, 4>{za.l[0], za.l[1], za.l[2], za.l[3]});
+    };
+    // every distinct (height, point) up front, each height's points in one call (their
+    // constructions overlap on the device)
+    {
+        std::map<uint64_t, std::vector<eon_fr>> todo;
+        for (const OpenRound& r : rounds) {
+            if (r.data->size() != r.points.size()) throw Error(EON_E_SHAPE, "one point list per matrix");
+            for (size_t m = 0; m < r.data->size(); m++)
+                for (const Fr& z : r.points[m]) {
+                    const uint64_t n = (*r.data)[m].coeffs.height;
+                    const auto key = key_of(n, z);
+                    if (bases_at.count(key)) continue;
+                    bases_at.emplace(key, nullptr);
+                    todo[n].push_back(z.abi());
+                }
+        }
+        for (auto& [n, zs] : todo) {
+            std::vector<eon_msm_bases*> made(zs.size(), nullptr);
+            check(ctx_, eon_kzg_opening_bases_create_many(ctx_, bases_, n, zs.data(), (uint32_t)zs.size(), made.data()),
+                  "opening bases");
+            for (size_t t = 0; t < zs.size(); t++)
+                bases_at[std::make_pair(n, std::array<uint64_t, 4>{zs[t].l[0], zs[t].l[1], zs[t].l[2], zs[t].l[3]})] =
+                    made[t];
+        }
+    }
+    auto opening_bases = [&](uint64_t n, const Fr& z) { return bases_at.at(key_of(n, z)); };
+    hipStream_t st = static_cast<hipStream_t>(eon_ctx_stream(ctx_));
+    std::vector<Opened> out(rounds.size());
+    for (size_t r = 0; r < rounds.size(); r++) {
+        const auto& data = *rounds[r].data;
+        if (data.size() != rounds[r].points.size()) throw Error(EON_E_SHAPE, "one point list per matrix");
+        out[r].values.resize(data.size());
+        out[r].witnesses.resize(data.size());
+        for (size_t m = 0; m < data.size(); m++) {
+            const MatrixProverData& md = data[m];
+            const std::vector<Fr>& pts = rounds[r].points[m];
+            const uint64_t n = md.coeffs.height;
+            const uint32_t w = md.coeffs.width;
+            out[r].values[m].resize(pts.size());
+            out[r].witnesses[m].resize(pts.size());
+            // f(z) of every column (the remainder of quotient_and_eval, util.rs:100-111)
+            DeviceBuffer vals(std::max<uint64_t>(pts.size() * w, 1) * sizeof(eon_fr));
+            std::vector<const eon_msm_bases*> hb;
+            for (size_t p = 0; p < pts.size(); p++) {
+                const eon_fr z = pts[p].abi();
+                check(ctx_,
+                      eon_quotient_and_eval_columns_dev(ctx_, md.coeffs.data(), n, w, &z, nullptr,
+                                                        vals.as<eon_fr>() + p * w),
+                      "opened values");
+                hb.push_back(opening_bases(n, pts[p]));
+            }
+            std::vector<eon_fr> hv(pts.size() * w);
+            hip_check(hipMemcpyAsync(hv.data(), vals.get(), hv.size() * sizeof(eon_fr), hipMemcpyDeviceToHost, st),
+                      "opened values");
+            hip_check(hipStreamSynchronize(st), "opened values");
+            // every point's witnesses of every column in one run over the prepared digits
+            std::vector<eon_g1_affine> wits(pts.size() * w);
+            check(ctx_,
+                  eon_msm_g1_columns_prepared(ctx_, hb.data(), (uint32_t)hb.size(), md.prepared.get(), wits.data()),
+                  "witnesses");
+            for (size_t p = 0; p < pts.size(); p++) {
+                out[r].values[m][p].assign(hv.begin() + p * w, hv.begin() + (p + 1) * w);
+                out[r].witnesses[m][p].assign(wits.begin() + p * w, wits.begin() + (p + 1) * w);
+            }
+        }
+    }
+    return out;
+}
+
+std::vector<Opened> KzgPcs::open_quotients(const std::vector<OpenRound>& rounds) {
     struct Job {
         size_t round, matrix, point;
         uint64_t n;

@@ -4,6 +4,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -74,11 +75,18 @@ struct Domain {
     bool operator==(const Domain& o) const { return shift == o.shift && log_size == o.log_size; }
 };
 
-// kzg/src/pcs.rs:46-63: the committed evaluations and their coefficients
+struct PreparedDeleter {
+    void operator()(eon_msm_scalars* s) const { eon_msm_scalars_destroy(s); }
+};
+using PreparedScalars = std::unique_ptr<eon_msm_scalars, PreparedDeleter>;
+
+// kzg/src/pcs.rs:46-63: the committed evaluations and their coefficients, plus the coefficients'
+// sorted MSM digits (kept from the commitment for the opening witnesses)
 struct MatrixProverData {
     Domain domain;
     DeviceMatrix evals;
     DeviceMatrix coeffs;
+    PreparedScalars prepared;
 };
 
 // one round's opened values / witnesses: [matrix][point][column]
@@ -106,20 +114,36 @@ class KzgPcs {
     // pcs.rs:223-265: coset_idft_batch of each matrix, one commitment per column
     void commit(std::vector<std::pair<Domain, DeviceMatrix>> evaluations,
                 std::vector<std::vector<eon_g1_affine>>& commitments, std::vector<MatrixProverData>& data);
-    // pcs.rs:267-287 (values of the reference's Horner loop, from one padded coset DFT)
+    // commit in two halves: the coefficients of every matrix (pcs.rs:242, appended to data), then
+    // the column commitments of data[first..] (pcs.rs:244-251) -- so that work which needs only
+    // the coefficients (the trace LDE) can run on the auxiliary context meanwhile
+    void commit_coeffs(std::vector<std::pair<Domain, DeviceMatrix>> evaluations, std::vector<MatrixProverData>& data);
+    void commit_columns(std::vector<MatrixProverData>& data, size_t first,
+                        std::vector<std::vector<eon_g1_affine>>& commitments);
+    // pcs.rs:267-287 (values of the reference's Horner loop, from one padded coset DFT); aux:
+    // on the auxiliary context (its own non-blocking stream; synchronised before returning)
     DeviceMatrix get_evaluations_on_domain(const std::vector<MatrixProverData>& data, size_t idx,
-                                           const Domain& domain);
+                                           const Domain& domain, bool aux = false);
+    // a second context on the same device for work concurrent with this one's (null if none)
+    eon_ctx* aux_ctx() const { return aux_; }
     // commit/src/pcs.rs:82-101 with split_evals (domain.rs:188-221)
     void commit_quotient(const Domain& quotient_domain, const DeviceMatrix& quotient_evals, uint32_t num_chunks,
                          std::vector<std::vector<eon_g1_affine>>& commitments, std::vector<MatrixProverData>& data);
-    // pcs.rs:289-335: per (matrix, point) every column's value and witness; the quotients of one
-    // height are committed by one batched column MSM
+    // pcs.rs:289-335: per (matrix, point) every column's value and witness.  The witness of
+    // column c at z is the MSM of c's own coefficients against the opening bases H(z)
+    // (eon_kzg_opening_bases_create), reusing the digits sorted at commit time; without prepared
+    // digits (EON_KZG_OPEN=quotient) the synthetic-division quotients of one height are committed
+    // by one batched column MSM instead.
     std::vector<Opened> open(const std::vector<OpenRound>& rounds);
 
   private:
+    std::vector<Opened> open_quotients(const std::vector<OpenRound>& rounds);
+    bool keep_digits_ = true;
     eon_ctx* ctx_;
     uint64_t max_degree_;
     eon_msm_bases* bases_ = nullptr;
+    eon_ctx* aux_ = nullptr;
+    void* aux_stream_ = nullptr;
 };
 
 }  // namespace eon_host

@@ -14,7 +14,10 @@
 #include <hip/hip_runtime_api.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <thread>
 
 namespace eon_host {
 
@@ -74,23 +77,58 @@ Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t hei
     auto t0 = tick();
     std::vector<std::vector<eon_g1_affine>> trace_commit;
     std::vector<MatrixProverData> trace_data;
+    const Domain quotient_domain = trace_domain.create_disjoint_domain(1ull << (log_n + log_qd));
+    const uint64_t q_rows = quotient_domain.size();
+    // The trace LDE (prover.rs:315) needs only the committed coefficients, not alpha: it runs on
+    // the PCS's auxiliary context while the column MSMs of the commitment (prover.rs:186-187)
+    // run on the main one, and filling the MSM's memory- and latency-bound phases (digit sorts,
+    // bucket reductions) with NTT passes.  Opt-in (EON_PROVE_OVERLAP=1): measured equal to the
+    // reference's order so far -- the NTT saturates the VALUs the piece sums need.
+    static const bool overlap = [] {
+        const char* e = getenv("EON_PROVE_OVERLAP");
+        return e && e[0] == '1';
+    }();
+    DeviceMatrix lde;
+    clock::time_point t1, t2;
     {
         std::vector<std::pair<Domain, DeviceMatrix>> ev;
         ev.emplace_back(trace_domain, DeviceMatrix::borrow(trace, height, width));
-        pcs.commit(std::move(ev), trace_commit, trace_data);  // prover.rs:186-187
+        pcs.commit_coeffs(std::move(ev), trace_data);
     }
-    auto t1 = tick();
-    const Domain quotient_domain = trace_domain.create_disjoint_domain(1ull << (log_n + log_qd));
-    const uint64_t q_rows = quotient_domain.size();
+    if (overlap && pcs.aux_ctx()) {
+        std::exception_ptr lde_err;
+        const int dev = eon_ctx_device(ctx);
+        std::thread lde_thread([&] {
+            try {
+                hip_ok(hipSetDevice(dev), "hipSetDevice");
+                lde = pcs.get_evaluations_on_domain(trace_data, 0, quotient_domain, true);
+            } catch (...) {
+                lde_err = std::current_exception();
+            }
+        });
+        try {
+            pcs.commit_columns(trace_data, 0, trace_commit);
+        } catch (...) {
+            lde_thread.join();
+            throw;
+        }
+        t1 = tick();
+        lde_thread.join();
+        if (lde_err) std::rethrow_exception(lde_err);
+    } else {
+        pcs.commit_columns(trace_data, 0, trace_commit);
+        t1 = tick();
+        lde = pcs.get_evaluations_on_domain(trace_data, 0, quotient_domain);
+    }
     DeviceMatrix qv = DeviceMatrix::alloc(q_rows, 1);
-    clock::time_point t2;
     {
-        DeviceMatrix lde = pcs.get_evaluations_on_domain(trace_data, 0, quotient_domain);  // prover.rs:315
         t2 = tick();
         const eon_fr a = alpha.abi();
         check(ctx, eon_p2air_quotient_values_dev(ctx, air, lde.data(), log_n, log_qd, &a, qv.mutable_data()),
               "quotient_values");
     }
+    check(ctx, eon_ctx_synchronize(ctx), "quotient_values");
+    lde = DeviceMatrix();  // back to the buffer cache before the opening
     auto t3 = tick();
     if (shard) {
         DeviceBuffer parts(sizeof(eon_fr) * q_rows * world);

@@ -11,8 +11,12 @@ Reference: ``KzgPcs`` (kzg/src/pcs.rs:143-402) implementing ``Pcs<Fr, Challenger
                                     DFT of the zero-padded coefficients.
 * ``commit_quotient``            -- commit/src/pcs.rs:82-101: split_evals / split_domains
                                     (domain.rs:174-221), then commit.
-* ``open``                       -- pcs.rs:289-335: per (matrix, point) the synthetic-division
-                                    quotients of every column and their commitments.
+* ``open``                       -- pcs.rs:289-335: per (matrix, point) every column's value and
+                                    the commitment of its synthetic-division quotient, computed as
+                                    the MSM of the column's own coefficients against the opening
+                                    bases H(z) (eon_kzg_opening_bases_create) over the digits
+                                    sorted at commit time.  EON_KZG_OPEN=quotient keeps the
+                                    reference's route (quotients, then their commitments).
 
 Commitments / witnesses are (width, 8) u64 arrays of affine G1 points (x, y Fq Montgomery).
 """
@@ -20,6 +24,7 @@ Commitments / witnesses are (width, 8) u64 arrays of affine G1 points (x, y Fq M
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -77,6 +82,7 @@ class MatrixProverData:
     domain: Domain
     evals: object
     coeffs: object
+    prepared: object = None  # msm.PreparedScalars of coeffs (the commitment's sorted digits)
 
 
 @dataclass
@@ -93,6 +99,7 @@ class GpuKzgPcs:
         self.max_degree = max_degree
         self.bases = MsmBases(srs_powers(max_degree + 1, alpha, self.ctx), self.ctx, precompute=True)
         self.dft = Radix2Dit(self.ctx)
+        self.keep_digits = os.environ.get("EON_KZG_OPEN") != "quotient"
 
     # -- Pcs surface -----------------------------------------------------------------------------
     def natural_domain_for_degree(self, degree: int) -> Domain:
@@ -111,8 +118,13 @@ class GpuKzgPcs:
                 raise _lib.EonError(_lib.EON_E_SHAPE, "evaluation height must match domain size")
             self.ensure_supported(max(h - 1, 0))
             coeffs = self.dft.coset_idft_batch(evals, domain.shift)
-            commitments.append(self.bases.msm_columns(coeffs))
-            data.append(MatrixProverData(domain, evals, coeffs))
+            prepared = None
+            if self.keep_digits:
+                cm, prepared = self.bases.prepare_columns(coeffs)
+            else:
+                cm = self.bases.msm_columns(coeffs)
+            commitments.append(cm)
+            data.append(MatrixProverData(domain, evals, coeffs, prepared))
         return commitments, data
 
     def get_evaluations_on_domain(self, prover_data, idx: int, domain: Domain):
@@ -134,8 +146,54 @@ class GpuKzgPcs:
     def open(self, rounds):
         """rounds: [(prover_data, points_per_matrix)] -> (opened values, witnesses) per round.
 
-        pcs.rs:289-335 computes, per (matrix, point), every column's synthetic-division quotient
-        and commits each one.  All quotients of one height share the SRS prefix, so they are
+        pcs.rs:289-335 commits, per (matrix, point z, column c), the quotient of c by (X - z).
+        That commitment equals sum_j c_j H_j(z) with H_j(z) = sum_{i<j} z^(j-1-i) G_i, so every
+        point's witnesses are one run over the digits sorted when the matrix was committed."""
+        import torch
+
+        for prover_data, _ in rounds:
+            if any(m.prepared is None for m in prover_data):
+                return self.open_quotients(rounds)
+        bases_at = {}  # (height, point) -> opening bases, shared across matrices
+        todo = {}
+        for prover_data, points_per_matrix in rounds:
+            for m, points in zip(prover_data, points_per_matrix):
+                n = int(m.coeffs.shape[0])
+                for z in points:
+                    if (n, z) not in bases_at and z not in todo.setdefault(n, []):
+                        todo[n].append(z)
+        for n, zs in todo.items():  # each height's points in one call
+            for z, b in zip(zs, self.bases.opening_bases_many(n, zs)):
+                bases_at[(n, z)] = b
+        out = []
+        for prover_data, points_per_matrix in rounds:
+            if len(prover_data) != len(points_per_matrix):
+                raise _lib.EonError(_lib.EON_E_SHAPE, "one point list per matrix")
+            o = Opened(values=[[None] * len(p) for p in points_per_matrix],
+                       witnesses=[[None] * len(p) for p in points_per_matrix])
+            for mi, (m, points) in enumerate(zip(prover_data, points_per_matrix)):
+                n, w = int(m.coeffs.shape[0]), int(m.coeffs.shape[1])
+                hb = []
+                for pi, z in enumerate(points):
+                    v = torch.empty((w, 4), dtype=torch.int64, device=m.coeffs.device)
+                    pz = fr_to_abi(z)
+                    self.ctx.set_stream(torch.cuda.current_stream(m.coeffs.device).cuda_stream)
+                    self.ctx.check(self.ctx.lib.eon_quotient_and_eval_columns_dev(
+                        self.ctx.handle, ctypes.c_void_p(m.coeffs.data_ptr()), n, w, ctypes.byref(pz), None,
+                        ctypes.c_void_p(v.data_ptr())))
+                    o.values[mi][pi] = v.cpu().numpy().view(np.uint64)
+                    hb.append(bases_at[(n, z)])
+                wits = m.prepared.msm(hb)
+                for pi in range(len(points)):
+                    o.witnesses[mi][pi] = wits[pi]
+            out.append(o)
+        for b in bases_at.values():
+            b.close()
+        return out
+
+    def open_quotients(self, rounds):
+        """open by the reference's route: pcs.rs:289-335 computes, per (matrix, point), every
+        column's synthetic-division quotient and commits each one.  All quotients of one height share the SRS prefix, so they are
         gathered into one matrix and committed by ONE batched column MSM (one pipeline fill and
         drain instead of one per (matrix, point))."""
         import torch

@@ -1,0 +1,62 @@
+"""GPU parity of the KZG opening as an MSM of the committed coefficients against opening bases
+(eon_msm_g1_columns_prepare_dev / eon_msm_g1_columns_prepared / eon_kzg_opening_bases_create)
+against the oracle's route, the reference's: quotient_and_eval per column
+(kzg/src/util.rs:100-111) then commit_column of the quotient over the SRS (kzg/src/util.rs:37-40,
+kzg/src/pcs.rs:305-316), with the C Pippenger restatement as the MSM."""
+
+import numpy as np
+import pytest
+
+from oracle import coracle as C
+from plonky3_eon_amd import EonError
+from plonky3_eon_amd.msm import MsmBases, srs_powers
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to("cuda:0")
+
+
+@pytest.mark.parametrize("log_n,width", [(1, 2), (4, 3), (10, 5)])
+def test_opening_witnesses_match_synthetic_division(gpu_ctx, log_n, width):
+    n = 1 << log_n
+    pts = srs_powers(n + 1, 12345, gpu_ctx)  # max_degree n, as KzgPcs's SRS
+    srs = MsmBases(pts, gpu_ctx, precompute=True)
+    coeffs = C.random_fr(31 + log_n, n * width).reshape(n, width, 4)
+    cm, prep = srs.prepare_columns(_dev(coeffs))
+    np.testing.assert_array_equal(cm, srs.msm_columns(coeffs))
+    points = [C.fr_from_u64(0), C.fr_from_u64(1), C.random_fr(77, 1)[0], C.random_fr(78, 1)[0]]
+    # four points at once: z = 0 and z != 0 mixed, over the three construction streams
+    hs = srs.opening_bases_many(n, points)
+    got = prep.msm([srs] + hs)
+    np.testing.assert_array_equal(got[0], cm)  # the prepared digits reproduce the commitments
+    for t, z in enumerate(points):
+        for j in range(width):
+            q, _ = C.quotient_and_eval(coeffs[:, j], z)
+            want = C.g1_msm(pts[: n - 1], q) if n > 1 else np.zeros(8, np.uint64)
+            np.testing.assert_array_equal(got[t + 1, j], want, err_msg=f"point {t} column {j}")
+    prep.close()
+    for h in hs:
+        h.close()
+
+
+def test_opening_bases_edge_cases(gpu_ctx):
+    n = 16
+    pts = srs_powers(n, 7, gpu_ctx)
+    srs = MsmBases(pts, gpu_ctx, precompute=True)
+    # n - 1 SRS points are enough; n + 1 would need n
+    srs.opening_bases(n + 1, C.fr_from_u64(3)).close()
+    with pytest.raises(EonError):
+        srs.opening_bases(n + 2, C.fr_from_u64(3))
+    # a single-row column has an empty quotient: the witness is the identity
+    c1 = C.random_fr(5, 2).reshape(1, 2, 4)
+    _, prep = srs.prepare_columns(_dev(c1), want_commitments=False)
+    h = srs.opening_bases(1, C.fr_from_u64(9))
+    np.testing.assert_array_equal(prep.msm([h]), np.zeros((1, 2, 8), np.uint64))
+    # bases of another window layout are refused
+    plain = MsmBases(pts, gpu_ctx, precompute=False)
+    with pytest.raises(EonError):
+        prep.msm([plain])

@@ -152,3 +152,39 @@ def test_msm_columns_batched_kzg_identity(gpu_ctx):
     for j in list(range(0, width, 13)) + [width - 1]:
         f_alpha = C.eval_poly_col(mat, j, alpha)
         np.testing.assert_array_equal(got[j], C.g1_mul(g, f_alpha), err_msg=f"column {j}")
+
+
+def test_columns_fused_reduce_edge_cases(gpu_ctx):
+    """>= 64 columns of fixed-base MSMs take the fused radix-2^29 bucket reduction
+    (k_bucket_reduce29): equal piece partials (doubling) and opposite ones (identity) inside one
+    bucket, zero and small-scalar columns, against the Python double-and-add oracle."""
+    g = O.G1_GEN
+    P = O.g1_mul(g, 1234567)
+    rows, width = 300, 66
+    pts = np.stack([pt(P)] * 150 + [pt(O.g1_neg(P))] * 150)
+    bases = MsmBases(pts, gpu_ctx, precompute=True)
+    rng = O.SplitMix64(5)
+    cols, want = [], []
+    for j in range(width):
+        if j == 0:
+            s = [0] * rows
+        elif j % 3 == 1:  # equal scalars: every bucket holds equal pieces of one sign
+            v = O.from_mont(rng.fr_mont())
+            s = [v] * rows
+        elif j % 3 == 2:  # small scalars
+            s = [rng.next() % 1000 for _ in range(rows)]
+        else:
+            s = [O.from_mont(rng.fr_mont()) for _ in range(rows)]
+        cols.append(s)
+        k = (sum(s[:150]) - sum(s[150:])) % O.P
+        want.append(O.g1_mul(P, k) if k else O.INF)
+    mat = np.stack([np.stack([fr(cols[j][i]) for j in range(width)]) for i in range(rows)])
+    got = bases.msm_columns(mat)
+    for j in range(width):
+        assert as_py(got[j]) == want[j], j
+    # the same with all bases equal: pieces of one bucket are equal (the doubling case)
+    bases2 = MsmBases(np.stack([pt(P)] * rows), gpu_ctx, precompute=True)
+    got2 = bases2.msm_columns(mat)
+    for j in range(width):
+        k = sum(cols[j]) % O.P
+        assert as_py(got2[j]) == (O.g1_mul(P, k) if k else O.INF), j

@@ -24,7 +24,10 @@ def consts():
                          [[lim(x) for x in r] for r in py[2]])
 
 
-def test_open_kernel_vs_oracle(gpu_ctx):
+@pytest.mark.parametrize("prepared", [False, True])
+def test_open_kernel_vs_oracle(gpu_ctx, prepared):
+    """KzgPcs::open both ways: the reference's quotients (prepared digits absent) and the MSM of
+    the committed coefficients against the opening bases."""
     import torch
 
     from plonky3_eon_amd.kzg import GpuKzgPcs, MatrixProverData, Domain
@@ -33,7 +36,8 @@ def test_open_kernel_vs_oracle(gpu_ctx):
     for rows, w in [(1, 2), (2, 3), (257, 5), (600, 3)]:
         cf = C.random_fr(rows + w, rows * w).reshape(rows, w, 4)
         dev = torch.from_numpy(cf.view(np.int64)).to("cuda:0")
-        data = [MatrixProverData(Domain(1, 0), None, dev)]
+        prep = pcs.bases.prepare_columns(dev, want_commitments=False)[1] if prepared else None
+        data = [MatrixProverData(Domain(1, 0), None, dev, prep)]
         z = 0xABCDEF123456789
         r = pcs.open([(data, [[z, 0]])])[0]
         for pi, pt in enumerate((z, 0)):
@@ -73,6 +77,34 @@ def test_prove_vs_oracle(gpu_ctx, consts, log_n, vl):
     for c in range(2):
         np.testing.assert_array_equal(qo.values[c][0], want["quotient_open"][c][0][0])
         np.testing.assert_array_equal(qo.witnesses[c][0], want["quotient_open"][c][1][0])
+
+
+def test_open_routes_agree_full_height(gpu_ctx, consts):
+    """At the headline height (2^17 rows, VECTOR_LEN 1: 164 columns, two MSM batches) the prove
+    through the opening bases equals the prove through the reference's per-column quotients --
+    the oracle cannot run this size, the two GPU routes check each other."""
+    import torch
+
+    from plonky3_eon_amd.air import Poseidon2Air
+    from plonky3_eon_amd.kzg import GpuKzgPcs
+    from plonky3_eon_amd.prover import prove
+
+    log_n, vl = 17, 1
+    n = 1 << log_n
+    pcs = GpuKzgPcs(n, 12345, gpu_ctx)
+    air = Poseidon2Air(consts.begin, consts.partial, consts.end, vl, gpu_ctx)
+    inputs = C.random_fr(91, n * vl * 3).reshape(n * vl, 3, 4)
+    trace = air.generate_trace(torch.from_numpy(inputs.view(np.int64)).to("cuda:0"))
+    alpha, zeta = 0x1234567890ABCDEF1234, 0xFEDCBA0987654321
+    a = prove(air, pcs, trace, alpha, zeta)
+    pcs.keep_digits = False
+    b = prove(air, pcs, trace, alpha, zeta)
+    np.testing.assert_array_equal(a.trace_commit[0], b.trace_commit[0])
+    for r in range(2):
+        for m in range(len(a.opened[r].values)):
+            for p in range(len(a.opened[r].values[m])):
+                np.testing.assert_array_equal(a.opened[r].values[m][p], b.opened[r].values[m][p])
+                np.testing.assert_array_equal(a.opened[r].witnesses[m][p], b.opened[r].witnesses[m][p])
 
 
 @pytest.mark.parametrize("log_n,vl", [(3, 1), (5, 8)])

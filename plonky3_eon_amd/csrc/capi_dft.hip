@@ -304,7 +304,8 @@ int eon_ctx_create(int device_ordinal, eon_ctx** out) {
         ok = ok && hipStreamCreateWithPriority(&c->msm_sort, hipStreamNonBlocking, prio_greatest) == hipSuccess;
     }
     for (hipEvent_t* e : {&c->msm_ev[0], &c->msm_ev[1], &c->msm_ev[2], &c->msm_sorted[0], &c->msm_sorted[1],
-                          &c->msm_sorted[2], &c->msm_reduced[0], &c->msm_reduced[1], &c->msm_reduced[2]})
+                          &c->msm_sorted[2], &c->msm_reduced[0], &c->msm_reduced[1], &c->msm_reduced[2],
+                          &c->msm_pdone[0], &c->msm_pdone[1], &c->msm_pdone[2], &c->msm_pdone[3]})
         ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         (void)hipStreamDestroy(c->own_stream);
@@ -339,6 +340,7 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     ctx->msm.release();
     ctx->msm_b.release();
     ctx->msm_c.release();
+    ctx->msm_d.release();
     for (auto& sb : ctx->sorted_cache) sb.release();
     ctx->sorted_cache.clear();
     ctx->sel_tab.release();
@@ -353,7 +355,8 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     for (hipStream_t st : ctx->msm_comp)
         if (st) (void)hipStreamDestroy(st);
     for (hipEvent_t e : {ctx->msm_ev[0], ctx->msm_ev[1], ctx->msm_ev[2], ctx->msm_sorted[0], ctx->msm_sorted[1],
-                         ctx->msm_sorted[2], ctx->msm_reduced[0], ctx->msm_reduced[1], ctx->msm_reduced[2]})
+                         ctx->msm_sorted[2], ctx->msm_reduced[0], ctx->msm_reduced[1], ctx->msm_reduced[2],
+                         ctx->msm_pdone[0], ctx->msm_pdone[1], ctx->msm_pdone[2], ctx->msm_pdone[3]})
         (void)hipEventDestroy(e);
     delete ctx;
 }

@@ -118,7 +118,7 @@ struct eon_ctx {
 
     // MSM pipeline: workspaces msm / msm_b / msm_c for batches k % 3; piece sums + reductions on
     // `stream` / msm_side, digit sorts on the high-priority msm_sort (msm.hip: msm_run_columns)
-    eon::MsmWork msm, msm_b, msm_c;
+    eon::MsmWork msm, msm_b, msm_c, msm_d;
     hipStream_t msm_side = nullptr, msm_sort = nullptr;
     // third compute stream of the prepared path (jobs round-robin over stream / msm_side / msm_side2)
     hipStream_t msm_side2 = nullptr;
@@ -131,6 +131,8 @@ struct eon_ctx {
     hipStream_t msm_comp[2] = {nullptr, nullptr};
     hipEvent_t msm_ev[3] = {nullptr, nullptr, nullptr};
     hipEvent_t msm_sorted[3] = {nullptr, nullptr, nullptr}, msm_reduced[3] = {nullptr, nullptr, nullptr};
+    // prepared path: "piece sums of job j done" (jobs chained through them, round-robin)
+    hipEvent_t msm_pdone[4] = {nullptr, nullptr, nullptr, nullptr};
 
     // sorted-digit buffers of destroyed eon_msm_scalars, reused by the next prepared MSM (the
     // prover commits matrices of the same shape every proof: keeping ~22 GB resident beats a

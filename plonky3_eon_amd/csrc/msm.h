@@ -26,6 +26,14 @@ uint32_t bases_window(const eon_msm_bases* b);
 bool bases_precomputed(const eon_msm_bases* b);
 // release a bases object (caller holds ctx->mu and has synchronised its work)
 void bases_free(eon_msm_bases* b);
+// the window table in 29-Montgomery form (precomputed radix-2^29 bases; else null), its windows
+const G1Affine* bases_table29(const eon_msm_bases* b);
+uint32_t bases_windows(const eon_msm_bases* b);
+// fixed-base bases whose window table the caller writes (affine, radix-2^32 ABI form, entry
+// i * windows + w = 2^(c w) P_i), then seals: points <- the w = 0 entries, table -> 29-form
+Status bases_alloc_table(eon_ctx* ctx, uint64_t n, uint32_t c, eon_msm_bases** out);
+G1Affine* bases_table_mut(eon_msm_bases* b);
+Status bases_seal_table(eon_msm_bases* b, hipStream_t st);
 
 constexpr uint32_t BATCH = 32;  // points per thread in batched XYZZ -> affine conversion
 hipError_t launch_batch_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out, hipStream_t st);

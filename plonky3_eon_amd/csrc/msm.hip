@@ -958,6 +958,44 @@ namespace eon {
 
 const G1Affine* bases_points(const eon_msm_bases* b) { return b->points.as<G1Affine>(); }
 
+const G1Affine* bases_table29(const eon_msm_bases* b) {
+    return b->precomputed && b->r29 ? b->table.as<G1Affine>() : nullptr;
+}
+
+uint32_t bases_windows(const eon_msm_bases* b) { return b->windows; }
+
+Status bases_alloc_table(eon_ctx* ctx, uint64_t n, uint32_t c, eon_msm_bases** out) {
+    if (n == 0 || n > (1ull << 27)) return Status::err(EON_E_SHAPE, "table bases need 1 <= n <= 2^27");
+    auto* b = new eon_msm_bases();
+    b->ctx = ctx;
+    b->n = n;
+    b->precomputed = true;
+    b->c = c;
+    b->windows = (255 + c - 1) / c;
+    b->r29 = getenv("EON_MSM_R32") == nullptr;
+    if (b->points.ensure(n * sizeof(G1Affine)) != hipSuccess ||
+        b->table.ensure(n * b->windows * sizeof(G1Affine)) != hipSuccess) {
+        bases_free(b);
+        return Status::err(EON_E_OOM, "bases allocation failed");
+    }
+    *out = b;
+    return Status::ok();
+}
+
+G1Affine* bases_table_mut(eon_msm_bases* b) { return b->table.as<G1Affine>(); }
+
+Status bases_seal_table(eon_msm_bases* b, hipStream_t st) {
+    // points = the w = 0 entries (radix-2^32 ABI form), then the table to 29-Montgomery
+    EON_HIP(hipMemcpy2DAsync(b->points.p, sizeof(G1Affine), b->table.p, sizeof(G1Affine) * b->windows,
+                             sizeof(G1Affine), b->n, hipMemcpyDeviceToDevice, st));
+    if (b->r29) {
+        const uint64_t m = b->n * b->windows;
+        hipLaunchKernelGGL(k_table_to29, dim3(blocks_for(m, 256)), dim3(256), 0, st, b->table.as<G1Affine>(), m);
+        EON_HIP(hipGetLastError());
+    }
+    return Status::ok();
+}
+
 void bases_free(eon_msm_bases* b) {
     b->points.release();
     b->table.release();
@@ -995,6 +1033,27 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
     if (width == 0) return Status::ok();
     if (n == 0) return out_host ? identity_columns(width, out_host) : Status::ok();
     const MsmLayout L = msm_layout(b, n, width);
+    // EON_MSM_SORT_FIRST=1 with kept digits: every batch sorted first (each sort alone on the
+    // device), then the prepared pipeline -- measured ~5 ms slower per trace commit than the
+    // streaming pipeline below, which keeps the sorted buffers as it goes.
+    static const bool sort_first = getenv("EON_MSM_SORT_FIRST") != nullptr;
+    if (keep && sort_first) {
+        keep->batches = make_batches(scalars, width, L.cpb);
+        keep->sorted.resize(keep->batches.size());
+        for (auto& sb : keep->sorted) {
+            if (ctx->sorted_cache.empty()) break;
+            sb = std::move(ctx->sorted_cache.back());
+            ctx->sorted_cache.back() = SortedBufs{};
+            ctx->sorted_cache.pop_back();
+        }
+        for (size_t k = 0; k < keep->batches.size(); k++) {
+            EON_TRY(batch_sort(ctx, L, n, width, keep->batches[k], ctx->msm, keep->sorted[k], ctx->stream));
+            keep->batches[k].scalars = nullptr;
+        }
+        std::vector<G1Affine> tmp(out_host ? 0 : width);
+        const eon_msm_bases* bl[1] = {b};
+        return msm_run_prepared(ctx, bl, 1, keep, out_host ? out_host : tmp.data());
+    }
     // every batch leaves XYZZ results; one batched XYZZ -> affine conversion at the end (the
     // conversion is an inversion-latency-bound launch, so it is paid once per call)
     EON_HIP(ctx->msm.results.ensure(width * (sizeof(G1Affine) + sizeof(G1Xyzz))));
@@ -1086,28 +1145,40 @@ Status msm_run_prepared(eon_ctx* ctx, const eon_msm_bases* const* bases, uint32_
     EON_HIP(ctx->msm.results.ensure(total * (sizeof(G1Affine) + sizeof(G1Xyzz))));
     G1Affine* res = ctx->msm.results.as<G1Affine>();
     G1Xyzz* res_xyzz = reinterpret_cast<G1Xyzz*>(res + total);
-    // jobs (batch k, bases t) round-robin over three streams and three workspaces, enqueued
-    // without a host wait (the reductions have no read-backs): a piece-sum launch is always
-    // queued, and each job's latency-bound reduction runs in the slots the others leave.  A
-    // workspace is reused only by its own stream, three jobs later.
-    hipStream_t comp[3] = {ctx->stream, ctx->msm_side, ctx->msm_side2};
-    MsmWork* wks[3] = {&ctx->msm, &ctx->msm_b, &ctx->msm_c};
+    // Jobs (batch k, bases t) round-robin over NS streams and workspaces (NS = 3, or
+    // EON_MSM_PREP_STREAMS = 2..4), enqueued without a host wait (the reductions have no
+    // read-backs); a workspace is reused only by its own stream, NS jobs later.
+    // EON_MSM_PIECE_CHAIN=1 chains the piece sums (job j's start when job j-1's end, so each
+    // reduction runs beside the next job's piece sums): measured equal to unchained.
+    static const uint32_t NS = [] {
+        const char* e = getenv("EON_MSM_PREP_STREAMS");
+        const int v = e ? atoi(e) : 3;
+        return (uint32_t)(v < 2 ? 2 : (v > 4 ? 4 : v));
+    }();
+    static const bool chain = [] {
+        const char* e = getenv("EON_MSM_PIECE_CHAIN");
+        return e && e[0] == '1';
+    }();
+    hipStream_t comp[4] = {ctx->stream, ctx->msm_side, ctx->msm_side2, ctx->msm_sort};
+    MsmWork* wks[4] = {&ctx->msm, &ctx->msm_b, &ctx->msm_c, &ctx->msm_d};
     EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));
-    EON_HIP(hipStreamWaitEvent(ctx->msm_side, ctx->msm_ev[0], 0));
-    EON_HIP(hipStreamWaitEvent(ctx->msm_side2, ctx->msm_ev[0], 0));
+    for (uint32_t i = 1; i < NS; i++) EON_HIP(hipStreamWaitEvent(comp[i], ctx->msm_ev[0], 0));
     for (size_t k = 0; k < s->batches.size(); k++)
         for (uint32_t t = 0; t < nbases; t++) {
             const size_t j = k * nbases + t;
+            hipStream_t st = comp[j % NS];
             Batch bt = s->batches[k];
             bt.out = res_xyzz + (uint64_t)t * width + bt.col0;
             const SortedRef sr = sorted_ref(s->sorted[k]);
-            EON_TRY(batch_pieces(ctx, bases[t], bt, sr, *wks[j % 3], comp[j % 3]));
-            EON_TRY(batch_reduce(ctx, s->layout, bt, sr, *wks[j % 3], comp[j % 3], fused_reduce(bases[t], bt)));
+            if (chain && j > 0) EON_HIP(hipStreamWaitEvent(st, ctx->msm_pdone[(j - 1) % 4], 0));
+            EON_TRY(batch_pieces(ctx, bases[t], bt, sr, *wks[j % NS], st));
+            if (chain) EON_HIP(hipEventRecord(ctx->msm_pdone[j % 4], st));
+            EON_TRY(batch_reduce(ctx, s->layout, bt, sr, *wks[j % NS], st, fused_reduce(bases[t], bt)));
         }
-    EON_HIP(hipEventRecord(ctx->msm_ev[1], ctx->msm_side));
-    EON_HIP(hipEventRecord(ctx->msm_ev[2], ctx->msm_side2));
-    EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[1], 0));
-    EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[2], 0));
+    for (uint32_t i = 1; i < NS; i++) {
+        EON_HIP(hipEventRecord(ctx->msm_ev[1], comp[i]));
+        EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[1], 0));
+    }
     EON_HIP(launch_batch_to_affine(res_xyzz, total, res, ctx->stream));
     EON_HIP(hipMemcpyAsync(out_host, res, total * sizeof(G1Affine), hipMemcpyDeviceToHost, ctx->stream));
     EON_HIP(hipStreamSynchronize(ctx->stream));

@@ -12,6 +12,7 @@
 // two additions of the scan, then the fixed-base window table of the SRS layout (msm.hip).
 #include "context.h"
 #include "ec.h"
+#include "ec29.h"
 #include "msm.h"
 
 using namespace eon;
@@ -108,6 +109,139 @@ __global__ void k_open_shift(const G1Affine* g, uint64_t n, G1Affine* h) {
     st_affine(h + j, r);
 }
 
+// ---- radix-2^29 path (r29 SRS bases with the c = 16, 16-window table) --------------------------
+
+constexpr uint32_t TC = 16, TW = 16;  // table window bits and windows of the fast path
+
+__device__ __forceinline__ void ld_affine29(const G1Affine* p, bool neg_y, F29& x, F29& y) {
+    G1Affine a = ld_affine(p);
+    if (neg_y) a.y = neg(a.y);  // p - y on the integer (29-Montgomery canonical) representation
+    x = unpack29(a.x);
+    y = unpack29(a.y);
+}
+
+// acc += (x, y) (affine, canonical 29-form, not the identity) with the exceptional cases
+__device__ __forceinline__ void madd29_any(G1X29& acc, bool& inf, const F29& x, const F29& y) {
+    if (inf) {
+        acc.X = x;
+        acc.Y = y;
+        acc.ZZ = const29<FqP>(R29<FqP>::ONE);
+        acc.ZZZ = acc.ZZ;
+        inf = false;
+    } else if (!madd29(acc, x, y)) {
+        inf = madd29_exceptional(acc, x, y);
+    }
+}
+
+// P_i = z^-i G_i from the SRS window table T_(i,w) = 2^(16 w) G_i (29-form): k = z^-i made odd
+// (k + 1 when even, G_i subtracted at the end) is recoded into 16 odd signed 16-bit digits,
+// each written as 16 digits +-1, so that every bit level adds every window's entry (no lane
+// divergence): 15 doublings + 256 mixed additions, against ~254 + ~254 divergent ones for
+// double-and-add.
+__global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, uint64_t n, Fr zinv, G1Xyzz* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (i + 1 == n) {
+        st_xyzz(out + i, xyzz_inf());
+        return;
+    }
+    const G1Affine* row = tab + i * TW;
+    {
+        const G1Affine g = ld_affine(row);
+        if (is_inf(g)) {  // the identity's table row is all identity
+            st_xyzz(out + i, xyzz_inf());
+            return;
+        }
+    }
+    Fr k = to_canonical(pow_u64(zinv, i));
+    const bool even = (k.v[0] & 1) == 0;
+    if (even) k.v[0] += 1;  // no carry: k even
+    // odd recoding: d_w = (k mod 2^17) - 2^16, k <- (k - d_w) / 2^16; u_w = (d_w + 2^16 - 1) / 2
+    uint32_t u[TW];
+    uint32_t kw[9];
+#pragma unroll
+    for (int j = 0; j < 8; j++) kw[j] = k.v[j];
+    kw[8] = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < TW; w++) {
+        int32_t d;
+        if (w + 1 < TW) {
+            d = (int32_t)(kw[0] & 0x1FFFFu) - 0x10000;
+        } else {
+            d = (int32_t)kw[0];  // the rest, odd, < 2^15
+        }
+        u[w] = (uint32_t)((d + 0xFFFF) >> 1);
+        // k - d (d odd, |d| < 2^16), then >> 16 (exact)
+        uint64_t borrow_or_carry;
+        if (d >= 0) {
+            uint64_t t = (uint64_t)kw[0] - (uint32_t)d;
+            kw[0] = (uint32_t)t;
+            borrow_or_carry = (t >> 63) & 1;  // borrow
+#pragma unroll
+            for (int j = 1; j < 9; j++) {
+                t = (uint64_t)kw[j] - borrow_or_carry;
+                kw[j] = (uint32_t)t;
+                borrow_or_carry = (t >> 63) & 1;
+            }
+        } else {
+            uint64_t t = (uint64_t)kw[0] + (uint32_t)(-d);
+            kw[0] = (uint32_t)t;
+            borrow_or_carry = t >> 32;
+#pragma unroll
+            for (int j = 1; j < 9; j++) {
+                t = (uint64_t)kw[j] + borrow_or_carry;
+                kw[j] = (uint32_t)t;
+                borrow_or_carry = t >> 32;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) kw[j] = (kw[j] >> 16) | (kw[j + 1] << 16);
+        kw[8] >>= 16;
+    }
+    G1X29 acc;
+    bool inf = true;
+    F29 x, y;
+    for (int b = (int)TC - 1; b >= 0; b--) {
+        if (!inf) dbl29(acc);
+        for (uint32_t w = 0; w < TW; w++) {
+            ld_affine29(row + w, ((u[w] >> b) & 1) == 0, x, y);
+            madd29_any(acc, inf, x, y);
+        }
+    }
+    if (even) {
+        ld_affine29(row, true, x, y);
+        madd29_any(acc, inf, x, y);
+    }
+    st_xyzz(out + i, x29_to_xyzz(acc, inf));
+}
+
+// H_j = z^(j-1) S_j (double-and-add in radix 2^29; S_j affine, radix-2^32 ABI form), then its
+// window table 2^(16 w) H_j, w < TW, by doublings: tmp[j TW + w] (radix-2^32 XYZZ)
+__global__ void __launch_bounds__(64) k_open_finish29(const G1Affine* s, uint64_t n, Fr z, G1Xyzz* tmp) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    G1X29 acc;
+    bool inf = true;
+    const G1Affine a = j ? ld_affine(s + j) : G1Affine{Fq::zero(), Fq::zero()};
+    if (!is_inf(a)) {
+        const F29 x = unpack29(to_fq261(a.x)), y = unpack29(to_fq261(a.y));
+        const Fr k = to_canonical(pow_u64(z, j - 1));
+        for (int w = 7; w >= 0; w--) {
+            const uint32_t word = k.v[w];
+            for (int bit = 31; bit >= 0; bit--) {
+                if (!inf) dbl29(acc);
+                if ((word >> bit) & 1) madd29_any(acc, inf, x, y);
+            }
+        }
+    }
+    G1Xyzz* dst = tmp + j * TW;
+    for (uint32_t w = 0; w < TW; w++) {
+        st_xyzz(dst + w, x29_to_xyzz(acc, inf));
+        if (!inf && w + 1 < TW)
+            for (uint32_t d = 0; d < TC; d++) dbl29(acc);
+    }
+}
+
 unsigned grid_for(uint64_t threads, uint32_t block) { return (unsigned)((threads + block - 1) / block); }
 
 // exclusive prefix sum of a[0..len) in place; tmp holds >= len / SCAN + len / SCAN^2 + ... points
@@ -130,9 +264,44 @@ struct Scratch {
     }
 };
 
+// radix-2^29 fast path: P_i from the SRS table, one kernel for H_j and its window table
+Status opening_bases_async29(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, const Fr& z, hipStream_t st,
+                             Scratch& sc, eon_msm_bases** out) {
+    EON_HIP(sc.pts.ensure(n * sizeof(G1Xyzz)));
+    EON_HIP(sc.tmp.ensure((n / (SCAN - 1) + 64) * sizeof(G1Xyzz)));
+    EON_HIP(sc.aff.ensure(n * sizeof(G1Affine)));
+    EON_HIP(sc.table_tmp.ensure(n * TW * sizeof(G1Xyzz)));
+    eon_msm_bases* b = nullptr;
+    EON_TRY(bases_alloc_table(ctx, n, TC, &b));
+    // ~15 dbl (6M+3S) + 257 madd (8M+2S) and ~254 dbl + ~127 madd + 240 dbl per point
+    ctx->prof.begin("k_open_scale29", n * (TW * 64ull + 128ull), st, n * 2705ull);
+    hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(n, 64)), dim3(64), 0, st, bases_table29(srs), n, inverse(z),
+                       sc.pts.as<G1Xyzz>());
+    ctx->prof.end(st);
+    scan_exclusive(sc.pts.as<G1Xyzz>(), n, sc.tmp.as<G1Xyzz>(), st);
+    EON_HIP(launch_batch_to_affine(sc.pts.as<G1Xyzz>(), n, sc.aff.as<G1Affine>(), st));
+    ctx->prof.begin("k_open_finish29", n * (64ull + TW * 128ull), st, n * 5716ull);
+    hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(n, 64)), dim3(64), 0, st, sc.aff.as<G1Affine>(), n, z,
+                       sc.table_tmp.as<G1Xyzz>());
+    ctx->prof.end(st);
+    hipError_t e = launch_batch_to_affine(sc.table_tmp.as<G1Xyzz>(), n * TW, bases_table_mut(b), st);
+    Status s = e == hipSuccess ? bases_seal_table(b, st) : Status::err(EON_E_DEVICE, hipGetErrorString(e));
+    if (s.bad()) {
+        (void)hipStreamSynchronize(st);
+        bases_free(b);
+        return s;
+    }
+    *out = b;
+    return Status::ok();
+}
+
 // enqueue the bases of point z on st (no host sync)
 Status opening_bases_async(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, const Fr& z, hipStream_t st,
                            Scratch& sc, eon_msm_bases** out) {
+    static const bool slow = getenv("EON_OPEN_BASES_R32") != nullptr;
+    if (!slow && !z.is_zero() && bases_table29(srs) && bases_window(srs) == TC && bases_windows(srs) == TW &&
+        n >= 2)
+        return opening_bases_async29(ctx, srs, n, z, st, sc, out);
     const G1Affine* g = bases_points(srs);
     EON_HIP(sc.h_aff.ensure(n * sizeof(G1Affine)));
     if (z.is_zero()) {

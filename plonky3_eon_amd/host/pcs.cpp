@@ -7,8 +7,10 @@
 #include <array>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <map>
 #include <mutex>
+#include <thread>
 
 namespace eon_host {
 
@@ -260,88 +262,148 @@ void KzgPcs::commit_quotient(const Domain& quotient_domain, const DeviceMatrix& 
 }
 
 std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
-    for (const OpenRound& r : rounds)
+    for (const OpenRound& r : rounds) {
+        if (r.data->size() != r.points.size()) throw Error(EON_E_SHAPE, "one point list per matrix");
         for (const MatrixProverData& m : *r.data)
             if (!m.prepared) return open_quotients(rounds);
-    // opening bases per (height, point), shared by every matrix opened there (the trace and the
-    // quotient chunks at zeta)
-    std::map<std::pair<uint64_t, std::array<uint64_t, 4>>, eon_msm_bases*> bases_at;
+    }
+    using Key = std::pair<uint64_t, std::array<uint64_t, 4>>;
+    auto key_of = [](uint64_t n, const Fr& z) {
+        const eon_fr za = z.abi();
+        return Key(n, std::array<uint64_t, 4>{za.l[0], za.l[1], za.l[2], za.l[3]});
+    };
+    // opening bases per distinct (height, point), in order of first use; shared by every matrix
+    // opened there (the trace and the quotient chunks at zeta)
+    std::vector<Key> keys;
+    std::map<Key, eon_msm_bases*> bases_at;
     struct BasesGuard {
-        std::map<std::pair<uint64_t, std::array<uint64_t, 4>>, eon_msm_bases*>& m;
+        std::map<Key, eon_msm_bases*>& m;
         ~BasesGuard() {
             for (auto& kv : m)
                 if (kv.second) eon_msm_bases_destroy(kv.second);
         }
     } guard{bases_at};
-    auto key_of = [](uint64_t n, const Fr& z) {
-        const eon_fr za = z.abi();
-        return std::make_pair(n, std::array<uint64_t, 4>{za.l[0], za.l[1], za.l[2], za.l[3]});
-    };
-    // every distinct (height, point) up front, each height's points in one call (their
-    // constructions overlap on the device)
-    {
-        std::map<uint64_t, std::vector<eon_fr>> todo;
-        for (const OpenRound& r : rounds) {
-            if (r.data->size() != r.points.size()) throw Error(EON_E_SHAPE, "one point list per matrix");
-            for (size_t m = 0; m < r.data->size(); m++)
-                for (const Fr& z : r.points[m]) {
-                    const uint64_t n = (*r.data)[m].coeffs.height;
-                    const auto key = key_of(n, z);
-                    if (bases_at.count(key)) continue;
-                    bases_at.emplace(key, nullptr);
-                    todo[n].push_back(z.abi());
-                }
-        }
-        for (auto& [n, zs] : todo) {
+    for (const OpenRound& r : rounds)
+        for (size_t m = 0; m < r.data->size(); m++)
+            for (const Fr& z : r.points[m]) {
+                const Key k = key_of((*r.data)[m].coeffs.height, z);
+                if (bases_at.emplace(k, nullptr).second) keys.push_back(k);
+            }
+    auto build = [&](eon_ctx* c, const std::vector<Key>& ks) {
+        std::map<uint64_t, std::vector<eon_fr>> by_height;
+        for (const Key& k : ks) by_height[k.first].push_back(eon_fr{{k.second[0], k.second[1], k.second[2], k.second[3]}});
+        for (auto& [n, zs] : by_height) {
             std::vector<eon_msm_bases*> made(zs.size(), nullptr);
-            check(ctx_, eon_kzg_opening_bases_create_many(ctx_, bases_, n, zs.data(), (uint32_t)zs.size(), made.data()),
+            check(c, eon_kzg_opening_bases_create_many(c, bases_, n, zs.data(), (uint32_t)zs.size(), made.data()),
                   "opening bases");
             for (size_t t = 0; t < zs.size(); t++)
-                bases_at[std::make_pair(n, std::array<uint64_t, 4>{zs[t].l[0], zs[t].l[1], zs[t].l[2], zs[t].l[3]})] =
-                    made[t];
+                bases_at[Key(n, std::array<uint64_t, 4>{zs[t].l[0], zs[t].l[1], zs[t].l[2], zs[t].l[3]})] = made[t];
         }
-    }
-    auto opening_bases = [&](uint64_t n, const Fr& z) { return bases_at.at(key_of(n, z)); };
+    };
     hipStream_t st = static_cast<hipStream_t>(eon_ctx_stream(ctx_));
     std::vector<Opened> out(rounds.size());
+    // f(z) of every column at every point (the remainder of quotient_and_eval, util.rs:100-111)
     for (size_t r = 0; r < rounds.size(); r++) {
         const auto& data = *rounds[r].data;
-        if (data.size() != rounds[r].points.size()) throw Error(EON_E_SHAPE, "one point list per matrix");
         out[r].values.resize(data.size());
         out[r].witnesses.resize(data.size());
         for (size_t m = 0; m < data.size(); m++) {
             const MatrixProverData& md = data[m];
             const std::vector<Fr>& pts = rounds[r].points[m];
-            const uint64_t n = md.coeffs.height;
             const uint32_t w = md.coeffs.width;
             out[r].values[m].resize(pts.size());
             out[r].witnesses[m].resize(pts.size());
-            // f(z) of every column (the remainder of quotient_and_eval, util.rs:100-111)
             DeviceBuffer vals(std::max<uint64_t>(pts.size() * w, 1) * sizeof(eon_fr));
-            std::vector<const eon_msm_bases*> hb;
             for (size_t p = 0; p < pts.size(); p++) {
                 const eon_fr z = pts[p].abi();
                 check(ctx_,
-                      eon_quotient_and_eval_columns_dev(ctx_, md.coeffs.data(), n, w, &z, nullptr,
+                      eon_quotient_and_eval_columns_dev(ctx_, md.coeffs.data(), md.coeffs.height, w, &z, nullptr,
                                                         vals.as<eon_fr>() + p * w),
                       "opened values");
-                hb.push_back(opening_bases(n, pts[p]));
             }
             std::vector<eon_fr> hv(pts.size() * w);
             hip_check(hipMemcpyAsync(hv.data(), vals.get(), hv.size() * sizeof(eon_fr), hipMemcpyDeviceToHost, st),
                       "opened values");
             hip_check(hipStreamSynchronize(st), "opened values");
-            // every point's witnesses of every column in one run over the prepared digits
-            std::vector<eon_g1_affine> wits(pts.size() * w);
-            check(ctx_,
-                  eon_msm_g1_columns_prepared(ctx_, hb.data(), (uint32_t)hb.size(), md.prepared.get(), wits.data()),
-                  "witnesses");
-            for (size_t p = 0; p < pts.size(); p++) {
+            for (size_t p = 0; p < pts.size(); p++)
                 out[r].values[m][p].assign(hv.begin() + p * w, hv.begin() + (p + 1) * w);
-                out[r].witnesses[m][p].assign(wits.begin() + p * w, wits.begin() + (p + 1) * w);
-            }
         }
     }
+    // witnesses of the (matrix, point) pairs whose bases are ready, every point of a matrix in
+    // one run over its prepared digits
+    std::vector<std::vector<std::vector<bool>>> done(rounds.size());
+    for (size_t r = 0; r < rounds.size(); r++)
+        for (size_t m = 0; m < rounds[r].points.size(); m++) done[r].emplace_back(rounds[r].points[m].size(), false);
+    auto run_ready = [&] {
+        for (size_t r = 0; r < rounds.size(); r++)
+            for (size_t m = 0; m < rounds[r].data->size(); m++) {
+                const MatrixProverData& md = (*rounds[r].data)[m];
+                const uint32_t w = md.coeffs.width;
+                std::vector<size_t> ps;
+                std::vector<const eon_msm_bases*> hb;
+                for (size_t p = 0; p < rounds[r].points[m].size(); p++) {
+                    eon_msm_bases* b = bases_at.at(key_of(md.coeffs.height, rounds[r].points[m][p]));
+                    if (done[r][m][p] || !b) continue;
+                    ps.push_back(p);
+                    hb.push_back(b);
+                }
+                if (ps.empty()) continue;
+                std::vector<eon_g1_affine> wits(ps.size() * w);
+                check(ctx_,
+                      eon_msm_g1_columns_prepared(ctx_, hb.data(), (uint32_t)hb.size(), md.prepared.get(), wits.data()),
+                      "witnesses");
+                for (size_t q = 0; q < ps.size(); q++) {
+                    out[r].witnesses[m][ps[q]].assign(wits.begin() + q * w, wits.begin() + (q + 1) * w);
+                    done[r][m][ps[q]] = true;
+                }
+            }
+    };
+    // EON_OPEN_OVERLAP=1: the first point's bases, then the others built on the auxiliary context
+    // while the main one runs the first point's witness MSMs.  Measured equal to building all
+    // bases first (the MSM already saturates the VALUs the bases' kernels need), so off.
+    static const bool overlap = [] {
+        const char* e = getenv("EON_OPEN_OVERLAP");
+        return e && e[0] == '1';
+    }();
+    if (!overlap || !aux_ || keys.size() < 2) {
+        build(ctx_, keys);
+        run_ready();
+        return out;
+    }
+    build(ctx_, {keys[0]});
+    const std::vector<Key> rest(keys.begin() + 1, keys.end());
+    // the thread fills its own map; merged after the join (bases_at is read by run_ready meanwhile)
+    std::map<Key, eon_msm_bases*> made;
+    std::exception_ptr err;
+    const int dev = eon_ctx_device(ctx_);
+    std::thread th([&] {
+        try {
+            hip_check(hipSetDevice(dev), "hipSetDevice");
+            std::map<uint64_t, std::vector<eon_fr>> by_height;
+            for (const Key& k : rest)
+                by_height[k.first].push_back(eon_fr{{k.second[0], k.second[1], k.second[2], k.second[3]}});
+            for (auto& [n, zs] : by_height) {
+                std::vector<eon_msm_bases*> bs(zs.size(), nullptr);
+                check(aux_, eon_kzg_opening_bases_create_many(aux_, bases_, n, zs.data(), (uint32_t)zs.size(), bs.data()),
+                      "opening bases");
+                for (size_t t = 0; t < zs.size(); t++)
+                    made[Key(n, std::array<uint64_t, 4>{zs[t].l[0], zs[t].l[1], zs[t].l[2], zs[t].l[3]})] = bs[t];
+            }
+        } catch (...) {
+            err = std::current_exception();
+        }
+    });
+    try {
+        run_ready();
+    } catch (...) {
+        th.join();
+        for (auto& kv : made) bases_at[kv.first] = kv.second;
+        throw;
+    }
+    th.join();
+    for (auto& kv : made) bases_at[kv.first] = kv.second;
+    if (err) std::rethrow_exception(err);
+    run_ready();
     return out;
 }
 

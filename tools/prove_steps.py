@@ -1,4 +1,5 @@
-"""Per-step prove timings and device memory (diagnostic): python tools/prove_steps.py [steps]"""
+"""Per-step prove timings and device memory (diagnostic):
+python tools/prove_steps.py [steps] [bench.py options, e.g. --vector-len 1]"""
 import sys
 import time
 from pathlib import Path
@@ -11,7 +12,7 @@ import bench  # noqa: E402
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    args = bench.make_parser().parse_args([])
+    args = bench.make_parser().parse_args(sys.argv[2:])
     from plonky3_eon_amd import Context
 
     torch.cuda.set_device(0)

@@ -42,6 +42,18 @@ typedef struct {
 } eon_g1_affine;
 
 typedef struct eon_ctx eon_ctx;
+
+/* An all-gather over DEVICE buffers among `world` processes (one per GPU): recv receives `world`
+ * blocks of `bytes`, in rank order.  Called with a context's stream; it must leave recv complete
+ * and ordered before that stream's later work (an RCCL all-gather enqueued on `hip_stream` does; a
+ * host-staged one synchronizes).  The lane-sharded prove (eon_prove.h) and a context's sharded
+ * work (eon_ctx_set_collective) use it. */
+typedef struct {
+    uint32_t rank;
+    uint32_t world;
+    int (*all_gather)(void* user, const void* send, void* recv, uint64_t bytes, void* hip_stream);
+    void* user;
+} eon_collective;
 typedef struct eon_msm_bases eon_msm_bases;
 typedef struct eon_msm_scalars eon_msm_scalars;
 
@@ -72,6 +84,11 @@ int eon_ctx_set_stream(eon_ctx* ctx, void* hip_stream);
 void* eon_ctx_stream(eon_ctx* ctx);
 /* The device ordinal the context was created on. */
 int eon_ctx_device(const eon_ctx* ctx);
+/* Bind the context to a process group (copied; NULL or world <= 1 unbinds).  Work that is the
+ * same on every rank then splits across the ranks: eon_kzg_opening_bases_create(_many) computes
+ * 1/world of the rows and all-gathers the tables.  Every rank must then make the same calls in
+ * the same order. */
+int eon_ctx_set_collective(eon_ctx* ctx, const eon_collective* coll);
 int eon_ctx_synchronize(eon_ctx* ctx);
 /* Per-launch kernel timing with HIP events on the launch stream (the analogue of the
  * reference's tracing spans, e.g. dft/src/radix_2_dit_parallel.rs:168).  eon_ctx_profile(ctx, 1)

@@ -34,15 +34,7 @@ void eon_kzg_pcs_destroy(eon_kzg_pcs* pcs);
 const char* eon_kzg_pcs_last_error(const eon_kzg_pcs* pcs);
 
 /* Lane-sharded prove: this rank's share of VECTOR_LEN and an all-gather over
- * DEVICE buffers -- recv receives `world` blocks of `bytes`, in rank order.  The driver calls it
- * with the context's stream; it must leave recv complete and ordered before that stream's later
- * work (an RCCL all-gather enqueued on `hip_stream` does; a host-staged one synchronizes). */
-typedef struct {
-    uint32_t rank;
-    uint32_t world;
-    int (*all_gather)(void* user, const void* send, void* recv, uint64_t bytes, void* hip_stream);
-    void* user;
-} eon_collective;
+ * DEVICE buffers (eon_collective, declared in eon.h). */
 
 /* An RCCL (NCCL API over xGMI) all-gather for eon_collective: rank 0 creates the unique id
  * (128 bytes), every rank receives it out of band (e.g. torch.distributed) and initialises its

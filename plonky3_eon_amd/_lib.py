@@ -66,6 +66,7 @@ SIGNATURES = {
     "eon_ctx_set_stream": (_INT, [_P, _P]),
     "eon_ctx_stream": (_P, [_P]),
     "eon_ctx_device": (_INT, [_P]),
+    "eon_ctx_set_collective": (_INT, [_P, _P]),
     "eon_ctx_synchronize": (_INT, [_P]),
     "eon_ctx_profile": (_INT, [_P, _INT]),
     "eon_ctx_profile_report": (_INT, [_P, ctypes.c_char_p, _U64]),

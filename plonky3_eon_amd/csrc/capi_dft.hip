@@ -373,6 +373,18 @@ int eon_ctx_set_stream(eon_ctx* ctx, void* hip_stream) {
 
 int eon_ctx_device(const eon_ctx* ctx) { return ctx ? ctx->device : -1; }
 
+int eon_ctx_set_collective(eon_ctx* ctx, const eon_collective* coll) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!coll || coll->world <= 1) {
+        ctx->coll = eon_collective{0, 0, nullptr, nullptr};
+        return EON_OK;
+    }
+    if (!coll->all_gather || coll->rank >= coll->world) return EON_E_ARG;
+    ctx->coll = *coll;
+    return EON_OK;
+}
+
 void* eon_ctx_stream(eon_ctx* ctx) {
     if (!ctx) return nullptr;
     std::lock_guard<std::mutex> lk(ctx->mu);

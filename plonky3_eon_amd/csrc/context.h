@@ -116,6 +116,9 @@ struct eon_ctx {
     // per-launch HIP-event timing (eon_ctx_profile_*)
     eon::Profiler prof;
 
+    // process group for work replicated on every rank (eon_ctx_set_collective; world 0 = none)
+    eon_collective coll{0, 0, nullptr, nullptr};
+
     // MSM pipeline: workspaces msm / msm_b / msm_c for batches k % 3; piece sums + reductions on
     // `stream` / msm_side, digit sorts on the high-priority msm_sort (msm.hip: msm_run_columns)
     eon::MsmWork msm, msm_b, msm_c, msm_d;

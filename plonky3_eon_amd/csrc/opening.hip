@@ -15,6 +15,10 @@
 #include "ec29.h"
 #include "msm.h"
 
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
 using namespace eon;
 
 namespace {
@@ -138,10 +142,14 @@ __device__ __forceinline__ void madd29_any(G1X29& acc, bool& inf, const F29& x, 
 // each written as 16 digits +-1, so that every bit level adds every window's entry (no lane
 // divergence): 15 doublings + 256 mixed additions, against ~254 + ~254 divergent ones for
 // double-and-add.
-__global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, uint64_t n, Fr zinv, G1Xyzz* out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (i + 1 == n) {
+// rows i = lo + t, t < cnt (a rank's slice; rows >= n - 1 are the identity)
+__global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, uint64_t n, uint64_t lo, uint64_t cnt,
+                                                     Fr zinv, G1Xyzz* out_slice) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const uint64_t i = lo + t;
+    G1Xyzz* out = out_slice - lo;
+    if (i + 1 >= n) {
         st_xyzz(out + i, xyzz_inf());
         return;
     }
@@ -217,12 +225,17 @@ __global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, uint64
 
 // H_j = z^(j-1) S_j (double-and-add in radix 2^29; S_j affine, radix-2^32 ABI form), then its
 // window table 2^(16 w) H_j, w < TW, by doublings: tmp[j TW + w] (radix-2^32 XYZZ)
-__global__ void __launch_bounds__(64) k_open_finish29(const G1Affine* s, uint64_t n, Fr z, G1Xyzz* tmp) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+// rows j = lo + t, t < cnt; s and tmp are the slice's (rows >= n are the identity)
+__global__ void __launch_bounds__(64) k_open_finish29(const G1Affine* s_slice, uint64_t n, uint64_t lo, uint64_t cnt,
+                                                      Fr z, G1Xyzz* tmp_slice) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const uint64_t j = lo + t;
+    const G1Affine* s = s_slice - lo;
+    G1Xyzz* tmp = tmp_slice - lo * TW;
     G1X29 acc;
     bool inf = true;
-    const G1Affine a = j ? ld_affine(s + j) : G1Affine{Fq::zero(), Fq::zero()};
+    const G1Affine a = (j && j < n) ? ld_affine(s + j) : G1Affine{Fq::zero(), Fq::zero()};
     if (!is_inf(a)) {
         const F29 x = unpack29(to_fq261(a.x)), y = unpack29(to_fq261(a.y));
         const Fr k = to_canonical(pow_u64(z, j - 1));
@@ -240,6 +253,20 @@ __global__ void __launch_bounds__(64) k_open_finish29(const G1Affine* s, uint64_
         if (!inf && w + 1 < TW)
             for (uint32_t d = 0; d < TC; d++) dbl29(acc);
     }
+}
+
+__global__ void k_set_inf(G1Xyzz* p) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) st_xyzz(p, xyzz_inf());
+}
+
+// sharded scan: s[t] += sum of the slice totals of the ranks before this one
+__global__ void k_add_rank_offset(G1Xyzz* s, uint64_t cnt, const G1Affine* totals, uint32_t npoints,
+                                  uint32_t point, uint32_t rank) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    G1Xyzz acc = ld_xyzz(s + t);
+    for (uint32_t g = 0; g < rank; g++) acc = xyzz_add_affine(acc, ld_affine(totals + (uint64_t)g * npoints + point));
+    st_xyzz(s + t, acc);
 }
 
 unsigned grid_for(uint64_t threads, uint32_t block) { return (unsigned)((threads + block - 1) / block); }
@@ -275,13 +302,13 @@ Status opening_bases_async29(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
     EON_TRY(bases_alloc_table(ctx, n, TC, &b));
     // ~15 dbl (6M+3S) + 257 madd (8M+2S) and ~254 dbl + ~127 madd + 240 dbl per point
     ctx->prof.begin("k_open_scale29", n * (TW * 64ull + 128ull), st, n * 2705ull);
-    hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(n, 64)), dim3(64), 0, st, bases_table29(srs), n, inverse(z),
-                       sc.pts.as<G1Xyzz>());
+    hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(n, 64)), dim3(64), 0, st, bases_table29(srs), n, 0ull, n,
+                       inverse(z), sc.pts.as<G1Xyzz>());
     ctx->prof.end(st);
     scan_exclusive(sc.pts.as<G1Xyzz>(), n, sc.tmp.as<G1Xyzz>(), st);
     EON_HIP(launch_batch_to_affine(sc.pts.as<G1Xyzz>(), n, sc.aff.as<G1Affine>(), st));
     ctx->prof.begin("k_open_finish29", n * (64ull + TW * 128ull), st, n * 5716ull);
-    hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(n, 64)), dim3(64), 0, st, sc.aff.as<G1Affine>(), n, z,
+    hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(n, 64)), dim3(64), 0, st, sc.aff.as<G1Affine>(), n, 0ull, n, z,
                        sc.table_tmp.as<G1Xyzz>());
     ctx->prof.end(st);
     hipError_t e = launch_batch_to_affine(sc.table_tmp.as<G1Xyzz>(), n * TW, bases_table_mut(b), st);
@@ -331,6 +358,106 @@ Status opening_bases_async(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, c
                         &sc.table_tmp);
 }
 
+// Sharded over the context's process group (every rank calls with the same arguments): rank g
+// computes rows [g m, (g+1) m), m = ceil(n / world), of every point's bases -- P_i, the slice's
+// exclusive prefix sums and total, H_j and its window table -- with two all-gathers: the slice
+// totals (each rank adds those of the ranks before it) and the finished table slices.
+Status opening_bases_sharded(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, const std::vector<Fr>& zs,
+                             eon_msm_bases** outs) {
+    const eon_collective& coll = ctx->coll;
+    const uint32_t world = coll.world, rank = coll.rank, np = (uint32_t)zs.size();
+    const uint64_t m = (n + world - 1) / world, lo = (uint64_t)rank * m;
+    hipStream_t streams[3] = {ctx->stream, ctx->msm_side, ctx->msm_side2};
+    // per point: slice points (+1 for the total), scan scratch, affine slice, table slice
+    std::vector<Scratch> sc(np);
+    DevBuf totals_x, totals_a, all_totals, send, recv;
+    struct Release {
+        std::vector<Scratch>& sc;
+        DevBuf* b[5];
+        ~Release() {
+            for (auto& x : sc) x.release();
+            for (DevBuf* x : b) x->release();
+        }
+    } release{sc, {&totals_x, &totals_a, &all_totals, &send, &recv}};
+    EON_HIP(totals_x.ensure(np * sizeof(G1Xyzz)));
+    EON_HIP(totals_a.ensure(np * sizeof(G1Affine)));
+    EON_HIP(all_totals.ensure((uint64_t)world * np * sizeof(G1Affine)));
+    const uint64_t slice_entries = m * TW;  // per point
+    EON_HIP(send.ensure(np * slice_entries * sizeof(G1Affine)));
+    EON_HIP(recv.ensure((uint64_t)world * np * slice_entries * sizeof(G1Affine)));
+    EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));
+    EON_HIP(hipStreamWaitEvent(ctx->msm_side, ctx->msm_ev[0], 0));
+    EON_HIP(hipStreamWaitEvent(ctx->msm_side2, ctx->msm_ev[0], 0));
+    // phase 1: P_i of the slice and its exclusive prefix sums; the total lands at index m
+    for (uint32_t t = 0; t < np; t++) {
+        hipStream_t st = streams[t % 3];
+        EON_HIP(sc[t].pts.ensure((m + 1) * sizeof(G1Xyzz)));
+        EON_HIP(sc[t].tmp.ensure(((m + 1) / (SCAN - 1) + 64) * sizeof(G1Xyzz)));
+        EON_HIP(sc[t].aff.ensure(m * sizeof(G1Affine)));
+        EON_HIP(sc[t].table_tmp.ensure(slice_entries * sizeof(G1Xyzz)));
+        ctx->prof.begin("k_open_scale29", m * (TW * 64ull + 128ull), st, m * 2705ull);
+        hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(m, 64)), dim3(64), 0, st, bases_table29(srs), n, lo, m,
+                           inverse(zs[t]), sc[t].pts.as<G1Xyzz>());
+        ctx->prof.end(st);
+        // one identity past the slice: the exclusive scan leaves the slice total there
+        hipLaunchKernelGGL(k_set_inf, dim3(1), dim3(1), 0, st, sc[t].pts.as<G1Xyzz>() + m);
+        scan_exclusive(sc[t].pts.as<G1Xyzz>(), m + 1, sc[t].tmp.as<G1Xyzz>(), st);
+        EON_HIP(hipMemcpyAsync(totals_x.as<G1Xyzz>() + t, sc[t].pts.as<G1Xyzz>() + m, sizeof(G1Xyzz),
+                               hipMemcpyDeviceToDevice, st));
+        EON_HIP(hipEventRecord(ctx->msm_ev[1 + (t % 2)], st));
+        EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[1 + (t % 2)], 0));
+    }
+    EON_HIP(launch_batch_to_affine(totals_x.as<G1Xyzz>(), np, totals_a.as<G1Affine>(), ctx->stream));
+    if (coll.all_gather(coll.user, totals_a.p, all_totals.p, np * sizeof(G1Affine), ctx->stream) != 0)
+        return Status::err(EON_E_DEVICE, "collective all_gather failed (opening bases totals)");
+    EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));
+    EON_HIP(hipStreamWaitEvent(ctx->msm_side, ctx->msm_ev[0], 0));
+    EON_HIP(hipStreamWaitEvent(ctx->msm_side2, ctx->msm_ev[0], 0));
+    // phase 2: S_j = the ranks' offset + the slice's prefix sums; H_j and its table slice
+    for (uint32_t t = 0; t < np; t++) {
+        hipStream_t st = streams[t % 3];
+        if (rank)
+            hipLaunchKernelGGL(k_add_rank_offset, dim3(grid_for(m, 64)), dim3(64), 0, st, sc[t].pts.as<G1Xyzz>(), m,
+                               all_totals.as<G1Affine>(), np, t, rank);
+        EON_HIP(launch_batch_to_affine(sc[t].pts.as<G1Xyzz>(), m, sc[t].aff.as<G1Affine>(), st));
+        ctx->prof.begin("k_open_finish29", m * (64ull + TW * 128ull), st, m * 5716ull);
+        hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(m, 64)), dim3(64), 0, st, sc[t].aff.as<G1Affine>(), n, lo,
+                           m, zs[t], sc[t].table_tmp.as<G1Xyzz>());
+        ctx->prof.end(st);
+        EON_HIP(launch_batch_to_affine(sc[t].table_tmp.as<G1Xyzz>(), slice_entries,
+                                       send.as<G1Affine>() + (uint64_t)t * slice_entries, st));
+        EON_HIP(hipEventRecord(ctx->msm_ev[1 + (t % 2)], st));
+        EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[1 + (t % 2)], 0));
+    }
+    if (coll.all_gather(coll.user, send.p, recv.p, np * slice_entries * sizeof(G1Affine), ctx->stream) != 0)
+        return Status::err(EON_E_DEVICE, "collective all_gather failed (opening bases tables)");
+    // phase 3: every point's table from the ranks' slices (rank order = row order), then sealed
+    for (uint32_t t = 0; t < np; t++) outs[t] = nullptr;
+    Status s = Status::ok();
+    for (uint32_t t = 0; t < np && !s.bad(); t++) {
+        s = bases_alloc_table(ctx, n, TC, outs + t);
+        if (s.bad()) break;
+        for (uint32_t g = 0; g < world; g++) {
+            const uint64_t r0 = (uint64_t)g * m;
+            if (r0 >= n) break;
+            const uint64_t rows = std::min<uint64_t>(m, n - r0);
+            const G1Affine* src = recv.as<G1Affine>() + ((uint64_t)g * np + t) * slice_entries;
+            const hipError_t e = hipMemcpyAsync(bases_table_mut(outs[t]) + r0 * TW, src, rows * TW * sizeof(G1Affine),
+                                                hipMemcpyDeviceToDevice, ctx->stream);
+            if (e != hipSuccess) s = Status::err(EON_E_DEVICE, hipGetErrorString(e));
+        }
+        if (!s.bad()) s = bases_seal_table(outs[t], ctx->stream);
+    }
+    for (hipStream_t st : streams) (void)hipStreamSynchronize(st);
+    if (s.bad())
+        for (uint32_t t = 0; t < np; t++)
+            if (outs[t]) {
+                bases_free(outs[t]);
+                outs[t] = nullptr;
+            }
+    return s;
+}
+
 // every point's bases at once: point t's whole pipeline on stream t % 3 (the latency-bound
 // scalar multiplications of different points overlap)
 Status opening_bases_many(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, const eon_fr* points,
@@ -344,6 +471,13 @@ Status opening_bases_many(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, co
         if (!fr_is_canonical(zs[t])) return Status::err(EON_E_ARG, "point is not a canonical Fr");
         outs[t] = nullptr;
     }
+    // sharded when the context is bound to a process group and every point takes the radix-2^29
+    // path (a uniform decision: every rank has the same points and SRS)
+    static const bool slow = getenv("EON_OPEN_BASES_R32") != nullptr;
+    static const bool no_shard = getenv("EON_OPEN_BASES_NO_SHARD") != nullptr;
+    bool fast = !slow && bases_table29(srs) && bases_window(srs) == TC && bases_windows(srs) == TW && n >= 2;
+    for (const Fr& z : zs) fast = fast && !z.is_zero();
+    if (fast && !no_shard && ctx->coll.world > 1 && npoints) return opening_bases_sharded(ctx, srs, n, zs, outs);
     hipStream_t streams[3] = {ctx->stream, ctx->msm_side, ctx->msm_side2};
     EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));
     EON_HIP(hipStreamWaitEvent(ctx->msm_side, ctx->msm_ev[0], 0));

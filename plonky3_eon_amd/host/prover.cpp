@@ -151,7 +151,20 @@ Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t hei
     rounds[0].points = {{zeta, zeta_next}};
     rounds[1].data = &quotient_data;
     rounds[1].points.assign(num_chunks, std::vector<Fr>{zeta});
-    std::vector<Opened> opened = pcs.open(rounds);  // prover.rs:424-442
+    // the opening bases are the same on every rank: sharded over the process group
+    // (eon_ctx_set_collective; EON_OPEN_BASES_NO_SHARD=1 keeps them replicated)
+    struct CollectiveScope {
+        eon_ctx* c;
+        CollectiveScope(eon_ctx* c_, const eon_collective* s) : c(c_) {
+            if (s) check(c, eon_ctx_set_collective(c, s), "eon_ctx_set_collective");
+        }
+        ~CollectiveScope() { (void)eon_ctx_set_collective(c, nullptr); }
+    };
+    std::vector<Opened> opened;
+    {
+        CollectiveScope scope(ctx, shard);
+        opened = pcs.open(rounds);  // prover.rs:424-442
+    }
     auto t5 = tick();
 
     proof.quotient_commit.resize(num_chunks);

@@ -13,6 +13,8 @@ RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment, backend gloo).
   native -- the C++ prove driver (libeonprove.so) sharded over the ranks with a torch.distributed
           eon_collective; rank 0 compares it with the driver's unsharded prove and the Python
           prover's.
+  openshard -- KZG opening bases built by every rank alone and then sharded over the ranks
+          (eon_ctx_set_collective) at the headline height 2^17: the witnesses must agree.
 
 Writes {"ok": true} or {"ok": false, "why": ...} as JSON to argv[2].
 """
@@ -257,6 +259,39 @@ def run_msmshard(rank, world, group):
     return None
 
 
+def run_openshard(rank, world, group):
+    import ctypes
+
+    import torch
+
+    from plonky3_eon_amd import Context
+    from plonky3_eon_amd.msm import MsmBases, srs_powers
+    from plonky3_eon_amd.native import TorchCollective
+
+    ctx = Context(0)
+    n, width = 1 << 17, 3
+    srs = MsmBases(srs_powers(n + 1, 12345, ctx), ctx, precompute=True)
+    coeffs = C.random_fr(11, n * width).reshape(n, width, 4)
+    _, prep = srs.prepare_columns(torch.from_numpy(coeffs.view(np.int64)).to("cuda:0"), want_commitments=False)
+    points = [C.random_fr(12, 1)[0], C.random_fr(13, 1)[0]]
+    alone = prep.msm(srs.opening_bases_many(n, points))
+    coll = TorchCollective(rank, world, group, 0)
+    ctx.check(ctx.lib.eon_ctx_set_collective(ctx.handle, ctypes.byref(coll.c)))
+    try:
+        shared = prep.msm(srs.opening_bases_many(n, points))
+    finally:
+        ctx.check(ctx.lib.eon_ctx_set_collective(ctx.handle, None))
+    if not np.array_equal(alone, shared):
+        return f"rank {rank}: sharded opening bases give different witnesses"
+    # spot-check one witness against the reference's route (quotient, then commit_column)
+    if rank == 0:
+        q, _ = C.quotient_and_eval(coeffs[:, 1], points[0])
+        g = srs_powers(n - 1, 12345, ctx)
+        if not np.array_equal(shared[0, 1], C.g1_msm(g, q)):
+            return "witness != commit_column(quotient)"
+    return None
+
+
 def main():
     import torch.distributed as dist
 
@@ -265,7 +300,7 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         fn = {"cpu": run_cpu, "gpu": run_gpu, "a2a": run_a2a, "fourstep": run_fourstep,
-              "msmshard": run_msmshard, "native": run_native}[mode]
+              "msmshard": run_msmshard, "native": run_native, "openshard": run_openshard}[mode]
         why = fn(rank, world, None)
     except Exception:
         why = traceback.format_exc()

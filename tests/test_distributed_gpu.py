@@ -14,7 +14,7 @@ def test_sharded_prove_matches_single(world, log_n, vl):
     assert all(r["ok"] for r in res), [r["why"] for r in res]
 
 
-@pytest.mark.parametrize("world,log_n,vl", [(2, 5, 4), (4, 3, 8)])
+@pytest.mark.parametrize("world,log_n,vl", [(2, 5, 4), (4, 3, 8), (2, 17, 2)])
 def test_native_sharded_prove_matches_single(world, log_n, vl):
     """The C++ driver's lane-sharded prove (torch.distributed eon_collective) == its unsharded
     prove == the Python prover."""
@@ -31,4 +31,12 @@ def test_fourstep_dft_matches_oracle(world):
 @pytest.mark.parametrize("world", [1, 3])
 def test_sharded_msm_matches_full(world):
     res = run_world("msmshard", world, timeout=900)
+    assert all(r["ok"] for r in res), [r["why"] for r in res]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_opening_bases(world):
+    """Opening bases split by rows over the ranks (two all-gathers) == each rank's own, at 2^17
+    rows (world 3: uneven slices)."""
+    res = run_world("openshard", world, timeout=900)
     assert all(r["ok"] for r in res), [r["why"] for r in res]

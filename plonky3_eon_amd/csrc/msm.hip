@@ -399,6 +399,47 @@ __global__ void __launch_bounds__(64) k_bucket_reduce29(const G1Raw29* pieces, c
     st_xyzz(U + (uint64_t)g * nseg + s, x29_to_xyzz(acc, acc_inf));
 }
 
+// After the first level (T_j, U_j of the S segments of each group): one block per group does
+// the rest, out[g] = sum_j U_j + 2^log_seg sum_j j T_j + sum_j T_j (= sum_b (b + 1) B_b).
+// Thread t takes segments [t Q, (t + 1) Q): running sums give its total and locally weighted sum,
+// (t Q) times its total by double-and-add, then an LDS tree over the block.  One launch instead
+// of the seg-level / tree / final chain (~12 latency-bound launches per batch).
+constexpr uint32_t GF_THREADS = 256;
+__global__ void __launch_bounds__(GF_THREADS) k_group_finish(const G1Xyzz* T, const G1Xyzz* U, uint32_t S,
+                                                            uint32_t log_seg, G1Xyzz* out) {
+    __shared__ G1Xyzz sh[GF_THREADS];
+    const uint32_t g = blockIdx.x, t = threadIdx.x;
+    const uint32_t nt = S < GF_THREADS ? S : GF_THREADS;
+    const uint32_t Q = S / nt;
+    G1Xyzz c = xyzz_inf();
+    if (t < nt) {
+        const G1Xyzz* Tg = T + (uint64_t)g * S + (uint64_t)t * Q;
+        const G1Xyzz* Ug = U + (uint64_t)g * S + (uint64_t)t * Q;
+        G1Xyzz run = xyzz_inf(), acc = xyzz_inf(), us = xyzz_inf();
+        for (uint32_t k = Q - 1; k >= 1; k--) {
+            run = xyzz_add(run, ld_xyzz(Tg + k));
+            acc = xyzz_add(acc, run);
+        }
+        run = xyzz_add(run, ld_xyzz(Tg));
+        for (uint32_t k = 0; k < Q; k++) us = xyzz_add(us, ld_xyzz(Ug + k));
+        if (t) acc = xyzz_add(acc, xyzz_mul_small(run, t * Q));
+        for (uint32_t d = 0; d < log_seg; d++) acc = xyzz_dbl(acc);
+        c = xyzz_add(xyzz_add(us, acc), run);
+    }
+    sh[t] = c;
+    __syncthreads();
+    for (uint32_t w = GF_THREADS / 2; w > 0; w >>= 1) {
+        if (t < w) {
+            G1Xyzz o = sh[t + w];
+            pin(o);
+            c = xyzz_add(c, o);
+            sh[t] = c;
+        }
+        __syncthreads();
+    }
+    if (t == 0) st_xyzz(out + g, c);
+}
+
 constexpr uint32_t MAX_SEG_LEVELS = 24;
 struct SegLogs {
     uint8_t v[MAX_SEG_LEVELS];
@@ -884,6 +925,25 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
     const G1Xyzz* X = wk.bucket_sums.as<G1Xyzz>();
     uint32_t Lb = B, m = 0;
     prof->begin("k_seg_level", (uint64_t)nb * 128 + (uint64_t)nb / SEG * 256, st);
+    // EON_MSM_SEG_LEVELS=1: the level-by-level chain below instead of k_group_finish
+    static const bool seg_levels = getenv("EON_MSM_SEG_LEVELS") != nullptr;
+    if (!seg_levels) {
+        const uint32_t seg = B < SEG ? B : SEG;
+        const uint32_t nseg = B / seg;
+        G1Xyzz* T = t_buf[0];
+        if (fused)
+            hipLaunchKernelGGL(k_bucket_reduce29, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
+                               wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, seg, groups, T, u_buf);
+        else
+            hipLaunchKernelGGL(k_seg_level, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st, X, B,
+                               seg, groups, T, u_buf);
+        G1Xyzz* per_group = wk.red_a.as<G1Xyzz>();
+        hipLaunchKernelGGL(k_group_finish, dim3(groups), dim3(GF_THREADS), 0, st, T, u_buf, nseg,
+                           31 - __builtin_clz(seg), per_group);
+        prof->end(st);
+        EON_HIP(hipGetLastError());
+        return write_columns(L, bt, per_group, st);
+    }
     while (Lb > 1) {
         const uint32_t seg = Lb < SEG ? Lb : SEG;
         const uint32_t nseg = Lb / seg;

@@ -22,10 +22,6 @@ struct alignas(16) G1Raw29 {
     uint32_t w[36];
 };
 
-__device__ __forceinline__ void pin29(F29& a) {
-#pragma unroll
-    for (int i = 0; i < 9; i++) asm volatile("" : "+v"(a.l[i]));
-}
 
 // 2A for an affine A (29-Montgomery, canonical coordinates): mdbl-2008-s-1
 __device__ __forceinline__ G1X29 dbl29_affine(const F29& x, const F29& y) {

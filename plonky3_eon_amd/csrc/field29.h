@@ -123,6 +123,12 @@ EON_HD bool is_zero29_raw(const F29& a) {
     return o == 0;
 }
 
+// make every limb an opaque register value (no rematerialisation from memory; see field.h pin)
+__device__ __forceinline__ void pin29(F29& a) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) asm volatile("" : "+v"(a.l[i]));
+}
+
 // limb-wise a + b, no carry propagation (a, b normalised -> limbs < 2^30): a product input only
 EON_HD F29 add29_lazy(const F29& a, const F29& b) {
     F29 r;

@@ -18,6 +18,7 @@
 //   * Twiddles: one stage-concatenated table tw[2^s + j] = w_{2^(s+1)}^j (inverse table with
 //     w^-1), built once on device for the largest size seen; smaller transforms use its prefix.
 #include "ntt.h"
+#include "field29.h"
 
 namespace eon {
 
@@ -176,6 +177,159 @@ __global__ void __launch_bounds__(1024) k_ntt_pass(PassArgs a) {
     }
 }
 
+// ---- radix-2^29 butterflies ---------------------------------------------------------------------
+// The same pass with the tile held in LDS as 9 x 29-bit limbs (three planes: limbs 0-3, 4-7, 8)
+// and lazy values < 4p: the product is mul29 (162 carry-free multiply-adds, no carry captures)
+// against twiddles converted to 29-Montgomery form (w 2^261) at staging, so y w 2^256 comes out
+// directly in the radix-2^32 Montgomery form of the product; a butterfly input is brought below
+// 2p by one conditional subtraction, its outputs stay below 4p; the store canonicalises.  Input
+// and output scalings keep the radix-2^32 product (once per element per pass).
+
+__device__ __forceinline__ void lds_put29(uint4* lo, uint4* hi, uint32_t* top, uint32_t i, const F29& x) {
+    lo[i] = make_uint4(x.l[0], x.l[1], x.l[2], x.l[3]);
+    hi[i] = make_uint4(x.l[4], x.l[5], x.l[6], x.l[7]);
+    top[i] = x.l[8];
+}
+
+__device__ __forceinline__ F29 lds_get29(const uint4* lo, const uint4* hi, const uint32_t* top, uint32_t i) {
+    const uint4 a = lo[i], b = hi[i];
+    F29 x;
+    x.l[0] = a.x; x.l[1] = a.y; x.l[2] = a.z; x.l[3] = a.w;
+    x.l[4] = b.x; x.l[5] = b.y; x.l[6] = b.z; x.l[7] = b.w;
+    x.l[8] = top[i];
+    return x;
+}
+
+// a - K p if a >= K p (a normalised)
+template <uint32_t K>
+__device__ __forceinline__ F29 reduce29(const F29& a) {
+    constexpr KP29<FrP, K> kp{};
+    F29 d;
+    int32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        const int32_t t = (int32_t)a.l[i] - (int32_t)kp.l[i] + c;
+        d.l[i] = (uint32_t)t & M29;
+        c = t >> 29;
+    }
+    return c < 0 ? a : d;
+}
+
+template <bool DIF, int LOG_CB>
+__global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
+    constexpr uint32_t CB = 1u << LOG_CB;
+    extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+    const uint32_t k = a.k;
+    const uint32_t ne = CB << k;
+    uint4* lo = lds;
+    uint4* hi = lds + ne;
+    uint32_t* top = reinterpret_cast<uint32_t*>(lds + 2 * ne);
+    // twiddles in 29-form, 9 words each (packing them to 32 B for a fourth resident tile per CU
+    // measured slower: the per-butterfly unpack costs more than the occupancy gains)
+    uint32_t* twl = top + ne;
+
+    const uint32_t s0 = a.s0;
+    const uint64_t g = blockIdx.x / a.col_tiles;
+    const uint64_t low = g & ((1ull << s0) - 1);
+    const uint64_t base_row = low + ((g >> s0) << (s0 + k));
+    const uint64_t col0 = (uint64_t)(blockIdx.x % a.col_tiles) * CB;
+    const uint64_t width = a.width;
+    const uint32_t T = blockDim.x;
+
+    for (uint32_t q = threadIdx.x + 1; q < (1u << k); q += T) {
+        const uint32_t l = 31 - __builtin_clz(q);
+        const uint32_t r = q - (1u << l);
+        const uint64_t s = s0 + l;
+        const F29 w = mul29<FrP>(unpack29(gload(a.tw + (1ull << s) + low + ((uint64_t)r << s0))),
+                                 const29<FrP>(R29<FrP>::TO261));
+#pragma unroll
+        for (int i = 0; i < 9; i++) twl[9 * q + i] = w.l[i];
+    }
+
+    for (uint32_t e = threadIdx.x; e < ne; e += T) {
+        const uint32_t c = e & (CB - 1);
+        const uint32_t m = e >> LOG_CB;
+        const uint64_t p = base_row + ((uint64_t)m << s0);
+        const uint64_t col = col0 + c;
+        Fr x = Fr::zero();
+        if (col < width) {
+            uint64_t r = p;
+            bool present = true;
+            switch (a.load_mode) {
+                case LOAD_BITREV:
+                    r = a.load_param ? (__builtin_bitreverse64(p) >> (64 - a.load_param)) : 0;
+                    break;
+                case LOAD_SPREAD: r = p >> a.load_param; break;
+                case LOAD_ZEROPAD: present = p < a.load_param; break;
+                case LOAD_BITREV_SPREAD: {
+                    const uint32_t nb = a.load_param >> 8;
+                    const uint64_t q = p >> (a.load_param & 0xff);
+                    r = nb ? (__builtin_bitreverse64(q) >> (64 - nb)) : 0;
+                    break;
+                }
+                default: break;
+            }
+            if (present) {
+                x = gload(a.src + r * width + col);
+                if (a.load_scale) x = mul(x, ld_pinned(a.load_scale + r));
+                if (a.has_load_const) x = mul(x, a.load_const);
+            }
+        }
+        lds_put29(lo, hi, top, e, unpack29(x));
+    }
+    __syncthreads();
+
+    for (uint32_t it = 0; it < k; it++) {
+        const uint32_t l = DIF ? (k - 1 - it) : it;
+        const uint32_t half = 1u << l;
+        for (uint32_t b = threadIdx.x; b < (ne >> 1); b += T) {
+            const uint32_t c = b & (CB - 1);
+            const uint32_t j = b >> LOG_CB;
+            const uint32_t r = j & (half - 1);
+            const uint32_t m0 = ((j >> l) << (l + 1)) | r;
+            const uint32_t i0 = (m0 << LOG_CB) | c;
+            const uint32_t i1 = ((m0 + half) << LOG_CB) | c;
+            const F29 x = reduce29<2>(lds_get29(lo, hi, top, i0));  // < 2p
+            const F29 y = lds_get29(lo, hi, top, i1);                 // < 4p
+            const bool unit = (r | low) == 0;
+            F29 u, v;
+            F29 w;
+            if (!unit) {
+#pragma unroll
+                for (int i = 0; i < 9; i++) w.l[i] = twl[9 * (half + r) + i];
+                pin29(w);
+            }
+            if (!DIF) {
+                // DitButterfly (dft/src/butterflies.rs:177-185): (x + w*y, x - w*y)
+                const F29 t = unit ? reduce29<2>(y) : mul29<FrP>(y, w);  // < 2p
+                u = add29_norm(x, t);
+                v = sub29<FrP, 2>(x, t);
+            } else {
+                // DIF butterfly: (x + y, (x - y) * w)
+                const F29 y2 = reduce29<2>(y);
+                u = add29_norm(x, y2);
+                const F29 d = sub29<FrP, 2>(x, y2);  // < 4p
+                v = unit ? d : mul29<FrP>(d, w);
+            }
+            lds_put29(lo, hi, top, i0, u);
+            lds_put29(lo, hi, top, i1, v);
+        }
+        __syncthreads();
+    }
+
+    for (uint32_t e = threadIdx.x; e < ne; e += T) {
+        const uint32_t c = e & (CB - 1);
+        const uint32_t m = e >> LOG_CB;
+        const uint64_t p = base_row + ((uint64_t)m << s0);
+        const uint64_t col = col0 + c;
+        if (col < width) {
+            Fr x = pack29<FrP>(canon29<FrP>(reduce29<2>(lds_get29(lo, hi, top, e))));
+            if (a.store_scale) x = mul(x, ld_pinned(a.store_scale + p));
+            gstore(a.dst + p * width + col, x);
+        }
+    }
+}
+
 // out[idx(j)] = scale * base^j for j in [0, n); idx(j) = j, or reverse_bits(j, rev_log) when
 // rev_log != NATURAL_IDX.  Each thread walks a contiguous chunk of exponents.
 __global__ void k_powers(Fr* out, uint64_t n, Fr base, Fr scale, uint32_t rev_log, uint32_t chunk) {
@@ -216,10 +370,17 @@ static hipError_t launch_pass(bool dif, uint32_t log_cb, const PassArgs& a, uint
     uint32_t threads = ne / 2;
     if (threads > max_threads) threads = max_threads;
     if (threads < 64) threads = 64;
-    const size_t lds = (size_t)ne * 32 + ((size_t)1 << a.k) * 32;
+    // EON_NTT_R32=1: the radix-2^32 butterflies (k_ntt_pass)
+    static const bool r32 = getenv("EON_NTT_R32") != nullptr;
+    const size_t lds = r32 ? (size_t)ne * 32 + ((size_t)1 << a.k) * 32 : (size_t)ne * 36 + ((size_t)1 << a.k) * 36;
     dim3 grid((unsigned)(groups * col_tiles));
-#define EON_LAUNCH(D, C) \
-    hipLaunchKernelGGL((k_ntt_pass<D, C>), grid, dim3(threads), lds, st, a)
+#define EON_LAUNCH(D, C)                                                             \
+    do {                                                                             \
+        if (r32)                                                                     \
+            hipLaunchKernelGGL((k_ntt_pass<D, C>), grid, dim3(threads), lds, st, a); \
+        else                                                                         \
+            hipLaunchKernelGGL((k_ntt_pass29<D, C>), grid, dim3(threads), lds, st, a); \
+    } while (0)
     switch ((dif ? 4 : 0) + log_cb) {
         case 0: EON_LAUNCH(false, 0); break;
         case 1: EON_LAUNCH(false, 1); break;
@@ -302,10 +463,15 @@ hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
         }
         a.store_scale = last ? s.store_scale : nullptr;
         const uint64_t groups = (1ull << s.log_m) >> a.k;
-        static const char* names[8] = {"k_ntt_pass<false, 0>", "k_ntt_pass<false, 1>",
-                                       "k_ntt_pass<false, 2>", "k_ntt_pass<false, 3>",
-                                       "k_ntt_pass<true, 0>",  "k_ntt_pass<true, 1>",
-                                       "k_ntt_pass<true, 2>",  "k_ntt_pass<true, 3>"};
+        static const char* names32[8] = {"k_ntt_pass<false, 0>", "k_ntt_pass<false, 1>",
+                                         "k_ntt_pass<false, 2>", "k_ntt_pass<false, 3>",
+                                         "k_ntt_pass<true, 0>",  "k_ntt_pass<true, 1>",
+                                         "k_ntt_pass<true, 2>",  "k_ntt_pass<true, 3>"};
+        static const char* names29[8] = {"k_ntt_pass29<false, 0>", "k_ntt_pass29<false, 1>",
+                                         "k_ntt_pass29<false, 2>", "k_ntt_pass29<false, 3>",
+                                         "k_ntt_pass29<true, 0>",  "k_ntt_pass29<true, 1>",
+                                         "k_ntt_pass29<true, 2>",  "k_ntt_pass29<true, 3>"};
+        static const char* const* names = getenv("EON_NTT_R32") ? names32 : names29;
         // mulmods: one per butterfly (the BASELINE.md count), plus the fused input/output scalings
         const uint64_t elems = (1ull << s.log_m) * s.width;
         const uint64_t mm = elems / 2 * a.k + (a.load_scale ? elems : 0) + (a.has_load_const ? elems : 0) +

@@ -11,5 +11,5 @@ pmc() {  # workload kernel steps
   && timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_${w}_write -o w --output-format csv -- python3 bench.py --workload $w --steps $st --warmup 1 --no-cpu-baseline > /dev/null 2>> gpurun_out/pmc_$w.err \
   && python3 tools/pmc_traffic.py gpurun_out/pmc_${w}_fetch gpurun_out/pmc_${w}_write "$k" gpurun_out/pmc_$w.json gpurun_out/traffic_$w.json
 }
-pmc prove k_piece_sum 1 && pmc lde "k_ntt_pass<false, 3>" 2 && pmc msm k_piece_sum 2
+pmc prove k_piece_sum 1 && pmc lde "k_ntt_pass29<false, 3>" 2 && pmc msm k_piece_sum 2
 rc=$?; tail -2 gpurun_out/pmc_*.err; exit $rc

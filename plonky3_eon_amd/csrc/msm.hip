@@ -440,6 +440,40 @@ __global__ void __launch_bounds__(GF_THREADS) k_group_finish(const G1Xyzz* T, co
     if (t == 0) st_xyzz(out + g, c);
 }
 
+// Few-groups form of k_bucket_reduce29 (a single MSM, the quotient chunks): segment s of group g
+// (buckets [lo, lo + SEG), lo = s SEG; bucket b holds digit b + 1) sums its buckets' raw
+// radix-2^29 pieces and returns sum_b (b + 1) B_b = running-sum form + lo * (sum_b B_b) -- the
+// value of k_segment_sum over the bucket sums, without the combine / bucket-final passes.
+__global__ void __launch_bounds__(64) k_segment_reduce29(const G1Raw29* pieces, const uint32_t* piece_off,
+                                                         uint32_t B, uint32_t groups, G1Xyzz* seg_out) {
+    const uint32_t nseg = B / SEG;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nseg * groups) return;
+    const uint32_t g = t / nseg, s = t % nseg;
+    const uint32_t lo = s * SEG;
+    G1X29 run, acc, x;
+    bool run_inf = true, acc_inf = true;
+    for (int k = (int)SEG - 1; k >= 0; k--) {
+        const uint32_t bp = (lo + (uint32_t)k) * groups + g;
+        const uint32_t e1 = piece_off[bp + 1];
+        for (uint32_t e = piece_off[bp]; e < e1; e++) {
+            const bool inf = ld_raw29(pieces + e, x);
+            acc29(run, run_inf, x, inf);
+        }
+        acc29(acc, acc_inf, run, run_inf);
+    }
+    if (lo && !run_inf) {  // acc += lo * run (double-and-add, MSB first)
+        G1X29 m;
+        bool m_inf = true;
+        for (int bit = 31 - __builtin_clz(lo); bit >= 0; bit--) {
+            if (!m_inf) dbl29(m);
+            if ((lo >> bit) & 1) acc29(m, m_inf, run, false);
+        }
+        acc29(acc, acc_inf, m, m_inf);
+    }
+    st_xyzz(seg_out + t, x29_to_xyzz(acc, acc_inf));
+}
+
 constexpr uint32_t MAX_SEG_LEVELS = 24;
 struct SegLogs {
     uint8_t v[MAX_SEG_LEVELS];
@@ -793,11 +827,15 @@ static SortedRef sorted_ref(const SortedBufs& s) {
                      s.piece_off.as<uint32_t>()};
 }
 
-// the reduction reads k_piece_sum29's raw partials directly (k_bucket_reduce29): radix-2^29
-// pieces, no combine level needed, the many-groups weighted sum
+// the reduction reads k_piece_sum29's raw partials directly (k_bucket_reduce29 /
+// k_segment_reduce29): radix-2^29 pieces, no combine level needed, and either many groups or few
+// pieces per bucket -- with few groups and several pieces per bucket (a single 2^20 MSM: ~4.5)
+// the one-thread-per-segment chain is longer than combine + bucket-final + k_segment_sum
+// (3.23 vs 3.00 ms for the 2^20 MSM)
 static bool fused_reduce(const eon_msm_bases* b, const Batch& bt) {
     static const bool off = getenv("EON_MSM_UNFUSED") != nullptr;
-    return !off && b->r29 && bt.levels <= 1 && bt.groups >= 64 && bt.B >= SEG;
+    return !off && b->r29 && bt.levels <= 1 && bt.B >= SEG &&
+           (bt.groups >= 64 || (uint64_t)bt.n_pieces <= 2ull * bt.nb);
 }
 
 // piece sums of one sorted batch against bases `b` (asynchronous); wk supplies the piece buffers
@@ -851,15 +889,19 @@ static Status write_columns(const MsmLayout& L, const Batch& bt, const G1Xyzz* p
 }
 
 // sum_d d * B_d per group, few-groups form: k_segment_sum + LDS trees (short dependency chains)
-static Status reduce_segments(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, MsmWork& wk,
-                              hipStream_t st) {
+static Status reduce_segments(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, const SortedRef& sr,
+                              MsmWork& wk, hipStream_t st, bool fused) {
     const uint32_t nseg = bt.B / SEG;  // c >= 4, so B >= SEG
     const uint32_t groups = bt.groups;
     EON_HIP(wk.red_a.ensure((uint64_t)groups * nseg * sizeof(G1Xyzz)));
     EON_HIP(wk.red_b.ensure((uint64_t)groups * nseg * sizeof(G1Xyzz)));
     ctx->prof.begin("k_segment_sum", (uint64_t)bt.nb * 128 + (uint64_t)groups * nseg * 128, st);
-    hipLaunchKernelGGL(k_segment_sum, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
-                       wk.bucket_sums.as<G1Xyzz>(), bt.B, groups, wk.red_a.as<G1Xyzz>());
+    if (fused)
+        hipLaunchKernelGGL(k_segment_reduce29, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
+                           wk.piece_raw.as<G1Raw29>(), sr.piece_off, bt.B, groups, wk.red_a.as<G1Xyzz>());
+    else
+        hipLaunchKernelGGL(k_segment_sum, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
+                           wk.bucket_sums.as<G1Xyzz>(), bt.B, groups, wk.red_a.as<G1Xyzz>());
     ctx->prof.end(st);
     G1Xyzz* cur = wk.red_a.as<G1Xyzz>();
     G1Xyzz* nxt = wk.red_b.as<G1Xyzz>();
@@ -912,7 +954,7 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
     if (!fused)
         hipLaunchKernelGGL(k_bucket_final, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_cur, B, groups,
                            part_cur, wk.bucket_sums.as<G1Xyzz>());
-    if (groups < 64) return reduce_segments(ctx, L, bt, wk, st);
+    if (groups < 64) return reduce_segments(ctx, L, bt, sr, wk, st, fused);
     // sum_d d * B_d = W(S) + T(S) per group (bucket b holds digit b + 1), level by level
     G1Xyzz* t_buf[2] = {wk.piece_sums.as<G1Xyzz>(), wk.piece_sums.as<G1Xyzz>() + (uint64_t)groups * (B / 2)};
     G1Xyzz* u_buf = wk.piece_sums2.as<G1Xyzz>();
@@ -1072,6 +1114,154 @@ static SortedBufs& wks_sorted(eon_ctx* ctx, size_t w) {
     return wks[w]->sorted;
 }
 
+// ---- host-side XYZZ -> affine for a call's few results ------------------------------------------
+// A device conversion of a handful of points is one thread's Fermat inversion: ~380 dependent
+// products, ~0.5 ms of latency per call (0.7 ms of a 2^20 MSM's 3.5).  The results travel to the
+// host anyway, so they are converted there: Montgomery batch inversion with 64-bit limbs (the same
+// R = 2^256 residues, so the bytes equal the device conversion's).
+namespace hostq {
+
+struct F {
+    uint64_t l[4];
+};
+
+static const F& P() {
+    static const F p = [] {
+        F r;
+        for (int i = 0; i < 4; i++) r.l[i] = (uint64_t)FqP::P[2 * i] | ((uint64_t)FqP::P[2 * i + 1] << 32);
+        return r;
+    }();
+    return p;
+}
+
+static uint64_t inv64() {
+    static const uint64_t v = [] {
+        uint64_t x = 1;
+        for (int i = 0; i < 6; i++) x *= 2 - P().l[0] * x;
+        return ~x + 1;
+    }();
+    return v;
+}
+
+static bool is_zero(const F& a) { return (a.l[0] | a.l[1] | a.l[2] | a.l[3]) == 0; }
+
+// a b 2^-256 mod p, canonical (CIOS)
+static F mul(const F& a, const F& b) {
+    const F& p = P();
+    const uint64_t inv = inv64();
+    uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 4; i++) {
+        unsigned __int128 c = 0;
+        for (int j = 0; j < 4; j++) {
+            c += (unsigned __int128)a.l[j] * b.l[i] + t[j];
+            t[j] = (uint64_t)c;
+            c >>= 64;
+        }
+        c += t[4];
+        t[4] = (uint64_t)c;
+        t[5] = (uint64_t)(c >> 64);
+        const uint64_t m = t[0] * inv;
+        c = (unsigned __int128)m * p.l[0] + t[0];
+        c >>= 64;
+        for (int j = 1; j < 4; j++) {
+            c += (unsigned __int128)m * p.l[j] + t[j];
+            t[j - 1] = (uint64_t)c;
+            c >>= 64;
+        }
+        c += t[4];
+        t[3] = (uint64_t)c;
+        t[4] = t[5] + (uint64_t)(c >> 64);
+    }
+    F r{{t[0], t[1], t[2], t[3]}}, d;
+    uint64_t borrow = 0;
+    for (int i = 0; i < 4; i++) {
+        const unsigned __int128 x = (unsigned __int128)t[i] - p.l[i] - borrow;
+        d.l[i] = (uint64_t)x;
+        borrow = (uint64_t)(x >> 64) & 1;
+    }
+    return (t[4] || !borrow) ? d : r;
+}
+
+// a^(p-2) (a != 0)
+static F inverse(const F& a) {
+    F e = P();
+    e.l[0] -= 2;  // p is odd and > 2: no borrow
+    F r = a, base = a;
+    bool first = true;
+    for (int w = 3; w >= 0; w--)
+        for (int bit = 63; bit >= 0; bit--) {
+            if (!first) r = mul(r, r);
+            if ((e.l[w] >> bit) & 1) {
+                if (first) {
+                    r = base;
+                    first = false;
+                } else {
+                    r = mul(r, base);
+                }
+            }
+        }
+    return r;
+}
+
+static F from_dev(const Fq& a) {
+    F r;
+    for (int i = 0; i < 4; i++) r.l[i] = (uint64_t)a.v[2 * i] | ((uint64_t)a.v[2 * i + 1] << 32);
+    return r;
+}
+
+static Fq to_dev(const F& a) {
+    Fq r;
+    for (int i = 0; i < 4; i++) {
+        r.v[2 * i] = (uint32_t)a.l[i];
+        r.v[2 * i + 1] = (uint32_t)(a.l[i] >> 32);
+    }
+    return r;
+}
+
+// out[i] = affine(in[i]) (x = X / ZZ, y = Y / ZZZ; the identity -> (0, 0))
+static void batch_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out) {
+    std::vector<F> pre(m);
+    F acc{{0, 0, 0, 0}};
+    bool any = false;
+    for (uint64_t i = 0; i < m; i++) {
+        pre[i] = acc;
+        const F zzz = from_dev(in[i].ZZZ);
+        if (is_zero(from_dev(in[i].ZZ))) continue;
+        acc = any ? mul(acc, zzz) : zzz;
+        any = true;
+    }
+    if (!any) {
+        for (uint64_t i = 0; i < m; i++) out[i] = G1Affine{Fq::zero(), Fq::zero()};
+        return;
+    }
+    F inv = inverse(acc);  // 1 / prod ZZZ over the non-identity points
+    for (uint64_t i = m; i-- > 0;) {
+        if (is_zero(from_dev(in[i].ZZ))) {
+            out[i] = G1Affine{Fq::zero(), Fq::zero()};
+            continue;
+        }
+        const F zzz = from_dev(in[i].ZZZ);
+        // pre[i] = product of the earlier non-identity ZZZ (zero when there is none)
+        const bool first_live = is_zero(pre[i]);
+        const F inv_zzz = first_live ? inv : mul(inv, pre[i]);
+        if (!first_live) inv = mul(inv, zzz);
+        const F inv_z = mul(from_dev(in[i].ZZ), inv_zzz);  // ZZ / ZZZ = 1 / Z
+        out[i].x = to_dev(mul(from_dev(in[i].X), mul(inv_z, inv_z)));
+        out[i].y = to_dev(mul(from_dev(in[i].Y), inv_zzz));
+    }
+}
+
+}  // namespace hostq
+
+// device XYZZ results -> affine on the host (synchronises `st`)
+static Status results_to_host_affine(const G1Xyzz* dev, uint64_t m, G1Affine* out_host, hipStream_t st) {
+    std::vector<G1Xyzz> h(m);
+    EON_HIP(hipMemcpyAsync(h.data(), dev, m * sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
+    EON_HIP(hipStreamSynchronize(st));
+    hostq::batch_to_affine(h.data(), m, out_host);
+    return Status::ok();
+}
+
 static Status identity_columns(uint32_t width, G1Affine* out_host) {
     // G1::multi_exp returns the identity for empty input (curve.rs:163-165)
     for (uint32_t j = 0; j < width; j++) {
@@ -1177,9 +1367,8 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
         keep->batches = batches;
         for (Batch& bt : keep->batches) bt.scalars = nullptr;
     }
-    EON_HIP(launch_batch_to_affine(res_xyzz, width, res, ctx->stream));
-    if (out_host)
-        EON_HIP(hipMemcpyAsync(out_host, res, width * sizeof(G1Affine), hipMemcpyDeviceToHost, ctx->stream));
+    (void)res;
+    if (out_host) return results_to_host_affine(res_xyzz, width, out_host, ctx->stream);
     EON_HIP(hipStreamSynchronize(ctx->stream));
     return Status::ok();
 }
@@ -1239,10 +1428,8 @@ Status msm_run_prepared(eon_ctx* ctx, const eon_msm_bases* const* bases, uint32_
         EON_HIP(hipEventRecord(ctx->msm_ev[1], comp[i]));
         EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[1], 0));
     }
-    EON_HIP(launch_batch_to_affine(res_xyzz, total, res, ctx->stream));
-    EON_HIP(hipMemcpyAsync(out_host, res, total * sizeof(G1Affine), hipMemcpyDeviceToHost, ctx->stream));
-    EON_HIP(hipStreamSynchronize(ctx->stream));
-    return Status::ok();
+    (void)res;
+    return results_to_host_affine(res_xyzz, total, out_host, ctx->stream);
 }
 
 Status msm_run(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, uint64_t n,

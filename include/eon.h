@@ -180,6 +180,12 @@ int eon_msm_g1_columns_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_f
 int eon_quotient_and_eval_columns_dev(eon_ctx* ctx, const eon_fr* coeffs, uint64_t rows,
                                       uint32_t width, const eon_fr* point, eon_fr* quotient,
                                       eon_fr* values);
+/* The remainder of quotient_and_eval (kzg/src/util.rs:100-111) only -- f_j(z) for every column
+ * of the rows x width coefficient matrix (device) at npoints points (host array): values
+ * (device) receives npoints x width Fr, values[t * width + j] = f_j(points[t]).  One read of the
+ * coefficients serves up to four points (KzgPcs::open's opened values, kzg/src/pcs.rs:305-316). */
+int eon_eval_columns_dev(eon_ctx* ctx, const eon_fr* coeffs, uint64_t rows, uint32_t width,
+                         const eon_fr* points, uint32_t npoints, eon_fr* values);
 /* As eon_msm_bases_create with `bases` a DEVICE pointer (coordinates are not re-validated). */
 int eon_msm_bases_create_dev(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32_t flags,
                              eon_msm_bases** out);

@@ -91,6 +91,7 @@ SIGNATURES = {
     "eon_msm_g1_columns": (_INT, [_P, _P, _P, _U64, _U32, _P]),
     "eon_msm_g1_columns_dev": (_INT, [_P, _P, _P, _U64, _U32, _P]),
     "eon_quotient_and_eval_columns_dev": (_INT, [_P, _P, _U64, _U32, _P, _P, _P]),
+    "eon_eval_columns_dev": (_INT, [_P, _P, _U64, _U32, _P, _U32, _P]),
     "eon_msm_g1_columns_prepare_dev": (_INT, [_P, _P, _P, _U64, _U32, _P, ctypes.POINTER(_P)]),
     "eon_msm_g1_columns_prepared": (_INT, [_P, _P, _U32, _P, _P]),
     "eon_msm_scalars_destroy": (None, [_P]),

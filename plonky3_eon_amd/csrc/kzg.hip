@@ -10,6 +10,8 @@
 // Two mulmods per coefficient; threads = (n / BL) x width, adjacent threads = adjacent columns.
 #include "context.h"
 
+#include <algorithm>
+
 using namespace eon;
 
 namespace {
@@ -72,9 +74,105 @@ __global__ void k_horner_apply(const Fr* c, uint64_t n, uint32_t width, Fr z, co
     }
 }
 
+// ---- values only, several points in one pass ------------------------------------------------------
+// f(z) = sum_b T_b Z^b with T_b the block totals above and Z = z^BL; the blocks' Horner chain is
+// split once more into chunks of CH blocks (P_q = sum over the chunk, then sum_q P_q (Z^CH)^q), so
+// no thread walks more than max(BL, CH, n / (BL CH)) steps; one read of the coefficients serves
+// every point.
+constexpr uint32_t CH = 32;
+constexpr uint32_t MAX_PTS = 4;
+struct Pts {
+    Fr z[MAX_PTS];
+};
+
+__global__ void k_eval_block(const Fr* c, uint64_t n, uint32_t width, Pts zs, uint32_t np, Fr* totals) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nblk = (n + BL - 1) / BL;
+    if (t >= nblk * width) return;
+    const uint32_t col = (uint32_t)(t % width);
+    const uint64_t b = t / width;
+    const uint64_t lo = b * BL, hi = lo + BL < n ? lo + BL : n;
+    Fr r[MAX_PTS];
+    for (uint32_t p = 0; p < MAX_PTS; p++) r[p] = Fr::zero();
+    for (uint64_t i = hi; i-- > lo;) {
+        const Fr x = ld(c + i * width + col);
+#pragma unroll
+        for (uint32_t p = 0; p < MAX_PTS; p++)
+            if (p < np) r[p] = add(x, mul(zs.z[p], r[p]));
+    }
+    for (uint32_t p = 0; p < np; p++) st(totals + ((uint64_t)p * nblk + b) * width + col, r[p]);
+}
+
+// per (point, chunk of CH blocks, column): P_q = sum_{b in chunk} T_b Z^(b - q CH)
+__global__ void k_eval_chunks(const Fr* totals, uint64_t nblk, uint32_t width, Pts zbl, uint32_t np, Fr* part) {
+    const uint64_t nq = (nblk + CH - 1) / CH;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)np * nq * width) return;
+    const uint32_t col = (uint32_t)(t % width);
+    const uint64_t q = (t / width) % nq;
+    const uint32_t p = (uint32_t)(t / (width * nq));
+    const uint64_t b0 = q * CH, b1 = b0 + CH < nblk ? b0 + CH : nblk;
+    Fr acc = Fr::zero();
+    for (uint64_t b = b1; b-- > b0;) acc = add(ld(totals + ((uint64_t)p * nblk + b) * width + col), mul(zbl.z[p], acc));
+    st(part + ((uint64_t)p * nq + q) * width + col, acc);
+}
+
+// per (point, column): f(z) = sum_q P_q (Z^CH)^q
+__global__ void k_eval_final(const Fr* part, uint64_t nq, uint32_t width, Pts zch, uint32_t np, Fr* values) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)np * width) return;
+    const uint32_t col = (uint32_t)(t % width), p = (uint32_t)(t / width);
+    Fr acc = Fr::zero();
+    for (uint64_t q = nq; q-- > 0;) acc = add(ld(part + ((uint64_t)p * nq + q) * width + col), mul(zch.z[p], acc));
+    st(values + (uint64_t)p * width + col, acc);
+}
+
 }  // namespace
 
 extern "C" {
+
+int eon_eval_columns_dev(eon_ctx* ctx, const eon_fr* coeffs, uint64_t rows, uint32_t width, const eon_fr* points,
+                         uint32_t npoints, eon_fr* values) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    Status s = [&]() -> Status {
+        if ((npoints && !points) || (width && npoints && !values)) return Status::err(EON_E_ARG, "null argument");
+        if (width == 0 || npoints == 0) return Status::ok();
+        if (rows == 0) {  // empty column: (empty quotient, 0) (kzg/src/util.rs:101-103)
+            EON_HIP(hipMemsetAsync(values, 0, (size_t)npoints * width * sizeof(Fr), ctx->stream));
+            return Status::ok();
+        }
+        if (!coeffs) return Status::err(EON_E_ARG, "null argument");
+        const uint64_t nblk = (rows + BL - 1) / BL, nq = (nblk + CH - 1) / CH;
+        EON_HIP(ctx->kzg_tmp.ensure((uint64_t)MAX_PTS * (nblk + nq) * width * sizeof(Fr)));
+        Fr* totals = ctx->kzg_tmp.as<Fr>();
+        Fr* part = totals + (uint64_t)MAX_PTS * nblk * width;
+        const Fr* c = reinterpret_cast<const Fr*>(coeffs);
+        for (uint32_t p0 = 0; p0 < npoints; p0 += MAX_PTS) {
+            const uint32_t np = std::min<uint32_t>(MAX_PTS, npoints - p0);
+            Pts zs{}, zbl{}, zch{};
+            for (uint32_t p = 0; p < np; p++) {
+                zs.z[p] = fr_from_abi(points + p0 + p);
+                if (!fr_is_canonical(zs.z[p])) return Status::err(EON_E_ARG, "point is not a canonical Fr");
+                zbl.z[p] = pow_u64(zs.z[p], BL);
+                zch.z[p] = pow_u64(zbl.z[p], CH);
+            }
+            ctx->prof.begin("k_horner_block", rows * width * 32ull, ctx->stream);
+            hipLaunchKernelGGL(k_eval_block, dim3((unsigned)((nblk * width + 127) / 128)), dim3(128), 0, ctx->stream,
+                               c, rows, width, zs, np, totals);
+            ctx->prof.end(ctx->stream);
+            hipLaunchKernelGGL(k_eval_chunks, dim3((unsigned)((np * nq * width + 127) / 128)), dim3(128), 0,
+                               ctx->stream, totals, nblk, width, zbl, np, part);
+            hipLaunchKernelGGL(k_eval_final, dim3((unsigned)((np * width + 63) / 64)), dim3(64), 0, ctx->stream, part,
+                               nq, width, zch, np, reinterpret_cast<Fr*>(values) + (uint64_t)p0 * width);
+            EON_HIP(hipGetLastError());
+        }
+        return Status::ok();
+    }();
+    if (s.bad()) ctx->last_error = s.msg;
+    return s.code;
+}
 
 int eon_quotient_and_eval_columns_dev(eon_ctx* ctx, const eon_fr* coeffs, uint64_t rows,
                                       uint32_t width, const eon_fr* point, eon_fr* quotient,

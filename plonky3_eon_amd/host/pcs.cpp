@@ -314,13 +314,12 @@ std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
             out[r].values[m].resize(pts.size());
             out[r].witnesses[m].resize(pts.size());
             DeviceBuffer vals(std::max<uint64_t>(pts.size() * w, 1) * sizeof(eon_fr));
-            for (size_t p = 0; p < pts.size(); p++) {
-                const eon_fr z = pts[p].abi();
-                check(ctx_,
-                      eon_quotient_and_eval_columns_dev(ctx_, md.coeffs.data(), md.coeffs.height, w, &z, nullptr,
-                                                        vals.as<eon_fr>() + p * w),
-                      "opened values");
-            }
+            std::vector<eon_fr> zs(pts.size());
+            for (size_t p = 0; p < pts.size(); p++) zs[p] = pts[p].abi();
+            check(ctx_,
+                  eon_eval_columns_dev(ctx_, md.coeffs.data(), md.coeffs.height, w, zs.data(), (uint32_t)zs.size(),
+                                       vals.as<eon_fr>()),
+                  "opened values");
             std::vector<eon_fr> hv(pts.size() * w);
             hip_check(hipMemcpyAsync(hv.data(), vals.get(), hv.size() * sizeof(eon_fr), hipMemcpyDeviceToHost, st),
                       "opened values");

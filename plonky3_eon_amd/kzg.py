@@ -173,15 +173,17 @@ class GpuKzgPcs:
                        witnesses=[[None] * len(p) for p in points_per_matrix])
             for mi, (m, points) in enumerate(zip(prover_data, points_per_matrix)):
                 n, w = int(m.coeffs.shape[0]), int(m.coeffs.shape[1])
+                # every point's values in one pass over the coefficients (eon_eval_columns_dev)
+                v = torch.empty((max(len(points), 1), w, 4), dtype=torch.int64, device=m.coeffs.device)
+                zs = (_lib.eon_fr * max(len(points), 1))(*[fr_to_abi(z) for z in points])
+                self.ctx.set_stream(torch.cuda.current_stream(m.coeffs.device).cuda_stream)
+                self.ctx.check(self.ctx.lib.eon_eval_columns_dev(
+                    self.ctx.handle, ctypes.c_void_p(m.coeffs.data_ptr()), n, w, zs, len(points),
+                    ctypes.c_void_p(v.data_ptr())))
+                vh = v.cpu().numpy().view(np.uint64)
                 hb = []
                 for pi, z in enumerate(points):
-                    v = torch.empty((w, 4), dtype=torch.int64, device=m.coeffs.device)
-                    pz = fr_to_abi(z)
-                    self.ctx.set_stream(torch.cuda.current_stream(m.coeffs.device).cuda_stream)
-                    self.ctx.check(self.ctx.lib.eon_quotient_and_eval_columns_dev(
-                        self.ctx.handle, ctypes.c_void_p(m.coeffs.data_ptr()), n, w, ctypes.byref(pz), None,
-                        ctypes.c_void_p(v.data_ptr())))
-                    o.values[mi][pi] = v.cpu().numpy().view(np.uint64)
+                    o.values[mi][pi] = vh[pi]
                     hb.append(bases_at[(n, z)])
                 wits = m.prepared.msm(hb)
                 for pi in range(len(points)):

@@ -60,3 +60,29 @@ def test_opening_bases_edge_cases(gpu_ctx):
     plain = MsmBases(pts, gpu_ctx, precompute=False)
     with pytest.raises(EonError):
         prep.msm([plain])
+
+
+@pytest.mark.parametrize("rows,width,npts", [(1, 3, 1), (255, 2, 5), (257, 4, 4), (256 * 32 + 5, 3, 6),
+                                             (256 * 32 * 3, 2, 2)])
+def test_eval_columns_multi_point(gpu_ctx, rows, width, npts):
+    """eon_eval_columns_dev (every point's f_j(z) in one pass, block/chunk carries) against the
+    oracle's quotient_and_eval values, ragged heights and more points than one pass holds."""
+    import ctypes
+
+    import torch
+
+    from plonky3_eon_amd import _lib
+    from plonky3_eon_amd.kzg import fr_to_abi
+
+    coeffs = C.random_fr(rows + npts, rows * width).reshape(rows, width, 4)
+    points = [C.fr_from_u64(0)] + list(C.random_fr(rows + 7, npts - 1)) if npts > 1 else [C.fr_from_u64(5)]
+    out = torch.zeros((npts, width, 4), dtype=torch.int64, device="cuda:0")
+    zs = (_lib.eon_fr * npts)(*[fr_to_abi(z) for z in points])
+    gpu_ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    gpu_ctx.check(gpu_ctx.lib.eon_eval_columns_dev(gpu_ctx.handle, ctypes.c_void_p(_dev(coeffs).data_ptr()), rows,
+                                                   width, zs, npts, ctypes.c_void_p(out.data_ptr())))
+    got = out.cpu().numpy().view(np.uint64)
+    for t, z in enumerate(points):
+        for j in range(width):
+            _, v = C.quotient_and_eval(coeffs[:, j], z)
+            np.testing.assert_array_equal(got[t, j], v, err_msg=f"point {t} column {j}")

@@ -573,6 +573,13 @@ def main() -> int:
             "peak_mulmod_per_s": MULMOD_PEAK_PER_S,
             "frac": round(rate / MULMOD_PEAK_PER_S, 4),
         }
+        if kst.get("busy_ms"):
+            # launches of this kernel overlap on several streams (the MSM pipeline): the rate over
+            # the union of their intervals is what the chip sustained for it
+            rb = kmm / (kst["busy_ms"] * 1e-3)
+            roof["valu"]["busy_ms_per_step"] = round(kst["busy_ms"] / prof_steps, 3)
+            roof["valu"]["achieved_mulmod_per_s_busy"] = round(rb, 1)
+            roof["valu"]["frac_busy"] = round(rb / MULMOD_PEAK_PER_S, 4)
     if mulmods is not None:
         roof["valu_whole_step"] = {
             "achieved_mulmod_per_s": round(mulmods / (gpu_total_ms * 1e-3), 1),

@@ -8,8 +8,11 @@
  *                    commit_quotient / open of the Pcs trait (commit/src/pcs.rs:21-187)
  *   eon_prove_p2air  prove_with_preprocessed (eon-uni-stark/src/prover.rs:28-512) for the
  *                    Poseidon2-AIR: no preprocessed columns, no lookups,
- *                    ZK off, Challenge = Fr.  alpha and zeta are inputs (the DuplexChallenger
- *                    transcript is SURVEY.md 8(f) N2, not built).
+ *                    ZK off, Challenge = Fr.  alpha and zeta are either inputs
+ *                    (eon_prove_p2air) or sampled from the Fiat-Shamir transcript
+ *                    (eon_prove_p2air_fs with an eon_challenger).
+ *   eon_challenger   DuplexChallenger<Fr, Poseidon2Bn254<3>, 3, 2>
+ *                    (challenger/src/duplex_challenger.rs, bn254/src/poseidon2.rs) on the host.
  * Conventions are eon.h's: 0 / negative EON_E_* codes (the reference panics), host outputs,
  * device inputs, work on the context's stream.
  */
@@ -73,6 +76,39 @@ typedef struct {
 int eon_prove_p2air(eon_kzg_pcs* pcs, const eon_p2air* air, const eon_fr* trace, uint64_t height,
                     const eon_fr* alpha, const eon_fr* zeta, uint32_t max_constraint_degree,
                     const eon_collective* shard, eon_proof* out);
+
+/* ---- Fiat-Shamir transcript, host only ---------------------------------
+ * Poseidon2Bn254<3>::permute_mut (poseidon2/src/lib.rs:107-111) of state[3] in place, with the
+ * round constants of `perm` (the AIR's constant layout; the reference draws them with
+ * Poseidon2::new_from_rng(2 * half_full_rounds, partial_rounds), lib.rs:66-74). */
+int eon_poseidon2_bn254_permute(const eon_poseidon2_constants* perm, eon_fr state[3]);
+/* G1Affine::to_bytes, the 32-byte compressed form KzgCommitment observation reads
+ * (kzg/src/pcs.rs:417-436): canonical x little-endian, bit 7 of byte 31 = y odd, bit 6 =
+ * identity.  halo2curves' encoding, absent here: parity unpinned. */
+int eon_g1_to_bytes(const eon_g1_affine* point, uint8_t out[32]);
+
+typedef struct eon_challenger eon_challenger;
+/* DuplexChallenger::new(Poseidon2Bn254<3>) (duplex_challenger.rs:68-78): zero sponge state */
+int eon_challenger_create(const eon_poseidon2_constants* perm, eon_challenger** out);
+void eon_challenger_destroy(eon_challenger* ch);
+/* observe(Fr) for each of values[0..n) (duplex_challenger.rs:111-121) */
+int eon_challenger_observe(eon_challenger* ch, const eon_fr* values, uint64_t n);
+/* observe(KzgCommitment) for one matrix's n column commitments (kzg/src/pcs.rs:417-436) */
+int eon_challenger_observe_g1(eon_challenger* ch, const eon_g1_affine* points, uint64_t n);
+/* sample() -> Fr = sample_algebra_element for Challenge = Fr (duplex_challenger.rs:185-200) */
+int eon_challenger_sample(eon_challenger* ch, eon_fr* out);
+/* the sponge state (3 Fr), for tests */
+int eon_challenger_state(const eon_challenger* ch, eon_fr out[3]);
+
+/* prove with the transcript of prove_with_preprocessed: observe log_ext_degree, log_degree, the
+ * preprocessed width (0) and the trace commitment (prover.rs:196-202), sample alpha (:300),
+ * observe the quotient commitment (:373), sample zeta (:416).  `challenger` is the config's
+ * initialised challenger and is advanced as the reference's; alpha_out / zeta_out (host,
+ * nullable) receive the sampled challenges.  Sharded: the trace commitments are all-gathered
+ * before alpha so every rank observes the full transcript. */
+int eon_prove_p2air_fs(eon_kzg_pcs* pcs, const eon_p2air* air, const eon_fr* trace, uint64_t height,
+                       eon_challenger* challenger, uint32_t max_constraint_degree,
+                       const eon_collective* shard, eon_proof* out, eon_fr* alpha_out, eon_fr* zeta_out);
 
 uint32_t eon_prove_abi_version(void);
 

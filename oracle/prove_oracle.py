@@ -5,7 +5,9 @@ Follows prove_with_preprocessed (eon-uni-stark/src/prover.rs:28-534) with the re
 algorithms where they differ from the GPU path: get_evaluations_on_domain is the Horner loop of
 kzg/src/pcs.rs:267-287, openings run quotient_and_eval per column (kzg/src/util.rs:100-111),
 every commitment is commit_column = G1::multi_exp (kzg/src/util.rs:37-40).  alpha and zeta are
-inputs (the Fiat-Shamir transcript is out of scope, see plonky3_eon_amd/prover.py).
+inputs, or, with a pyoracle.DuplexChallenger, sampled from the transcript as prover.rs:196-208,
+300, 373, 416 (observe log_ext_degree, log_degree, preprocessed width 0, the trace commitment;
+alpha; observe the quotient commitment; zeta).
 """
 
 import numpy as np
@@ -18,12 +20,21 @@ def _lim(x):
     return np.array(O.int_to_limbs(O.to_mont(x % O.P)), dtype=np.uint64)
 
 
-def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1):
+def _points(abi_rows):
+    return [O.g1_from_bytes(np.ascontiguousarray(r, dtype=np.uint64).tobytes()) for r in abi_rows]
+
+
+def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1, challenger=None):
     n, w = trace.shape[0], trace.shape[1]
     log_n = n.bit_length() - 1
-    alpha = _lim(alpha_int)
     coeffs = C.idft_batch(trace)  # coset_idft_batch(evals, shift 1) (kzg/src/pcs.rs:242)
     trace_commit = np.stack([C.g1_msm(srs[:n], coeffs[:, j]) for j in range(w)])
+    if challenger is not None:
+        for v in (log_n, log_n, 0):
+            challenger.observe(v)
+        challenger.observe_g1(_points(trace_commit))
+        alpha_int = challenger.sample()
+    alpha = _lim(alpha_int)
     lde = C.kzg_evaluations_on_domain(coeffs, log_n + log_qd, _lim(O.GENERATOR))
     qv = C.p2_quotient_values(lde, log_n, log_qd, vl, consts, alpha)
     chunks = 1 << log_qd
@@ -35,6 +46,9 @@ def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1):
         cc = C.coset_idft_batch(ev, _lim(shift))
         q_coeffs.append(cc)
         quotient_commit.append(C.g1_msm(srs[:n], cc[:, 0]))
+    if challenger is not None:
+        challenger.observe_g1(_points(quotient_commit))
+        zeta_int = challenger.sample()
     zeta_next = zeta_int * O.two_adic_generator(log_n) % O.P
 
     def open_matrix(cf, points):
@@ -57,4 +71,6 @@ def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1):
         "trace_open": trace_open,
         "quotient_open": quot_open,
         "quotient_values": qv,
+        "alpha": alpha_int,
+        "zeta": zeta_int,
     }

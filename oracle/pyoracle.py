@@ -469,3 +469,67 @@ def p2_quotient_values(lde_rows, log_n, log_qd, vl, consts, alpha):
         acc = sum(pow(alpha, K - 1 - k, P) * c for k, c in enumerate(cs)) % P
         out.append(acc * inv_van[i] % P)
     return out
+
+
+# --- Fiat-Shamir transcript -------------------------------------------------
+def p2_permute(state, consts):
+    """Poseidon2Bn254<3>::permute_mut (poseidon2/src/lib.rs:107-111): mds_light, the initial full
+    rounds, the partial rounds (internal matrix), the terminal full rounds; x^5 S-box."""
+    begin, partial, end = consts
+    s = p2_ext([x % P for x in state])
+    for rc in begin:
+        s = p2_ext([pow((s[i] + rc[i]) % P, 5, P) for i in range(3)])
+    for rc in partial:
+        s[0] = pow((s[0] + rc) % P, 5, P)
+        s = p2_int(s)
+    for rc in end:
+        s = p2_ext([pow((s[i] + rc[i]) % P, 5, P) for i in range(3)])
+    return s
+
+
+class DuplexChallenger:
+    """DuplexChallenger<Fr, Poseidon2Bn254<3>, 3, 2> (challenger/src/duplex_challenger.rs:62-200),
+    canonical ints."""
+
+    RATE = 2
+
+    def __init__(self, consts):
+        self.consts = consts
+        self.state = [0, 0, 0]
+        self.inp, self.out = [], []
+
+    def _duplex(self):
+        for i, v in enumerate(self.inp):
+            self.state[i] = v
+        self.inp = []
+        self.state = p2_permute(self.state, self.consts)
+        self.out = self.state[: self.RATE]
+
+    def observe(self, v: int):
+        self.out = []
+        self.inp.append(v % P)
+        if len(self.inp) == self.RATE:
+            self._duplex()
+
+    def sample(self) -> int:
+        if self.inp or not self.out:
+            self._duplex()
+        return self.out.pop()
+
+    def observe_g1(self, points):
+        """CanObserve<KzgCommitment> (kzg/src/pcs.rs:417-436): compressed bytes, 8-byte LE chunks."""
+        for p in points:
+            b = g1_compressed(p)
+            for c in range(4):
+                self.observe(int.from_bytes(b[8 * c: 8 * c + 8], "little"))
+
+
+def g1_compressed(p) -> bytes:
+    """G1Affine::to_bytes as halo2curves (absent; parity unpinned): canonical x LE, bit 7 of byte
+    31 = y odd, bit 6 = identity."""
+    if p is INF:
+        return bytes(31) + b"\x40"
+    b = bytearray(p[0].to_bytes(32, "little"))
+    if p[1] & 1:
+        b[31] |= 0x80
+    return bytes(b)

@@ -18,6 +18,8 @@
 #include <vector>
 
 #include "context.h"
+
+#include <algorithm>
 #include "ntt.h"
 
 using namespace eon;
@@ -422,29 +424,50 @@ int eon_ctx_profile_report(eon_ctx* ctx, char* buf, uint64_t len) {
     if (!ctx || !buf || len == 0) return EON_E_ARG;
     std::lock_guard<std::mutex> lk(ctx->mu);
     (void)hipSetDevice(ctx->device);
+    // busy_ms: the union of a kernel's launch intervals (launches on several streams overlap, so
+    // total_ms / launches overstates what one launch would take alone)
     struct Agg {
         uint64_t n = 0, bytes = 0, mulmods = 0;
         double ms = 0;
+        std::vector<std::pair<double, double>> iv;
     };
     std::map<std::string, Agg> agg;
+    hipEvent_t t0 = ctx->prof.recs.empty() ? nullptr : ctx->prof.recs.front().start;
     for (auto& r : ctx->prof.recs) {
         if (hipEventSynchronize(r.stop) != hipSuccess) continue;
-        float ms = 0;
+        float ms = 0, a0 = 0, a1 = 0;
         if (hipEventElapsedTime(&ms, r.start, r.stop) != hipSuccess) continue;
         Agg& a = agg[r.kernel];
         a.n++;
         a.ms += ms;
         a.bytes += r.alg_bytes;
         a.mulmods += r.alg_mulmods;
+        if (hipEventElapsedTime(&a0, t0, r.start) == hipSuccess && hipEventElapsedTime(&a1, t0, r.stop) == hipSuccess)
+            a.iv.emplace_back(a0, a1);
     }
+    auto busy = [](std::vector<std::pair<double, double>> iv) {
+        std::sort(iv.begin(), iv.end());
+        double tot = 0, s = 0, e = -1e300;
+        for (auto& x : iv) {
+            if (x.first > e) {
+                if (e > s) tot += e - s;
+                s = x.first;
+                e = x.second;
+            } else if (x.second > e) {
+                e = x.second;
+            }
+        }
+        if (e > s) tot += e - s;
+        return tot;
+    };
     std::string out = "{";
     char tmp[256];
     for (auto& kv : agg) {
         snprintf(tmp, sizeof tmp,
-                 "%s\"%s\": {\"launches\": %llu, \"total_ms\": %.6f, \"alg_bytes\": %llu, "
-                 "\"alg_mulmods\": %llu}",
+                 "%s\"%s\": {\"launches\": %llu, \"total_ms\": %.6f, \"busy_ms\": %.6f, "
+                 "\"alg_bytes\": %llu, \"alg_mulmods\": %llu}",
                  out.size() > 1 ? ", " : "", kv.first.c_str(), (unsigned long long)kv.second.n,
-                 kv.second.ms, (unsigned long long)kv.second.bytes,
+                 kv.second.ms, busy(kv.second.iv), (unsigned long long)kv.second.bytes,
                  (unsigned long long)kv.second.mulmods);
         out += tmp;
     }

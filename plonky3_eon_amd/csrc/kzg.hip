@@ -158,7 +158,7 @@ int eon_eval_columns_dev(eon_ctx* ctx, const eon_fr* coeffs, uint64_t rows, uint
                 zbl.z[p] = pow_u64(zs.z[p], BL);
                 zch.z[p] = pow_u64(zbl.z[p], CH);
             }
-            ctx->prof.begin("k_horner_block", rows * width * 32ull, ctx->stream);
+            ctx->prof.begin("k_eval_block", rows * width * 32ull, ctx->stream);
             hipLaunchKernelGGL(k_eval_block, dim3((unsigned)((nblk * width + 127) / 128)), dim3(128), 0, ctx->stream,
                                c, rows, width, zs, np, totals);
             ctx->prof.end(ctx->stream);

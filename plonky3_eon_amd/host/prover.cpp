@@ -45,8 +45,9 @@ void hip_ok(hipError_t e, const char* what) {
 
 }  // namespace
 
-Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t height, const Fr& alpha,
-            const Fr& zeta, uint32_t max_constraint_degree, const eon_collective* shard) {
+Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t height, const Fr& alpha_in,
+            const Fr& zeta_in, uint32_t max_constraint_degree, const eon_collective* shard,
+            DuplexChallenger* challenger) {
     eon_ctx* ctx = pcs.ctx();
     using clock = std::chrono::steady_clock;
     auto tick = [&] {
@@ -118,8 +119,42 @@ Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t hei
     } else {
         pcs.commit_columns(trace_data, 0, trace_commit);
         t1 = tick();
-        lde = pcs.get_evaluations_on_domain(trace_data, 0, quotient_domain);
     }
+    // Fiat-Shamir up to alpha (prover.rs:196-208, 300) on a host thread while the device extends
+    // the trace: sharded, every rank observes the full commitment (all-gathered in rank = lane
+    // order first)
+    Fr alpha = alpha_in;
+    std::thread fs_thread;
+    std::vector<eon_g1_affine> full_commit;
+    if (challenger) {
+        if (shard) {
+            const uint64_t bytes = (uint64_t)width * sizeof(eon_g1_affine);
+            DeviceBuffer send(bytes), recv(bytes * world);
+            hip_ok(hipMemcpyAsync(send.get(), trace_commit[0].data(), bytes, hipMemcpyHostToDevice, st), "commit");
+            all_gather(ctx, shard, send.get(), recv.get(), bytes);
+            full_commit.resize((uint64_t)width * world);
+            hip_ok(hipMemcpyAsync(full_commit.data(), recv.get(), bytes * world, hipMemcpyDeviceToHost, st), "commit");
+            hip_ok(hipStreamSynchronize(st), "commit");
+        } else {
+            full_commit = trace_commit[0];
+        }
+        fs_thread = std::thread([&] {
+            challenger->observe(fr_from_u64(log_n));  // log_ext_degree (ZK off)
+            challenger->observe(fr_from_u64(log_n));  // log_degree
+            challenger->observe(fr_from_u64(0));      // preprocessed width
+            challenger->observe_g1(full_commit.data(), full_commit.size());
+            alpha = challenger->sample();  // no public values, no lookups
+        });
+    }
+    if (!(overlap && pcs.aux_ctx())) {
+        try {
+            lde = pcs.get_evaluations_on_domain(trace_data, 0, quotient_domain);
+        } catch (...) {
+            if (fs_thread.joinable()) fs_thread.join();
+            throw;
+        }
+    }
+    if (fs_thread.joinable()) fs_thread.join();
     DeviceMatrix qv = DeviceMatrix::alloc(q_rows, 1);
     {
         t2 = tick();
@@ -144,6 +179,13 @@ Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t hei
     std::vector<std::vector<eon_g1_affine>> quotient_commit;
     std::vector<MatrixProverData> quotient_data;
     pcs.commit_quotient(quotient_domain, qv, num_chunks, quotient_commit, quotient_data);  // :371-372
+    Fr zeta = zeta_in;
+    if (challenger) {
+        for (const auto& m : quotient_commit) challenger->observe_g1(m.data(), m.size());  // :373
+        zeta = challenger->sample();                                                       // :416
+    }
+    proof.alpha = alpha;
+    proof.zeta = zeta;
     auto t4 = tick();
     const Fr zeta_next = trace_domain.next_point(zeta);  // prover.rs:416-419
     std::vector<OpenRound> rounds(2);

@@ -1,10 +1,11 @@
 // prove_with_preprocessed (eon-uni-stark/src/prover.rs:28-512) for the Poseidon2-AIR over KzgPcs,
 // as a C++ driver above eon.h.  Specialised to what the benchmark AIR exercises:
 // no preprocessed columns, no lookups, ZK off (KzgPcs::ZK = false, kzg/src/pcs.rs:216),
-// Challenge = Fr; alpha and zeta are inputs (transcript: SURVEY.md 8(f) N2).
+// Challenge = Fr; alpha and zeta are inputs or sampled from a DuplexChallenger.
 #pragma once
 #include "eon_prove.h"
 #include "pcs.h"
+#include "transcript.h"
 
 namespace eon_host {
 
@@ -20,11 +21,14 @@ struct Proof {
     std::vector<eon_g1_affine> quotient_witnesses;  // [C]
     uint32_t degree_bits = 0;
     double stage_ms[EON_STAGES] = {};
+    Fr alpha, zeta;  // the challenges used
 };
 
 // `trace`: this rank's height x width(air) device trace.  With `shard` (world > 1) the AIR is the
-// rank's lane range; every rank returns the full proof.
+// rank's lane range; every rank returns the full proof.  With `challenger`, alpha and zeta are
+// sampled from it (prover.rs:196-208, 300, 373, 416) and the inputs are ignored.
 Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t height, const Fr& alpha,
-            const Fr& zeta, uint32_t max_constraint_degree, const eon_collective* shard);
+            const Fr& zeta, uint32_t max_constraint_degree, const eon_collective* shard,
+            DuplexChallenger* challenger = nullptr);
 
 }  // namespace eon_host

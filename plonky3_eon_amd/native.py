@@ -21,7 +21,7 @@ import numpy as np
 
 from . import _lib
 from .dft import Context, default_context
-from .field import fr_to_abi
+from .field import fr_to_abi, fr_unmont
 from .kzg import Opened
 from .prover import Proof, log_quotient_degree
 
@@ -60,6 +60,16 @@ SIGNATURES = {
     "eon_rccl_collective_finalize": (None, [ctypes.POINTER(eon_collective)]),
     "eon_prove_p2air": (_INT, [_P, _P, _P, _U64, _P, _P, _U32, ctypes.POINTER(eon_collective),
                                ctypes.POINTER(eon_proof)]),
+    "eon_poseidon2_bn254_permute": (_INT, [_P, _P]),
+    "eon_g1_to_bytes": (_INT, [_P, _P]),
+    "eon_challenger_create": (_INT, [_P, ctypes.POINTER(_P)]),
+    "eon_challenger_destroy": (None, [_P]),
+    "eon_challenger_observe": (_INT, [_P, _P, _U64]),
+    "eon_challenger_observe_g1": (_INT, [_P, _P, _U64]),
+    "eon_challenger_sample": (_INT, [_P, _P]),
+    "eon_challenger_state": (_INT, [_P, _P]),
+    "eon_prove_p2air_fs": (_INT, [_P, _P, _P, _U64, _P, _U32, ctypes.POINTER(eon_collective),
+                                  ctypes.POINTER(eon_proof), _P, _P]),
 }
 
 _plib = None
@@ -185,10 +195,90 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def prove_native(air, pcs: NativeKzgPcs, trace, alpha: int, zeta: int, max_constraint_degree: int = 3,
-                 collective=None) -> Proof:
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise _lib.EonError(rc, what)
+
+
+class Poseidon2Constants:
+    """eon_poseidon2_constants over host arrays, the layout Poseidon2Air takes: begin/end
+    (half_full_rounds, 3, 4) and partial (partial_rounds, 4) Montgomery u64 limbs."""
+
+    def __init__(self, begin, partial, end):
+        self.begin = np.ascontiguousarray(begin, dtype=np.uint64).reshape(-1, 3, 4)
+        self.partial = np.ascontiguousarray(partial, dtype=np.uint64).reshape(-1, 4)
+        self.end = np.ascontiguousarray(end, dtype=np.uint64).reshape(-1, 3, 4)
+        self.c = _lib.eon_poseidon2_constants(self.begin.shape[0], self.partial.shape[0], _p(self.begin),
+                                              _p(self.partial), _p(self.end))
+
+
+def poseidon2_permute(consts: Poseidon2Constants, state) -> np.ndarray:
+    """eon_poseidon2_bn254_permute: state = 3 Montgomery Fr (3, 4) u64."""
+    s = np.ascontiguousarray(np.asarray(state, dtype=np.uint64).reshape(3, 4)).copy()
+    _check(load().eon_poseidon2_bn254_permute(ctypes.byref(consts.c), _p(s)), "eon_poseidon2_bn254_permute")
+    return s
+
+
+def g1_to_bytes(point) -> bytes:
+    """eon_g1_to_bytes of one eon_g1_affine (8 u64: x, y Fq Montgomery)."""
+    p = np.ascontiguousarray(np.asarray(point, dtype=np.uint64).reshape(8))
+    out = (ctypes.c_uint8 * 32)()
+    _check(load().eon_g1_to_bytes(_p(p), out), "eon_g1_to_bytes")
+    return bytes(out)
+
+
+class Challenger:
+    """DuplexChallenger<Fr, Poseidon2Bn254<3>, 3, 2> of libeonprove (eon_challenger_*)."""
+
+    def __init__(self, consts: Poseidon2Constants):
+        self.lib = load()
+        self.consts = consts  # the C side copies them; kept for symmetry with the AIR
+        h = _P()
+        _check(self.lib.eon_challenger_create(ctypes.byref(consts.c), ctypes.byref(h)), "eon_challenger_create")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def observe(self, values):
+        """Montgomery Fr limbs (..., 4)"""
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.uint64).reshape(-1, 4))
+        _check(self.lib.eon_challenger_observe(self._h, _p(v), v.shape[0]), "eon_challenger_observe")
+
+    def observe_g1(self, points):
+        """eon_g1_affine rows (..., 8)"""
+        v = np.ascontiguousarray(np.asarray(points, dtype=np.uint64).reshape(-1, 8))
+        _check(self.lib.eon_challenger_observe_g1(self._h, _p(v), v.shape[0]), "eon_challenger_observe_g1")
+
+    def sample(self) -> np.ndarray:
+        out = np.zeros(4, np.uint64)
+        _check(self.lib.eon_challenger_sample(self._h, _p(out)), "eon_challenger_sample")
+        return out
+
+    def state(self) -> np.ndarray:
+        out = np.zeros((3, 4), np.uint64)
+        _check(self.lib.eon_challenger_state(self._h, _p(out)), "eon_challenger_state")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.eon_challenger_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def prove_native(air, pcs: NativeKzgPcs, trace, alpha: int | None, zeta: int | None,
+                 max_constraint_degree: int = 3, collective=None, challenger: Challenger | None = None) -> Proof:
     """prover.prove through the C++ driver.  `trace`: (N, width, 4) device tensor; with a
-    collective (world > 1) `air`/`trace` are this rank's lanes and the proof is the full one."""
+    collective (world > 1) `air`/`trace` are this rank's lanes and the proof is the full one.
+    With `challenger` (eon_prove_p2air_fs) alpha and zeta are sampled from the transcript and
+    returned in proof.alpha / proof.zeta (canonical ints); the arguments are ignored."""
     world = collective.c.world if collective is not None else 1
     w = air.width * world
     chunks = 1 << log_quotient_degree(max_constraint_degree)
@@ -199,20 +289,29 @@ def prove_native(air, pcs: NativeKzgPcs, trace, alpha: int, zeta: int, max_const
     qo = np.zeros((chunks, 4), np.uint64)
     qw = np.zeros((chunks, 8), np.uint64)
     out = eon_proof(_p(tc), _p(qc), _p(to), _p(tw), _p(qo), _p(qw), 0)
-    a, z = fr_to_abi(alpha), fr_to_abi(zeta)
     t = trace.contiguous()
     import torch
 
     torch.cuda.synchronize(t.device)  # the trace was produced on torch's stream
     pcs.ctx.set_stream(None)
     coll = ctypes.byref(collective.c) if collective is not None else None
-    pcs.check(pcs.lib.eon_prove_p2air(pcs._h, air.handle, ctypes.c_void_p(t.data_ptr()), int(t.shape[0]),
-                                      ctypes.byref(a), ctypes.byref(z), max_constraint_degree, coll,
-                                      ctypes.byref(out)))
+    if challenger is None:
+        a, z = fr_to_abi(alpha), fr_to_abi(zeta)
+        pcs.check(pcs.lib.eon_prove_p2air(pcs._h, air.handle, ctypes.c_void_p(t.data_ptr()), int(t.shape[0]),
+                                          ctypes.byref(a), ctypes.byref(z), max_constraint_degree, coll,
+                                          ctypes.byref(out)))
+    else:
+        a_out, z_out = np.zeros(4, np.uint64), np.zeros(4, np.uint64)
+        pcs.check(pcs.lib.eon_prove_p2air_fs(pcs._h, air.handle, ctypes.c_void_p(t.data_ptr()), int(t.shape[0]),
+                                             challenger.handle, max_constraint_degree, coll, ctypes.byref(out),
+                                             _p(a_out), _p(z_out)))
+        alpha = fr_unmont(sum(int(v) << (64 * i) for i, v in enumerate(a_out)))
+        zeta = fr_unmont(sum(int(v) << (64 * i) for i, v in enumerate(z_out)))
     opened_trace = Opened(values=[[to[0], to[1]]], witnesses=[[tw[0], tw[1]]])
     opened_quot = Opened(values=[[qo[c:c + 1]] for c in range(chunks)], witnesses=[[qw[c:c + 1]] for c in range(chunks)])
     timings = {name: out.stage_ms[i] for i, name in enumerate(STAGES)}
     if collective is None:
         timings.pop("exchange partial quotients")
         timings.pop("assemble columns")
-    return Proof([tc], [qc[c:c + 1] for c in range(chunks)], [opened_trace, opened_quot], out.degree_bits, timings)
+    return Proof([tc], [qc[c:c + 1] for c in range(chunks)], [opened_trace, opened_quot], out.degree_bits, timings,
+                 alpha, zeta)

@@ -18,7 +18,9 @@ from __future__ import annotations
 import time
 from dataclasses import dataclass, field
 
-from .field import FR_MODULUS
+import numpy as np
+
+from .field import FR_MODULUS, fr_mont, fr_unmont
 from .kzg import Domain, GpuKzgPcs
 
 
@@ -31,6 +33,8 @@ class Proof:
     opened: object
     degree_bits: int
     timings_ms: dict = field(default_factory=dict)
+    alpha: int | None = None  # the challenges used (canonical ints)
+    zeta: int | None = None
 
 
 def log_quotient_degree(max_constraint_degree: int) -> int:
@@ -39,9 +43,13 @@ def log_quotient_degree(max_constraint_degree: int) -> int:
     return (d - 1).bit_length()
 
 
-def prove(air, pcs: GpuKzgPcs, trace, alpha: int, zeta: int, max_constraint_degree: int = 3,
-          shard=None) -> Proof:
+def prove(air, pcs: GpuKzgPcs, trace, alpha: int | None, zeta: int | None, max_constraint_degree: int = 3,
+          shard=None, challenger=None) -> Proof:
     """trace: (N, width, 4) device tensor.  The Poseidon2-AIR's constraints have degree 3.
+
+    challenger: a native.Challenger (DuplexChallenger<Fr, Poseidon2Bn254<3>, 3, 2>); alpha and
+    zeta are then sampled from the transcript (prover.rs:196-208, 300, 373, 416) and returned in
+    proof.alpha / proof.zeta, the arguments ignored.
 
     shard: a distributed.Shard when the prove is split by vector lane over several ranks; `air`
     and `trace` are then this rank's lanes (a VectorizedPoseidon2Air of shard.lanes' length and
@@ -71,6 +79,14 @@ def prove(air, pcs: GpuKzgPcs, trace, alpha: int, zeta: int, max_constraint_degr
     t0 = tick()
     trace_commit, trace_data = pcs.commit([(trace_domain, trace)])  # prover.rs:186-187
     t1 = tick()
+    if challenger is not None:
+        commit_all = trace_commit[0]
+        if shard is not None:  # every rank observes the full commitment, in lane order
+            local = torch.from_numpy(np.ascontiguousarray(trace_commit[0]).view(np.int64)).to(trace.device)
+            commit_all = D.all_gather_rows(local, shard.group).cpu().numpy().view(np.uint64).reshape(-1, 8)
+        challenger.observe(np.stack([_lim(log_n), _lim(log_n), _lim(0)]))  # prover.rs:196-198
+        challenger.observe_g1(commit_all)  # :202
+        alpha = fr_unmont(_limbs_int(challenger.sample()))  # :300
     quotient_domain = trace_domain.create_disjoint_domain(1 << (log_n + log_qd))  # prover.rs:307-308
     lde = pcs.get_evaluations_on_domain(trace_data, 0, quotient_domain)  # prover.rs:315
     t2 = tick()
@@ -84,6 +100,10 @@ def prove(air, pcs: GpuKzgPcs, trace, alpha: int, zeta: int, max_constraint_degr
         del parts
     t3x = tick()
     quotient_commit, quotient_data = pcs.commit_quotient(quotient_domain, qv, num_chunks)  # :371-372
+    if challenger is not None:
+        for m in quotient_commit:
+            challenger.observe_g1(m)  # :373
+        zeta = fr_unmont(_limbs_int(challenger.sample()))  # :416
     t4 = tick()
     zeta_next = trace_domain.next_point(zeta)  # prover.rs:416-419
     opened = pcs.open([(trace_data, [[zeta, zeta_next]]),
@@ -106,7 +126,16 @@ def prove(air, pcs: GpuKzgPcs, trace, alpha: int, zeta: int, max_constraint_degr
     if shard is not None:
         t["exchange partial quotients"] = (t3x - t3) * 1e3
         t["assemble columns"] = (t6 - t5) * 1e3
-    return Proof(trace_commit, quotient_commit, opened, log_n, t)
+    return Proof(trace_commit, quotient_commit, opened, log_n, t, alpha, zeta)
+
+
+def _lim(x: int) -> np.ndarray:
+    m = fr_mont(x % FR_MODULUS)
+    return np.array([(m >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+
+
+def _limbs_int(a) -> int:
+    return sum(int(v) << (64 * i) for i, v in enumerate(np.asarray(a).reshape(4)))
 
 
 def zeta_next_of(zeta: int, log_n: int) -> int:

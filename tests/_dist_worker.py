@@ -153,7 +153,7 @@ def run_native(rank, world, group):
     from plonky3_eon_amd import distributed as D
     from plonky3_eon_amd.air import Poseidon2Air
     from plonky3_eon_amd.kzg import GpuKzgPcs
-    from plonky3_eon_amd.native import NativeKzgPcs, TorchCollective, prove_native
+    from plonky3_eon_amd.native import Challenger, NativeKzgPcs, Poseidon2Constants, TorchCollective, prove_native
     from plonky3_eon_amd.prover import prove
 
     log_n, vl = int(os.environ.get("EON_T_LOG_N", "5")), int(os.environ.get("EON_T_VL", "4"))
@@ -168,6 +168,12 @@ def run_native(rank, world, group):
     air = Poseidon2Air(k.begin, k.partial, k.end, l1 - l0, ctx)
     trace = air.generate_trace(torch.from_numpy(lane_inputs(inputs, n, vl, l0, l1).view(np.int64)).to(dev))
     p = prove_native(air, npcs, trace, alpha, zeta, collective=TorchCollective(rank, world, group))
+    # the Fiat-Shamir transcript: every rank observes the full (all-gathered) trace commitment
+    pyc = O.p2_constants(99, 2, 22)
+    ck = Poseidon2Constants([[lim(x) for x in r] for r in pyc[0]], [lim(x) for x in pyc[1]],
+                            [[lim(x) for x in r] for r in pyc[2]])
+    pf = prove_native(air, npcs, trace, None, None, collective=TorchCollective(rank, world, group),
+                      challenger=Challenger(ck))
     if rank != 0:
         return None
     full_air = Poseidon2Air(k.begin, k.partial, k.end, vl, ctx)
@@ -179,6 +185,12 @@ def run_native(rank, world, group):
             return f"{name}: sharded native prove differs from the unsharded one"
         if not np.array_equal(np.asarray(b), np.asarray(c)):
             return f"{name}: native prove differs from the Python prover"
+    qf = prove_native(full_air, npcs, full, None, None, challenger=Challenger(ck))
+    if (pf.alpha, pf.zeta) != (qf.alpha, qf.zeta):
+        return "sharded Fiat-Shamir transcript differs from the unsharded one"
+    for (name, a), (_, b) in zip(_proof_fields(pf), _proof_fields(qf)):
+        if not np.array_equal(np.asarray(a), np.asarray(b)):
+            return f"{name}: sharded Fiat-Shamir prove differs from the unsharded one"
     return None
 
 

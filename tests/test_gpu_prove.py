@@ -139,6 +139,52 @@ def test_native_prove_vs_oracle(gpu_ctx, consts, log_n, vl):
         np.testing.assert_array_equal(qo.witnesses[c][0], want["quotient_open"][c][1][0])
 
 
+@pytest.mark.parametrize("log_n,vl", [(3, 1), (4, 2)])
+def test_native_prove_fiat_shamir_vs_oracle(gpu_ctx, consts, log_n, vl):
+    """eon_prove_p2air_fs: alpha and zeta sampled from the DuplexChallenger transcript
+    (prover.rs:196-208, 300, 373, 416) -- challenges and proof equal the oracle's."""
+    import torch
+
+    from plonky3_eon_amd.air import Poseidon2Air
+    from plonky3_eon_amd.native import Challenger, NativeKzgPcs, Poseidon2Constants, prove_native
+
+    n = 1 << log_n
+    pcs = NativeKzgPcs(n, 12345, gpu_ctx)
+    air = Poseidon2Air(consts.begin, consts.partial, consts.end, vl, gpu_ctx)
+    inputs = C.random_fr(log_n * 5 + vl, n * vl * 3).reshape(n * vl, 3, 4)
+    trace = air.generate_trace(torch.from_numpy(inputs.view(np.int64)).to("cuda:0"))
+    pyc = O.p2_constants(99, 2, 22)  # the challenger's own permutation, as new_from_rng(4, 22)
+    ch = Challenger(Poseidon2Constants([[lim(x) for x in r] for r in pyc[0]], [lim(x) for x in pyc[1]],
+                                       [[lim(x) for x in r] for r in pyc[2]]))
+    proof = prove_native(air, pcs, trace, None, None, challenger=ch)
+
+    ref = O.DuplexChallenger(pyc)
+    srs = C.g1_srs(n + 1, C.fr_from_u64(12345))
+    want = prove_oracle.prove(C.p2_generate_trace(inputs, vl, consts), srs, consts, vl, None, None,
+                              challenger=ref)
+    assert (proof.alpha, proof.zeta) == (want["alpha"], want["zeta"])
+    np.testing.assert_array_equal(ch.state(), np.stack([lim(x) for x in ref.state]))
+    # the Python mirror (prover.py) with its own challenger samples the same challenges
+    from plonky3_eon_amd.kzg import GpuKzgPcs
+    from plonky3_eon_amd.prover import prove
+
+    ch2 = Challenger(Poseidon2Constants([[lim(x) for x in r] for r in pyc[0]], [lim(x) for x in pyc[1]],
+                                        [[lim(x) for x in r] for r in pyc[2]]))
+    pp = prove(air, GpuKzgPcs(n, 12345, gpu_ctx), trace, None, None, challenger=ch2)
+    assert (pp.alpha, pp.zeta) == (want["alpha"], want["zeta"])
+    np.testing.assert_array_equal(pp.opened[0].witnesses[0][1], want["trace_open"][1][1])
+    np.testing.assert_array_equal(proof.trace_commit[0], want["trace_commit"])
+    np.testing.assert_array_equal(np.stack([c[0] for c in proof.quotient_commit]), want["quotient_commit"])
+    tr = proof.opened[0]
+    for p in range(2):
+        np.testing.assert_array_equal(tr.values[0][p], want["trace_open"][0][p])
+        np.testing.assert_array_equal(tr.witnesses[0][p], want["trace_open"][1][p])
+    qo = proof.opened[1]
+    for c in range(2):
+        np.testing.assert_array_equal(qo.values[c][0], want["quotient_open"][c][0][0])
+        np.testing.assert_array_equal(qo.witnesses[c][0], want["quotient_open"][c][1][0])
+
+
 def test_native_errors(gpu_ctx, consts):
     """Reference panics -> EonError: degree above the SRS (KzgError::DegreeTooLarge), a
     non-power-of-two height."""

@@ -263,7 +263,9 @@ def cpu_baseline_prove(log_n: int, vl: int, consts) -> dict:
 class ProveWorkload:
     """configs[3]: eon-uni-stark prove of the vectorized Poseidon2-AIR (VECTOR_LEN 8, 2^(log_n+3)
     permutations, log-trace-length log_n) with KzgPcs over BN254 (SRS max_degree 2^log_n,
-    alpha 12345); alpha / zeta fixed (transcript out of scope).  At N > 1 the ONE proof is split
+    alpha 12345); alpha / zeta sampled from the Fiat-Shamir transcript (DuplexChallenger over
+    Poseidon2Bn254<3>, 8 full + 56 partial rounds, synthetic constants; --transcript fixed keeps
+    them constant).  At N > 1 the ONE proof is split
     by vector lane over the ranks (plonky3_eon_amd/distributed.py): strong scaling.
 
     --host native (default) runs the C++ prove driver (libeonprove.so, include/eon_prove.h; at N > 1
@@ -308,24 +310,30 @@ class ProveWorkload:
         self.trace = self.air.generate_trace(inputs)
         del inputs
         self.alpha, self.zeta = 0x1234567890ABCDEF1234567, 0xFEDCBA09876543210FEDCBA
+        self.fs = args.transcript == "fs"
+        self.ch_consts = p2_constants_limbs(77)  # the challenger's own permutation
         self.timings = []
 
     def step(self):
+        from plonky3_eon_amd.native import Challenger, Poseidon2Constants
         from plonky3_eon_amd.prover import prove
 
+        # config.initialise_challenger() per proof (prover.rs:164)
+        ch = Challenger(Poseidon2Constants(*self.ch_consts)) if self.fs else None
         if self.native:
             from plonky3_eon_amd.native import prove_native
 
-            p = prove_native(self.air, self.pcs, self.trace, self.alpha, self.zeta, collective=self.coll)
+            p = prove_native(self.air, self.pcs, self.trace, self.alpha, self.zeta, collective=self.coll,
+                             challenger=ch)
         else:
-            p = prove(self.air, self.pcs, self.trace, self.alpha, self.zeta, shard=self.shard)
+            p = prove(self.air, self.pcs, self.trace, self.alpha, self.zeta, shard=self.shard, challenger=ch)
         self.timings.append(p.timings_ms)
 
     def describe(self, world):
         w = 164 * self.vl
         return (f"configs[3]: eon-uni-stark prove, Poseidon2-AIR (VECTOR_LEN {self.vl}, width {w}) "
                 f"log-trace-length {self.log_n} (2^{self.log_n + (self.vl.bit_length() - 1)} permutations), "
-                f"KzgPcs over BN254", world, 1 << self.log_n, f"lane-shard x{world}" if world > 1 else "single")
+                f"KzgPcs over BN254" + (", Fiat-Shamir transcript" if self.fs else ", fixed alpha/zeta"), world, 1 << self.log_n, f"lane-shard x{world}" if world > 1 else "single")
 
     def throughput(self, world, ms):
         n = 1 << self.log_n
@@ -477,6 +485,8 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host", choices=["native", "python"], default="native",
                     help="prove: C++ driver (libeonprove.so) or the Python mirror")
+    ap.add_argument("--transcript", choices=["fs", "fixed"], default="fs",
+                    help="prove: alpha/zeta from the Fiat-Shamir transcript (default) or fixed")
     ap.add_argument("--collective", choices=["torch", "rccl"], default="torch",
                     help="prove --host native at N > 1: all-gathers through torch.distributed (RCCL "
                          "process group) or the driver's own RCCL communicator")

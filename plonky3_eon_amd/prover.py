@@ -5,9 +5,10 @@ what the benchmark AIR exercises: no preprocessed columns, no lo
 (KzgPcs::ZK = false, kzg/src/pcs.rs:216), Challenge = Fr.
 
 Fiat-Shamir: the reference samples alpha and zeta from a DuplexChallenger over
-Poseidon2Bn254 (prover.rs:196-208,300,416).  The transcript is out of scope this round
-(its G1 byte encoding is halo2curves-internal and unpinned), so alpha and
-zeta are explicit inputs; every value the prover computes from them is the reference's.
+Poseidon2Bn254 (prover.rs:196-208,300,373,416).  With `challenger` (native.Challenger, the host
+transcript of libeonprove) they are sampled the same way; without it they
+are explicit inputs.  The compressed G1 bytes the transcript reads are halo2curves-internal and
+unpinned.
 
 Stage timings (HIP events via the host clock after a device synchronize) are returned under
 the reference's span names ("commit to trace data", "commit to quotient poly chunks", "open").

@@ -45,10 +45,11 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "eon-uni-stark prove ms, Poseidon2-AIR 2^20 rows KZG/BN254, at 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# measured 256-bit Montgomery multiply peak on MI355X: the radix-2^29 carry-free product
-# (tools/ubench_r29.hip, profiles/r01_ubench_r29.txt: 1.73e11/s; the radix-2^32 FIPS product of
-# the NTT/quotient kernels peaks at 1.29e11/s, tools/ubench_mulmod.hip)
-MULMOD_PEAK_PER_S = 1.73e11
+# measured 256-bit Montgomery multiply peak on MI355X: the radix-2^29 carry-free product with its
+# columns chained through one accumulator (tools/ubench_r29.hip, profiles/r01_ubench_r29.txt:
+# 1.80e11/s; the radix-2^32 FIPS product of the quotient kernel peaks at 1.29e11/s,
+# tools/ubench_mulmod.hip)
+MULMOD_PEAK_PER_S = 1.80e11
 FR_P = [0x43E1F593F0000001, 0x2833E84879B97091, 0xB85045B68181585D, 0x30644E72E131A029]
 
 

@@ -204,6 +204,27 @@ EON_HD bool is_zero_mod29(const F29& a) {
     return z == 0 || e == 0;
 }
 
+// acc += a b as ONE v_mad_u64_u32 on the running accumulator: written in asm so that the
+// compiler cannot re-associate a column into a separate partial sum merged by an extra 64-bit add
+// (what it does with the C++ form: one v_lshl_add_u64 per column, 17 per product).  The host
+// pass of the compiler (kernel stubs, host-side users of EON_HD code) sees the plain expression.
+EON_HD void mad29_vv(uint64_t& acc, uint32_t a, uint32_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    uint64_t c;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(c) : "v"(a), "v"(b));
+#else
+    acc += (uint64_t)a * b;
+#endif
+}
+EON_HD void mad29_vs(uint64_t& acc, uint32_t a, uint32_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    uint64_t c;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(c) : "v"(a), "s"(b));
+#else
+    acc += (uint64_t)a * b;
+#endif
+}
+
 // Montgomery product a b 2^-261 mod p (product scanning; see the header comment for the bounds)
 template <class M>
 EON_HD F29 mul29(const F29& a, const F29& b) {
@@ -213,19 +234,19 @@ EON_HD F29 mul29(const F29& a, const F29& b) {
 #pragma unroll
     for (int k = 0; k < 9; k++) {
 #pragma unroll
-        for (int i = 0; i <= k; i++) acc += (uint64_t)a.l[i] * b.l[k - i];
+        for (int i = 0; i <= k; i++) mad29_vv(acc, a.l[i], b.l[k - i]);
 #pragma unroll
-        for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * R29<M>::P[k - i];
+        for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
         m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
-        acc += (uint64_t)m[k] * R29<M>::P[0];
+        mad29_vs(acc, m[k], R29<M>::P[0]);
         acc >>= 29;
     }
 #pragma unroll
     for (int k = 9; k < 17; k++) {
 #pragma unroll
         for (int i = k - 8; i < 9; i++) {
-            acc += (uint64_t)a.l[i] * b.l[k - i];
-            acc += (uint64_t)m[i] * R29<M>::P[k - i];
+            mad29_vv(acc, a.l[i], b.l[k - i]);
+            mad29_vs(acc, m[i], R29<M>::P[k - i]);
         }
         r.l[k - 9] = (uint32_t)acc & M29;
         acc >>= 29;
@@ -245,24 +266,24 @@ EON_HD F29 sqr29(const F29& a) {
     for (int k = 0; k < 9; k++) {
         uint64_t cross = 0;
 #pragma unroll
-        for (int i = 0; 2 * i < k; i++) cross += (uint64_t)a.l[i] * a.l[k - i];
+        for (int i = 0; 2 * i < k; i++) mad29_vv(cross, a.l[i], a.l[k - i]);
         acc += cross << 1;
-        if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+        if ((k & 1) == 0) mad29_vv(acc, a.l[k / 2], a.l[k / 2]);
 #pragma unroll
-        for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * R29<M>::P[k - i];
+        for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
         m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
-        acc += (uint64_t)m[k] * R29<M>::P[0];
+        mad29_vs(acc, m[k], R29<M>::P[0]);
         acc >>= 29;
     }
 #pragma unroll
     for (int k = 9; k < 17; k++) {
         uint64_t cross = 0;
 #pragma unroll
-        for (int i = k - 8; 2 * i < k; i++) cross += (uint64_t)a.l[i] * a.l[k - i];
+        for (int i = k - 8; 2 * i < k; i++) mad29_vv(cross, a.l[i], a.l[k - i]);
         acc += cross << 1;
-        if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+        if ((k & 1) == 0) mad29_vv(acc, a.l[k / 2], a.l[k / 2]);
 #pragma unroll
-        for (int i = k - 8; i < 9; i++) acc += (uint64_t)m[i] * R29<M>::P[k - i];
+        for (int i = k - 8; i < 9; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
         r.l[k - 9] = (uint32_t)acc & M29;
         acc >>= 29;
     }
@@ -281,22 +302,22 @@ EON_HD F29 mul29_sum2(const F29& a, const F29& b, const F29& c, const F29& d) {
     for (int k = 0; k < 9; k++) {
 #pragma unroll
         for (int i = 0; i <= k; i++) {
-            acc += (uint64_t)a.l[i] * b.l[k - i];
-            acc += (uint64_t)c.l[i] * d.l[k - i];
+            mad29_vv(acc, a.l[i], b.l[k - i]);
+            mad29_vv(acc, c.l[i], d.l[k - i]);
         }
 #pragma unroll
-        for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * R29<M>::P[k - i];
+        for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
         m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
-        acc += (uint64_t)m[k] * R29<M>::P[0];
+        mad29_vs(acc, m[k], R29<M>::P[0]);
         acc >>= 29;
     }
 #pragma unroll
     for (int k = 9; k < 17; k++) {
 #pragma unroll
         for (int i = k - 8; i < 9; i++) {
-            acc += (uint64_t)a.l[i] * b.l[k - i];
-            acc += (uint64_t)c.l[i] * d.l[k - i];
-            acc += (uint64_t)m[i] * R29<M>::P[k - i];
+            mad29_vv(acc, a.l[i], b.l[k - i]);
+            mad29_vv(acc, c.l[i], d.l[k - i]);
+            mad29_vs(acc, m[i], R29<M>::P[k - i]);
         }
         r.l[k - 9] = (uint32_t)acc & M29;
         acc >>= 29;

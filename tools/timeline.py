@@ -13,7 +13,7 @@ win_ms = float(sys.argv[3]) if len(sys.argv) > 3 else 0
 rows = list(csv.DictReader(open(path)))
 for r in rows:
     r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    r["n"] = r["Kernel_Name"].split("(")[0].replace("void ", "")[-40:]
+    r["n"] = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")[-40:]
 end = max(r["e"] for r in rows)
 t0 = end - win_ms * 1e6 if win_ms else min(r["s"] for r in rows)
 win = [r for r in rows if r["s"] >= t0]

@@ -21,7 +21,8 @@ __global__ void __launch_bounds__(256) k_mul29(const Fe<M>* in, Fe<M>* out, int 
     for (int c = 0; c < CH; c++) x[c] = unpack29(in[(tid + c) & 1023]);
     for (int it = 0; it < iters; it++) {
 #pragma unroll
-        for (int c = 0; c < CH; c++) x[c] = V == 1 ? mul29_2acc<M>(x[c], y) : mul29<M>(x[c], y);
+        for (int c = 0; c < CH; c++)
+            x[c] =  (V == 1 ? mul29_2acc<M>(x[c], y) : mul29<M>(x[c], y));
     }
     F29 acc = x[0];
 #pragma unroll

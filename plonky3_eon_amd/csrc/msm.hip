@@ -966,7 +966,9 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
     SegLogs logs{};
     const G1Xyzz* X = wk.bucket_sums.as<G1Xyzz>();
     uint32_t Lb = B, m = 0;
-    prof->begin("k_seg_level", (uint64_t)nb * 128 + (uint64_t)nb / SEG * 256, st);
+    // profiled as one span: the weighted bucket sum (k_bucket_reduce29 or k_seg_level, then
+    // k_group_finish, or the level chain)
+    prof->begin("bucket_reduce", (uint64_t)nb * 128 + (uint64_t)nb / SEG * 256, st);
     // EON_MSM_SEG_LEVELS=1: the level-by-level chain below instead of k_group_finish
     static const bool seg_levels = getenv("EON_MSM_SEG_LEVELS") != nullptr;
     if (!seg_levels) {

@@ -529,11 +529,12 @@ __global__ void k_precompute_windows(const G1Affine* pts, uint64_t n, uint32_t c
 
 // XYZZ -> affine with Montgomery's batch inversion over chunks of BATCH consecutive points; the
 // prefix products are parked in the outputs' x coordinates (no per-lane array, no scratch)
+template <uint32_t CHUNK>
 __global__ void k_batch_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t i0 = t * BATCH;
+    const uint64_t i0 = t * CHUNK;
     if (i0 >= m) return;
-    const uint64_t i1 = min(i0 + BATCH, m);
+    const uint64_t i1 = min(i0 + CHUNK, m);
     Fq acc = Fq::one();
     for (uint64_t i = i0; i < i1; i++) {
         st_vec(&out[i].x, acc);
@@ -601,8 +602,20 @@ static inline unsigned blocks_for(uint64_t n, unsigned bs) { return (unsigned)((
 
 hipError_t launch_batch_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out, hipStream_t st) {
     if (m == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_batch_to_affine, dim3(blocks_for((m + BATCH - 1) / BATCH, 128)), dim3(128),
-                       0, st, in, m, out);
+    // one inversion (~380 dependent products) per CHUNK points: a small chunk spends more
+    // products, a large one leaves the SIMDs idle behind the latency of too few waves
+    static const uint32_t chunk = [] {
+        const char* e = getenv("EON_B2A_CHUNK");
+        const int v = e ? atoi(e) : (int)BATCH;
+        return (uint32_t)(v == 8 || v == 16 || v == 64 ? v : 32);
+    }();
+    const unsigned threads = 128;
+    switch (chunk) {
+        case 8: hipLaunchKernelGGL(k_batch_to_affine<8>, dim3(blocks_for((m + 7) / 8, threads)), dim3(threads), 0, st, in, m, out); break;
+        case 16: hipLaunchKernelGGL(k_batch_to_affine<16>, dim3(blocks_for((m + 15) / 16, threads)), dim3(threads), 0, st, in, m, out); break;
+        case 64: hipLaunchKernelGGL(k_batch_to_affine<64>, dim3(blocks_for((m + 63) / 64, threads)), dim3(threads), 0, st, in, m, out); break;
+        default: hipLaunchKernelGGL(k_batch_to_affine<32>, dim3(blocks_for((m + 31) / 32, threads)), dim3(threads), 0, st, in, m, out); break;
+    }
     return hipGetLastError();
 }
 

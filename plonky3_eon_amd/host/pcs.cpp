@@ -302,7 +302,16 @@ std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
     };
     hipStream_t st = static_cast<hipStream_t>(eon_ctx_stream(ctx_));
     std::vector<Opened> out(rounds.size());
-    // f(z) of every column at every point (the remainder of quotient_and_eval, util.rs:100-111)
+    // f(z) of every column at every point (the remainder of quotient_and_eval, util.rs:100-111):
+    // enqueued on the auxiliary context, whose HBM-bound passes over the coefficients run beside
+    // the VALU-bound opening-bases construction; read back after the witnesses
+    eon_ctx* vctx = aux_ ? aux_ : ctx_;
+    hipStream_t vst = static_cast<hipStream_t>(eon_ctx_stream(vctx));
+    std::vector<std::vector<DeviceBuffer>> vals(rounds.size());
+    struct DrainOnExit {  // an error path must not free `vals` under the kernels writing them
+        hipStream_t s;
+        ~DrainOnExit() { (void)hipStreamSynchronize(s); }
+    } drain{vst};
     for (size_t r = 0; r < rounds.size(); r++) {
         const auto& data = *rounds[r].data;
         out[r].values.resize(data.size());
@@ -313,21 +322,29 @@ std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
             const uint32_t w = md.coeffs.width;
             out[r].values[m].resize(pts.size());
             out[r].witnesses[m].resize(pts.size());
-            DeviceBuffer vals(std::max<uint64_t>(pts.size() * w, 1) * sizeof(eon_fr));
+            vals[r].emplace_back(std::max<uint64_t>(pts.size() * w, 1) * sizeof(eon_fr));
             std::vector<eon_fr> zs(pts.size());
             for (size_t p = 0; p < pts.size(); p++) zs[p] = pts[p].abi();
-            check(ctx_,
-                  eon_eval_columns_dev(ctx_, md.coeffs.data(), md.coeffs.height, w, zs.data(), (uint32_t)zs.size(),
-                                       vals.as<eon_fr>()),
+            check(vctx,
+                  eon_eval_columns_dev(vctx, md.coeffs.data(), md.coeffs.height, w, zs.data(), (uint32_t)zs.size(),
+                                       vals[r].back().as<eon_fr>()),
                   "opened values");
-            std::vector<eon_fr> hv(pts.size() * w);
-            hip_check(hipMemcpyAsync(hv.data(), vals.get(), hv.size() * sizeof(eon_fr), hipMemcpyDeviceToHost, st),
-                      "opened values");
-            hip_check(hipStreamSynchronize(st), "opened values");
-            for (size_t p = 0; p < pts.size(); p++)
-                out[r].values[m][p].assign(hv.begin() + p * w, hv.begin() + (p + 1) * w);
         }
     }
+    auto collect_values = [&] {
+        for (size_t r = 0; r < rounds.size(); r++)
+            for (size_t m = 0; m < rounds[r].data->size(); m++) {
+                const size_t np = rounds[r].points[m].size();
+                const uint32_t w = (*rounds[r].data)[m].coeffs.width;
+                std::vector<eon_fr> hv(np * w);
+                hip_check(hipMemcpyAsync(hv.data(), vals[r][m].get(), hv.size() * sizeof(eon_fr),
+                                         hipMemcpyDeviceToHost, vst),
+                          "opened values");
+                hip_check(hipStreamSynchronize(vst), "opened values");
+                for (size_t p = 0; p < np; p++)
+                    out[r].values[m][p].assign(hv.begin() + p * w, hv.begin() + (p + 1) * w);
+            }
+    };
     // witnesses of the (matrix, point) pairs whose bases are ready, every point of a matrix in
     // one run over its prepared digits
     std::vector<std::vector<std::vector<bool>>> done(rounds.size());
@@ -367,6 +384,7 @@ std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
     if (!overlap || !aux_ || keys.size() < 2) {
         build(ctx_, keys);
         run_ready();
+        collect_values();
         return out;
     }
     build(ctx_, {keys[0]});
@@ -403,6 +421,7 @@ std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
     for (auto& kv : made) bases_at[kv.first] = kv.second;
     if (err) std::rethrow_exception(err);
     run_ready();
+    collect_values();
     return out;
 }
 

@@ -86,3 +86,33 @@ def test_eval_columns_multi_point(gpu_ctx, rows, width, npts):
         for j in range(width):
             _, v = C.quotient_and_eval(coeffs[:, j], z)
             np.testing.assert_array_equal(got[t, j], v, err_msg=f"point {t} column {j}")
+
+
+def test_eval_columns_edge_cases(gpu_ctx):
+    """Empty columns evaluate to 0 (kzg/src/util.rs:101-103), no points is a no-op, a
+    non-canonical point is refused."""
+    import ctypes
+
+    import torch
+
+    from plonky3_eon_amd import _lib
+    from plonky3_eon_amd.kzg import fr_to_abi
+
+    lib, h = gpu_ctx.lib, gpu_ctx.handle
+    out = torch.full((2, 3, 4), 7, dtype=torch.int64, device="cuda:0")
+    zs = (_lib.eon_fr * 2)(fr_to_abi(C.fr_from_u64(3)), fr_to_abi(C.fr_from_u64(4)))
+    gpu_ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    gpu_ctx.check(lib.eon_eval_columns_dev(h, None, 0, 3, zs, 2, ctypes.c_void_p(out.data_ptr())))
+    assert int(out.abs().sum().item()) == 0
+    out.fill_(7)
+    c = _dev(C.random_fr(3, 4 * 3).reshape(4, 3, 4))
+    gpu_ctx.check(lib.eon_eval_columns_dev(h, ctypes.c_void_p(c.data_ptr()), 4, 3, zs, 0,
+                                           ctypes.c_void_p(out.data_ptr())))
+    torch.cuda.synchronize()
+    assert bool((out == 7).all())
+    bad = _lib.eon_fr()
+    for i, v in enumerate([0x43E1F593F0000001, 0x2833E84879B97091, 0xB85045B68181585D, 0x30644E72E131A029]):
+        bad.l[i] = v  # r itself
+    with pytest.raises(EonError):
+        gpu_ctx.check(lib.eon_eval_columns_dev(h, ctypes.c_void_p(c.data_ptr()), 4, 3, ctypes.byref(bad), 1,
+                                               ctypes.c_void_p(out.data_ptr())))

@@ -36,6 +36,7 @@ struct PassArgs {
     uint32_t load_param;
     uint32_t has_load_const;
     uint32_t col_tiles;
+    uint32_t radix4;  // k_ntt_pass29: two stages per LDS round trip (EON_NTT_R4)
 };
 
 __device__ __forceinline__ void lds_put(uint4* lo, uint4* hi, uint32_t i, const Fr& x) {
@@ -279,7 +280,74 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
     }
     __syncthreads();
 
-    for (uint32_t it = 0; it < k; it++) {
+    auto tw29 = [&](uint32_t q) {
+        F29 w;
+#pragma unroll
+        for (int i = 0; i < 9; i++) w.l[i] = twl[9 * q + i];
+        pin29(w);
+        return w;
+    };
+    // DitButterfly (dft/src/butterflies.rs:177-185): (x + w y, x - w y); inputs < 4p, outputs < 4p
+    auto bfly_dit = [](F29& x, F29& y, const F29& w, bool unit) {
+        const F29 xr = reduce29<2>(x);
+        const F29 t = unit ? reduce29<2>(y) : mul29<FrP>(y, w);
+        x = add29_norm(xr, t);
+        y = sub29<FrP, 2>(xr, t);
+    };
+    // DIF butterfly: (x + y, (x - y) w)
+    auto bfly_dif = [](F29& x, F29& y, const F29& w, bool unit) {
+        const F29 xr = reduce29<2>(x), yr = reduce29<2>(y);
+        const F29 d = sub29<FrP, 2>(xr, yr);
+        x = add29_norm(xr, yr);
+        y = unit ? d : mul29<FrP>(d, w);
+    };
+    uint32_t it = 0;
+    // radix-4 rounds: the four elements m0 + t h (t < 4) close under two consecutive stages, so a
+    // thread carries them through both in registers -- half the LDS traffic and barriers
+    while (a.radix4 && it + 2 <= k) {
+        const uint32_t lq = DIF ? (k - 2 - it) : it;  // log2 of the quarter distance h
+        const uint32_t h = 1u << lq;
+        for (uint32_t b = threadIdx.x; b < (ne >> 2); b += T) {
+            const uint32_t c = b & (CB - 1);
+            const uint32_t j = b >> LOG_CB;
+            const uint32_t r0 = j & (h - 1);
+            const uint32_t m0 = ((j >> lq) << (lq + 2)) | r0;
+            uint32_t idx[4];
+            F29 x[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                idx[t] = ((m0 + t * h) << LOG_CB) | c;
+                x[t] = lds_get29(lo, hi, top, idx[t]);
+            }
+            const bool unit = (r0 | low) == 0;
+            if (!DIF) {
+                // stage lq (half h): (0,1), (2,3) with w(h + r0); stage lq + 1 (half 2h): (0,2) with
+                // w(2h + r0), (1,3) with w(3h + r0)
+                const F29 w = unit ? F29{} : tw29(h + r0);
+                bfly_dit(x[0], x[1], w, unit);
+                bfly_dit(x[2], x[3], w, unit);
+                const F29 w0 = unit ? F29{} : tw29(2 * h + r0);
+                bfly_dit(x[0], x[2], w0, unit);
+                const F29 w1 = tw29(3 * h + r0);
+                bfly_dit(x[1], x[3], w1, false);
+            } else {
+                // stage lq + 1 (half 2h): (0,2) with w(2h + r0), (1,3) with w(3h + r0); stage lq
+                // (half h): (0,1), (2,3) with w(h + r0)
+                const F29 w0 = unit ? F29{} : tw29(2 * h + r0);
+                bfly_dif(x[0], x[2], w0, unit);
+                const F29 w1 = tw29(3 * h + r0);
+                bfly_dif(x[1], x[3], w1, false);
+                const F29 w = unit ? F29{} : tw29(h + r0);
+                bfly_dif(x[0], x[1], w, unit);
+                bfly_dif(x[2], x[3], w, unit);
+            }
+#pragma unroll
+            for (int t = 0; t < 4; t++) lds_put29(lo, hi, top, idx[t], x[t]);
+        }
+        __syncthreads();
+        it += 2;
+    }
+    for (; it < k; it++) {
         const uint32_t l = DIF ? (k - 1 - it) : it;
         const uint32_t half = 1u << l;
         for (uint32_t b = threadIdx.x; b < (ne >> 1); b += T) {
@@ -478,6 +546,11 @@ hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
                             (a.store_scale ? elems : 0);
         if (prof) prof->begin(names[(s.dif ? 4 : 0) + log_cb], 64ull * elems, st, mm);
         a.col_tiles = (uint32_t)col_tiles;
+        static const bool r4 = [] {
+            const char* e = getenv("EON_NTT_R4");
+            return e && e[0] == '1';
+        }();
+        a.radix4 = r4 ? 1u : 0u;
         const uint32_t tpb = s.max_threads ? s.max_threads : (log_tile > 10 ? 1024 : 512);
         hipError_t e = launch_pass(s.dif, log_cb, a, groups, col_tiles, tpb, st);
         if (prof) prof->end(st);

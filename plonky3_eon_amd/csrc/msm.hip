@@ -653,7 +653,13 @@ Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32
         if (e != hipSuccess) return fail(Status::err(EON_E_DEVICE, hipGetErrorString(e)));
     }
     b->precomputed = (flags & EON_MSM_PRECOMPUTE) != 0 && n > 0;
-    b->c = force_c ? force_c : choose_c(n ? n : 1, b->precomputed);
+    // EON_MSM_C (A/B knob): the window of precomputed (fixed-base) tables
+    static const uint32_t env_c = [] {
+        const char* e = getenv("EON_MSM_C");
+        const int v = e ? atoi(e) : 0;
+        return (uint32_t)(v >= 8 && v <= 20 ? v : 0);
+    }();
+    b->c = force_c ? force_c : (env_c && b->precomputed ? env_c : choose_c(n ? n : 1, b->precomputed));
     b->windows = (255 + b->c - 1) / b->c;
     if (b->precomputed) {
         const uint64_t m = n * b->windows;

@@ -404,7 +404,7 @@ __global__ void __launch_bounds__(64) k_bucket_reduce29(const G1Raw29* pieces, c
 // Thread t takes segments [t Q, (t + 1) Q): running sums give its total and locally weighted sum,
 // (t Q) times its total by double-and-add, then an LDS tree over the block.  One launch instead
 // of the seg-level / tree / final chain (~12 latency-bound launches per batch).
-constexpr uint32_t GF_THREADS = 256;
+template <uint32_t GF_THREADS>
 __global__ void __launch_bounds__(GF_THREADS) k_group_finish(const G1Xyzz* T, const G1Xyzz* U, uint32_t S,
                                                             uint32_t log_seg, G1Xyzz* out) {
     __shared__ G1Xyzz sh[GF_THREADS];
@@ -1001,8 +1001,19 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
             hipLaunchKernelGGL(k_seg_level, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st, X, B,
                                seg, groups, T, u_buf);
         G1Xyzz* per_group = wk.red_a.as<G1Xyzz>();
-        hipLaunchKernelGGL(k_group_finish, dim3(groups), dim3(GF_THREADS), 0, st, T, u_buf, nseg,
-                           31 - __builtin_clz(seg), per_group);
+        // EON_MSM_GF_THREADS (256 / 512 / 1024): threads per group of the latency-bound finish
+        static const uint32_t gf = [] {
+            const char* e = getenv("EON_MSM_GF_THREADS");
+            const int v = e ? atoi(e) : 256;
+            return (uint32_t)(v == 512 || v == 1024 ? v : 256);
+        }();
+        const uint32_t lsg = 31 - __builtin_clz(seg);
+        if (gf == 1024)
+            hipLaunchKernelGGL(k_group_finish<1024>, dim3(groups), dim3(1024), 0, st, T, u_buf, nseg, lsg, per_group);
+        else if (gf == 512)
+            hipLaunchKernelGGL(k_group_finish<512>, dim3(groups), dim3(512), 0, st, T, u_buf, nseg, lsg, per_group);
+        else
+            hipLaunchKernelGGL(k_group_finish<256>, dim3(groups), dim3(256), 0, st, T, u_buf, nseg, lsg, per_group);
         prof->end(st);
         EON_HIP(hipGetLastError());
         return write_columns(L, bt, per_group, st);

@@ -1378,13 +1378,20 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
         EON_HIP(hipStreamWaitEvent(comp[i], ctx->msm_sorted[w], 0));
         return batch_pieces(ctx, b, batches[k], sorted_ref(sorted_of(k)), *wks[w], comp[i]);
     };
+    // EON_MSM_SORT_AHEAD=1: sort(k + 1) enqueued before pieces(k), so that its kernels take CU
+    // slots before the piece sum fills them (otherwise it is starved and runs after it)
+    static const bool sort_ahead = [] {
+        const char* e = getenv("EON_MSM_SORT_AHEAD");
+        return e && e[0] == '1';
+    }();
     EON_TRY(sort_batch(0));
     for (size_t k = 0; k < batches.size(); k++) {
         const int i = (int)(k & 1), w = (int)(k % 3);
         // pieces(k + 1) is enqueued only after reduce(k)'s read-backs: launched earlier it starves
         // the latency-bound reduction (measured +20 ms per prove)
+        if (sort_ahead && k + 1 < batches.size()) EON_TRY(sort_batch(k + 1));
         EON_TRY(pieces(k));
-        if (k + 1 < batches.size()) EON_TRY(sort_batch(k + 1));
+        if (!sort_ahead && k + 1 < batches.size()) EON_TRY(sort_batch(k + 1));
         EON_TRY(batch_reduce(ctx, L, batches[k], sorted_ref(sorted_of(k)), *wks[w], comp[i],
                              fused_reduce(b, batches[k])));
         EON_HIP(hipEventRecord(ctx->msm_reduced[w], comp[i]));

@@ -67,7 +67,8 @@ def lib():
         for k, a in {"or_p2_generate_trace": [P, U64, U32, U32, U32, P, P, P, P],
                      "or_selectors_on_coset": [U32, U32, fr_t, P, P, P, P],
                      "or_p2_quotient_values": [P, U32, U32, U32, U32, U32, P, P, P, fr_t, P],
-                     "or_quotient_and_eval": [P, U64, U64, fr_t, P, P]}.items():
+                     "or_quotient_and_eval": [P, U64, U64, fr_t, P, P],
+                     "or_bary_eval_cols": [P, U64, U64, P, U32, P]}.items():
             getattr(l, k).argtypes = a
             getattr(l, k).restype = None
         l.or_p2_num_cols.argtypes = [U32, U32]
@@ -274,6 +275,17 @@ def quotient_and_eval(coeffs_col, point_limbs):
     v = np.zeros(4, dtype=np.uint64)
     lib().or_quotient_and_eval(_ptr(c), n, 1, fr(point_limbs), _ptr(q) if n > 1 else None, _ptr(v))
     return q, v
+
+
+def bary_eval_cols(evals, points):
+    """Every column polynomial of `evals` (n x w natural order over H) at each point (Montgomery
+    limbs (npts, 4)): (npts, w, 4) -- the values quotient_and_eval returns, from the evaluations."""
+    e = np.ascontiguousarray(evals, dtype=np.uint64)
+    n, w = e.shape[0], e.shape[1]
+    pts = np.ascontiguousarray(points, dtype=np.uint64).reshape(-1, 4)
+    out = np.zeros((pts.shape[0], w, 4), dtype=np.uint64)
+    lib().or_bary_eval_cols(_ptr(e), n, w, _ptr(pts), pts.shape[0], _ptr(out))
+    return out
 
 
 def num_threads() -> int:

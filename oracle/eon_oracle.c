@@ -903,3 +903,74 @@ void or_quotient_and_eval(const fr_t* coeffs, uint64_t n, uint64_t stride, fr_t 
     }
     *value = carry;
 }
+
+/* Values at arbitrary points of the polynomials that interpolate each column of `evals` (n x w,
+ * natural order) over the subgroup H = <omega_n>: the f(z) quotient_and_eval returns
+ * (kzg/src/util.rs:100-111) computed straight from the evaluations by the barycentric formula
+ * f(x) = (x^n - 1)/n * sum_i e_i * omega^i / (x - omega^i) -- O(n w) per point, so the verifier
+ * restatement can check a full-size proof's opened values against the trace itself.  Points in H
+ * are returned as the evaluation there.  out[p * w + c]. */
+void or_bary_eval_cols(const fr_t* evals, uint64_t n, uint64_t w, const fr_t* points, uint32_t npts,
+                       fr_t* out) {
+    uint32_t lg = log2_strict(n);
+    fr_t g = or_two_adic_generator(lg), one = fone();
+    fr_t inv_n = or_fr_inverse(or_fr_from_u64(n));
+    fr_t* wt = (fr_t*)malloc(sizeof(fr_t) * n);
+    for (uint32_t p = 0; p < npts; p++) {
+        fr_t x = points[p];
+        /* x in H: f(x) is the evaluation at that row */
+        fr_t xn = x;
+        for (uint32_t i = 0; i < lg; i++) xn = fmul(xn, xn);
+        if (memcmp(xn.v, one.v, 32) == 0) {
+            fr_t pw = one;
+            for (uint64_t i = 0; i < n; i++) {
+                if (memcmp(pw.v, x.v, 32) == 0) {
+                    memcpy(out + (uint64_t)p * w, evals + i * w, sizeof(fr_t) * w);
+                    break;
+                }
+                pw = fmul(pw, g);
+            }
+            continue;
+        }
+        /* weights omega^i / (x - omega^i): batch inversion (Montgomery's trick) per thread block */
+        int nt = or_num_threads();
+        uint64_t blk = (n + nt - 1) / nt;
+#pragma omp parallel for schedule(static)
+        for (int t = 0; t < nt; t++) {
+            uint64_t lo = t * blk, hi = lo + blk < n ? lo + blk : n;
+            if (lo >= hi) continue;
+            fr_t pw = or_fr_pow(g, lo), acc = one;
+            for (uint64_t i = lo; i < hi; i++) {
+                wt[i] = acc; /* prefix product of the denominators before i */
+                acc = fmul(acc, fsub(x, pw));
+                pw = fmul(pw, g);
+            }
+            fr_t inv = or_fr_inverse(acc);
+            pw = or_fr_pow(g, hi - 1);
+            fr_t g_inv = or_fr_inverse(g);
+            for (uint64_t i = hi; i-- > lo;) {
+                fr_t d = fsub(x, pw);
+                fr_t di = fmul(inv, wt[i]); /* 1 / (x - omega^i) */
+                inv = fmul(inv, d);
+                wt[i] = fmul(di, pw);
+                pw = fmul(pw, g_inv);
+            }
+        }
+        fr_t scale = fmul(fsub(xn, one), inv_n);
+        fr_t* part = (fr_t*)calloc((size_t)nt * w, sizeof(fr_t));
+#pragma omp parallel for schedule(static)
+        for (int t = 0; t < nt; t++) {
+            uint64_t lo = t * blk, hi = lo + blk < n ? lo + blk : n;
+            fr_t* acc = part + (uint64_t)t * w;
+            for (uint64_t i = lo; i < hi; i++)
+                for (uint64_t c = 0; c < w; c++) acc[c] = fadd(acc[c], fmul(evals[i * w + c], wt[i]));
+        }
+        for (uint64_t c = 0; c < w; c++) {
+            fr_t s = {{0, 0, 0, 0}};
+            for (int t = 0; t < nt; t++) s = fadd(s, part[(uint64_t)t * w + c]);
+            out[(uint64_t)p * w + c] = fmul(s, scale);
+        }
+        free(part);
+    }
+    free(wt);
+}

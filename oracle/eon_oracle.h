@@ -61,5 +61,8 @@ void or_p2_quotient_values(const fr_t* lde, uint32_t log_n, uint32_t log_qd, uin
                            fr_t alpha, fr_t* out);
 void or_quotient_and_eval(const fr_t* coeffs, uint64_t n, uint64_t stride, fr_t point, fr_t* quotient,
                           fr_t* value);
+/* the column polynomials (evaluations over H) at arbitrary points, barycentric: out[p * w + c] */
+void or_bary_eval_cols(const fr_t* evals, uint64_t n, uint64_t w, const fr_t* points, uint32_t npts,
+                       fr_t* out);
 #endif
 

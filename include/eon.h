@@ -263,6 +263,64 @@ int eon_p2air_quotient_values_dev(eon_ctx* ctx, const eon_p2air* air, const eon_
                                   uint32_t log_n, uint32_t log_qd, const eon_fr* alpha,
                                   eon_fr* out);
 
+/* ---- generic AIR: quotient_values for any EonAir ---------------------------------------------
+ * The constraints get_symbolic_constraints returns (eon-uni-stark/src/symbolic_builder.rs:72-126)
+ * as a DAG of SymbolicExpression nodes (symbolic_expression.rs:78-145; SymbolicVariable /
+ * Entry, symbolic_variable.rs:8-40), in topological order: every operand index is smaller than
+ * its user's (a shared Arc is emitted once and referenced by index).  `constraints` lists the
+ * root node of each constraint in assert order (the folder's constraint_index order,
+ * folder.rs:81-85).  Leaves: EON_SYM_CONSTANT a = index into consts (canonical Fr);
+ * EON_SYM_MAIN a = column, b = row offset (0 local, 1 next); EON_SYM_PUBLIC a = public index;
+ * the three selectors (symbolic_builder.rs:205-221).  Preprocessed, permutation (LogUp) and
+ * challenge variables are rejected (EON_E_ARG): the prove path has no preprocessed data and no
+ * lookups (prover.rs:211-250 None branch). */
+enum {
+    EON_SYM_CONSTANT = 0,
+    EON_SYM_MAIN = 1,
+    EON_SYM_PUBLIC = 2,
+    EON_SYM_IS_FIRST_ROW = 3,
+    EON_SYM_IS_LAST_ROW = 4,
+    EON_SYM_IS_TRANSITION = 5,
+    EON_SYM_ADD = 6, /* a + b */
+    EON_SYM_SUB = 7, /* a - b */
+    EON_SYM_NEG = 8, /* -a */
+    EON_SYM_MUL = 9, /* a * b */
+    EON_SYM_PREPROCESSED = 10,
+    EON_SYM_PERMUTATION = 11,
+    EON_SYM_CHALLENGE = 12
+};
+typedef struct {
+    uint32_t kind;
+    uint32_t a;
+    uint32_t b;
+} eon_sym_node;
+typedef struct eon_air_program eon_air_program;
+typedef struct {
+    uint32_t width;                 /* main trace width */
+    uint32_t num_public_values;
+    uint32_t num_constraints;
+    uint32_t max_constraint_degree; /* get_max_constraint_degree (symbolic_builder.rs:46-69) */
+    uint32_t num_instructions;      /* compiled program (after common-subexpression elimination) */
+    uint32_t num_registers;
+    uint32_t num_constants;
+} eon_air_program_stats;
+/* Compile the constraint DAG for a trace of `width` columns and n_public public values. */
+int eon_air_program_create(eon_ctx* ctx, const eon_sym_node* nodes, uint32_t n_nodes, const eon_fr* consts,
+                           uint32_t n_consts, const uint32_t* constraints, uint32_t n_constraints,
+                           uint32_t width, uint32_t n_public, eon_air_program** out);
+void eon_air_program_destroy(eon_air_program* prog);
+int eon_air_program_info(const eon_air_program* prog, eon_air_program_stats* out);
+/* get_log_quotient_degree (symbolic_builder.rs:15-43): log2_ceil(max(max_degree + is_zk, 2) - 1) */
+uint32_t eon_air_program_log_quotient_degree(const eon_air_program* prog, uint32_t is_zk);
+/* quotient_values (eon-uni-stark/src/prover.rs:539-709) of the program: `lde` = the trace on the
+ * quotient domain GENERATOR * K, |K| = 2^(log_n + log_qd), natural order, device, width columns;
+ * publics = host array of n_public Fr (public_values); alpha host.  out (device, 2^(log_n+log_qd)
+ * Fr) = sum_k alpha^(K-1-k) C_k(local = row i, next = row (i + 2^log_qd) mod Q, selectors of
+ * selectors_on_coset, publics) * inv_vanishing[i]. */
+int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog, const eon_fr* lde, uint32_t log_n,
+                            uint32_t log_qd, const eon_fr* alpha, const eon_fr* publics, uint32_t n_public,
+                            eon_fr* out);
+
 /* out[i] = sum_{j<k} coeffs[j] * in[j * rows + i] (device in/out, host coeffs, 1 <= k <= 64):
  * the combine step of the lane-sharded quotient -- every rank all-gathers the
  * shards' partial quotients and weights shard g by alpha^(K_lane * (VECTOR_LEN - lane_end_g)). */

@@ -11,6 +11,8 @@
  *                    ZK off, Challenge = Fr.  alpha and zeta are either inputs
  *                    (eon_prove_p2air) or sampled from the Fiat-Shamir transcript
  *                    (eon_prove_p2air_fs with an eon_challenger).
+ *   eon_prove_air    the same for any AIR compiled into an eon_air_program (eon.h), with public
+ *                    values (e.g. eon-uni-stark/tests/fib_air.rs's FibonacciAir)
  *   eon_challenger   DuplexChallenger<Fr, Poseidon2Bn254<3>, 3, 2>
  *                    (challenger/src/duplex_challenger.rs, bn254/src/poseidon2.rs) on the host.
  * Conventions are eon.h's: 0 / negative EON_E_* codes (the reference panics), host outputs,
@@ -109,6 +111,18 @@ int eon_challenger_state(const eon_challenger* ch, eon_fr out[3]);
 int eon_prove_p2air_fs(eon_kzg_pcs* pcs, const eon_p2air* air, const eon_fr* trace, uint64_t height,
                        eon_challenger* challenger, uint32_t max_constraint_degree,
                        const eon_collective* shard, eon_proof* out, eon_fr* alpha_out, eon_fr* zeta_out);
+
+/* prove_with_preprocessed (prover.rs:28-512) for ANY AIR given as an eon_air_program (eon.h: the
+ * compiled get_symbolic_constraints DAG) with its public values (host, n_public Fr): the quotient
+ * degree is the program's get_log_quotient_degree (prover.rs:150-157), C = 2^that chunks, the
+ * public values are observed after the trace commitment (prover.rs:208) and read by the
+ * constraints (Entry::Public).  No sharding.  The trace is height x width(prog) on device. */
+int eon_prove_air(eon_kzg_pcs* pcs, const eon_air_program* prog, const eon_fr* trace, uint64_t height,
+                  const eon_fr* publics, uint32_t n_public, const eon_fr* alpha, const eon_fr* zeta,
+                  eon_proof* out);
+int eon_prove_air_fs(eon_kzg_pcs* pcs, const eon_air_program* prog, const eon_fr* trace, uint64_t height,
+                     const eon_fr* publics, uint32_t n_public, eon_challenger* challenger, eon_proof* out,
+                     eon_fr* alpha_out, eon_fr* zeta_out);
 
 uint32_t eon_prove_abi_version(void);
 

@@ -24,7 +24,9 @@ def _points(abi_rows):
     return [O.g1_from_bytes(np.ascontiguousarray(r, dtype=np.uint64).tobytes()) for r in abi_rows]
 
 
-def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1, challenger=None):
+def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1, challenger=None, constraint_fn=None, publics=()):
+    """consts / vl: the Poseidon2-AIR (C restatement of its quotient); or constraint_fn (the
+    signature of pyoracle.quotient_values_fn) for any other AIR, with its public values."""
     n, w = trace.shape[0], trace.shape[1]
     log_n = n.bit_length() - 1
     coeffs = C.idft_batch(trace)  # coset_idft_batch(evals, shift 1) (kzg/src/pcs.rs:242)
@@ -33,10 +35,17 @@ def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1, challenger=None
         for v in (log_n, log_n, 0):
             challenger.observe(v)
         challenger.observe_g1(_points(trace_commit))
+        for v in publics:  # observe_slice(public_values) (prover.rs:208)
+            challenger.observe(v)
         alpha_int = challenger.sample()
     alpha = _lim(alpha_int)
     lde = C.kzg_evaluations_on_domain(coeffs, log_n + log_qd, _lim(O.GENERATOR))
-    qv = C.p2_quotient_values(lde, log_n, log_qd, vl, consts, alpha)
+    if constraint_fn is None:
+        qv = C.p2_quotient_values(lde, log_n, log_qd, vl, consts, alpha)
+    else:
+        rows = [[O.from_mont(O.limbs_to_int([int(v) for v in e])) for e in r] for r in lde]
+        qv = np.stack([_lim(v) for v in O.quotient_values_fn(rows, log_n, log_qd, constraint_fn, alpha_int,
+                                                               list(publics))])
     chunks = 1 << log_qd
     g_q = O.two_adic_generator(log_n + log_qd)
     q_coeffs, quotient_commit = [], []

@@ -471,6 +471,45 @@ def p2_quotient_values(lde_rows, log_n, log_qd, vl, consts, alpha):
     return out
 
 
+def quotient_values_fn(lde_rows, log_n, log_qd, constraint_fn, alpha, publics=()):
+    """quotient_values (eon-uni-stark/src/prover.rs:539-709) for any AIR given as
+    constraint_fn(local, next, (is_first_row, is_last_row, is_transition), publics) -> the
+    assert_zero values in eval order; local = row i, next = row (i + 2^qd) mod Q
+    (vertically_packed_row_pair, matrix/src/lib.rs:392-411); selectors of selectors_on_coset over
+    the quotient domain GENERATOR * K (domain.rs:155-168, 252-292)."""
+    q = 1 << (log_n + log_qd)
+    first, last, trans, inv_van = selectors_on_coset(log_n, log_n + log_qd, GENERATOR)
+    out = []
+    for i in range(q):
+        cs = constraint_fn(lde_rows[i], lde_rows[(i + (1 << log_qd)) % q], (first[i], last[i], trans[i]), publics)
+        acc = 0
+        for c in cs:  # sum_k alpha^(K-1-k) C_k as the folder's running sum
+            acc = (acc * alpha + c) % P
+        out.append(acc * inv_van[i] % P)
+    return out
+
+
+def fib_constraints(local, nxt, sels, publics):
+    """FibonacciAir::eval (eon-uni-stark/tests/fib_air.rs:21-51), written out directly:
+    when_first_row: left = a, right = b; when_transition: right = next.left, left + right =
+    next.right; when_last_row: right = x.  assert_eq(x, y) = x - y, filtered by the selector
+    (eon-air/src/filtered_builder.rs:53-55)."""
+    first, last, trans = sels
+    a, b, x = publics
+    return [first * (local[0] - a) % P, first * (local[1] - b) % P, trans * (local[1] - nxt[0]) % P,
+            trans * (local[0] + local[1] - nxt[1]) % P, last * (local[1] - x) % P]
+
+
+def fib_trace(a, b, n):
+    """generate_trace_rows (fib_air.rs:54-76): rows (left, right), row i = (right, left + right) of
+    row i - 1."""
+    rows = [[a % P, b % P]]
+    for _ in range(1, n):
+        lft, rgt = rows[-1]
+        rows.append([rgt, (lft + rgt) % P])
+    return rows
+
+
 # --- Fiat-Shamir transcript (SURVEY.md 8(f) N2) -------------------------------------------------
 def p2_permute(state, consts):
     """Poseidon2Bn254<3>::permute_mut (poseidon2/src/lib.rs:107-111): mds_light, the initial full

@@ -38,14 +38,17 @@ def fr_limbs(x: int) -> np.ndarray:
     return np.array(O.int_to_limbs(O.to_mont(x % O.P)), dtype=np.uint64)
 
 
-def replay_transcript(challenger: O.DuplexChallenger, log_n: int, trace_commit, quotient_commit):
-    """prover.rs:196-202 (log_ext_degree, log_degree, preprocessed width 0, trace commitment), :300
-    (alpha), :373 (quotient commitment), :416 (zeta).  Commitments are ABI rows (.., 8)."""
+def replay_transcript(challenger: O.DuplexChallenger, log_n: int, trace_commit, quotient_commit, publics=()):
+    """prover.rs:196-202 (log_ext_degree, log_degree, preprocessed width 0, trace commitment),
+    :208 (public values), :300 (alpha), :373 (quotient commitment), :416 (zeta).  Commitments are
+    ABI rows (.., 8)."""
     pts = lambda rows: [O.g1_from_bytes(np.ascontiguousarray(r, dtype=np.uint64).tobytes())  # noqa: E731
                         for r in np.asarray(rows, dtype=np.uint64).reshape(-1, 8)]
     for v in (log_n, log_n, 0):
         challenger.observe(v)
     challenger.observe_g1(pts(trace_commit))
+    for v in publics:
+        challenger.observe(v)
     alpha = challenger.sample()
     challenger.observe_g1(pts(quotient_commit))
     zeta = challenger.sample()
@@ -99,6 +102,16 @@ def ood_check(constraint_fn, local, nxt, quotient_chunks, alpha: int, zeta: int,
     return folded * sels[3] % O.P == quotient
 
 
+def fib_constraint_fn(publics):
+    """FibonacciAir (eon-uni-stark/tests/fib_air.rs:21-51) at the opened point: the selectors of
+    selectors_at_point (is_first_row, is_last_row, is_transition)."""
+
+    def fn(local, nxt, sels):
+        return O.fib_constraints(local, nxt, sels[:3], publics)
+
+    return fn
+
+
 def p2air_constraint_fn(consts_int, vl: int):
     """The (vectorized) Poseidon2-AIR's constraints (poseidon2-air/src/air.rs:108-288, lanes in
     order as vectorized.rs:259-274); no selectors, no next row."""
@@ -146,7 +159,7 @@ def kzg_claims_identity(claims, srs_alpha: int, seed: int = 2024, extra=()) -> b
 
 def verify_kzg_proof(proof, constraint_fn, log_n: int, log_qd: int, srs_alpha: int, alpha: int | None = None,
                      zeta: int | None = None, challenger: O.DuplexChallenger | None = None, trace=None,
-                     seed: int = 2024) -> dict:
+                     seed: int = 2024, publics=()) -> dict:
     """Verify a prove() output.  With `challenger` (a fresh pyoracle.DuplexChallenger with the
     config's permutation) alpha / zeta are re-derived from the transcript; otherwise the given
     ones are used.  `trace`: the (n, w, 4) host trace, for the check against the trace.  Returns
@@ -156,7 +169,7 @@ def verify_kzg_proof(proof, constraint_fn, log_n: int, log_qd: int, srs_alpha: i
     w = tc.shape[0]
     res = {}
     if challenger is not None:
-        alpha, zeta = replay_transcript(challenger, log_n, tc, qc)
+        alpha, zeta = replay_transcript(challenger, log_n, tc, qc, publics)
         res["transcript"] = (proof.alpha, proof.zeta) == (alpha, zeta) if proof.alpha is not None else True
     zeta_next = zeta * O.two_adic_generator(log_n) % O.P
     tr = proof.opened[0]

@@ -48,6 +48,16 @@ class eon_poseidon2_constants(ctypes.Structure):
                 ("beginning", ctypes.c_void_p), ("partial", ctypes.c_void_p), ("ending", ctypes.c_void_p)]
 
 
+class eon_sym_node(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint32), ("a", ctypes.c_uint32), ("b", ctypes.c_uint32)]
+
+
+class eon_air_program_stats(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint32) for k in ("width", "num_public_values", "num_constraints",
+                                               "max_constraint_degree", "num_instructions", "num_registers",
+                                               "num_constants")]
+
+
 class eon_g1_affine(ctypes.Structure):
     _fields_ = [("x", ctypes.c_uint64 * 4), ("y", ctypes.c_uint64 * 4)]
 
@@ -108,6 +118,11 @@ SIGNATURES = {
     "eon_p2air_constraints_per_perm": (_U32, [_P]),
     "eon_p2air_generate_trace_dev": (_INT, [_P, _P, _P, _U64, _P]),
     "eon_p2air_quotient_values_dev": (_INT, [_P, _P, _P, _U32, _U32, _P, _P]),
+    "eon_air_program_create": (_INT, [_P, _P, _U32, _P, _U32, _P, _U32, _U32, _U32, ctypes.POINTER(_P)]),
+    "eon_air_program_destroy": (None, [_P]),
+    "eon_air_program_info": (_INT, [_P, _P]),
+    "eon_air_program_log_quotient_degree": (_U32, [_P, _U32]),
+    "eon_quotient_values_dev": (_INT, [_P, _P, _P, _U32, _U32, _P, _P, _U32, _P]),
     "eon_fr_lincomb_dev": (_INT, [_P, _P, _U32, _U64, _P, _P]),
     "eon_fourstep_twiddle_pack_dev": (_INT, [_P, _P, _U32, _U32, _U64, _U32, _U32, _P]),
 }

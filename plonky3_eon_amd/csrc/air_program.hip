@@ -1,0 +1,498 @@
+// Generic AIR quotient: quotient_values (eon-uni-stark/src/prover.rs:539-709) for ANY AIR whose
+// constraints arrive as the symbolic DAG get_symbolic_constraints returns
+// (eon-uni-stark/src/symbolic_builder.rs:72-126; SymbolicExpression, symbolic_expression.rs:78-145).
+//
+// Host side (eon_air_program_create): the DAG is value-numbered (hash-consing: identical leaves,
+// constants by value, commutative + and * with sorted operands), scheduled constraint by
+// constraint in the folder's order (each constraint's not-yet-computed sub-DAG in post-order, then
+// its ASSERT), and register-allocated by liveness (a register is reused right after its last read).
+// Leaves are operand modes, not instructions: trace column of the local / next row, a constant
+// (program constants, then the public values), a selector.  degree_multiple follows
+// symbolic_expression.rs:171-190, get_log_quotient_degree symbolic_builder.rs:15-43.
+//
+// Device side (k_air_quotient): one thread per quotient-domain row i runs the program with its
+// row window (local = row i, next = row (i + 2^qd) mod Q, vertically_packed_row_pair,
+// matrix/src/lib.rs:392-411), the selectors of selectors_on_coset at i, and the folder's
+// accumulator as a Horner chain acc = acc * alpha + C_k (folder.rs:81-85 with the reversed alpha
+// powers of prover.rs:578-579).  out[i] = acc * inv_vanishing[i] (prover.rs:699).  Every lane of
+// a wave executes the same instruction (uniform program counter: scalar instruction fetch, no
+// divergence); the register file lives in LDS (two 16-byte planes, conflict-free b128 access)
+// sized by the program's register count, or in a global buffer for very large programs.
+#include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <tuple>
+#include <vector>
+
+#include "quotient.h"
+
+using namespace eon;
+
+namespace {
+
+enum : uint32_t { OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_NEG = 3, OP_ASSERT = 4 };
+// operand = mode << 29 | index
+enum : uint32_t { M_REG = 0, M_LOCAL = 1, M_NEXT = 2, M_CONST = 3, M_FIRST = 4, M_LAST = 5, M_TRANS = 6 };
+constexpr uint32_t IDX_MASK = (1u << 29) - 1;
+
+struct Instr {
+    uint32_t op, dst, a, b;
+};
+
+__device__ __forceinline__ Fr ld(const Fr* p) { return ld_pinned(p); }
+
+struct Regs {
+    uint4* base;
+    uint64_t stride;  // uint4 units between planes
+    __device__ __forceinline__ Fr get(uint32_t r) const {
+        const uint4 a = base[(uint64_t)(2 * r) * stride], b = base[(uint64_t)(2 * r + 1) * stride];
+        Fr x;
+        x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
+        x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+        return x;
+    }
+    __device__ __forceinline__ void set(uint32_t r, const Fr& x) const {
+        base[(uint64_t)(2 * r) * stride] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+        base[(uint64_t)(2 * r + 1) * stride] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+    }
+};
+
+struct Window {
+    const Fr* local;
+    const Fr* next;
+    const Fr* table;  // program constants, then public values
+    const Fr* sels;   // is_first_row | is_last_row | is_transition, q each (null if unused)
+    uint64_t row, q;
+};
+
+__device__ __forceinline__ Fr fetch(uint32_t opnd, const Regs& rf, const Window& w) {
+    const uint32_t i = opnd & IDX_MASK;
+    switch (opnd >> 29) {
+        case M_REG: return rf.get(i);
+        case M_LOCAL: return ld(w.local + i);
+        case M_NEXT: return ld(w.next + i);
+        case M_CONST: return ld(w.table + i);
+        case M_FIRST: return ld(w.sels + w.row);
+        case M_LAST: return ld(w.sels + w.q + w.row);
+        default: return ld(w.sels + 2 * w.q + w.row);
+    }
+}
+
+template <bool LDS>
+__global__ void __launch_bounds__(256) k_air_quotient(const Instr* __restrict__ code, uint32_t n_code,
+                                                      const Fr* __restrict__ lde, uint32_t width, uint64_t q,
+                                                      uint64_t next_step, const Fr* __restrict__ table,
+                                                      const Fr* __restrict__ sels, const Fr* __restrict__ inv_van,
+                                                      uint32_t nr_mask, Fr alpha, Fr* __restrict__ out,
+                                                      uint4* __restrict__ gregs) {
+    extern __shared__ uint4 lds_regs[];
+    const uint64_t row = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= q) return;
+    Regs rf;
+    if (LDS) {
+        rf.base = lds_regs + threadIdx.x;
+        rf.stride = blockDim.x;
+    } else {
+        rf.base = gregs + row;
+        rf.stride = q;
+    }
+    Window w{lde + row * width, lde + ((row + next_step) & (q - 1)) * width, table, sels, row, q};
+    Fr acc = Fr::zero();
+    for (uint32_t pc = 0; pc < n_code; pc++) {
+        const Instr in = code[pc];
+        const Fr x = fetch(in.a, rf, w);
+        Fr r;
+        if (in.op == OP_ASSERT) {
+            acc = add(mul(acc, alpha), x);  // folder.rs:81-85, alpha powers reversed
+            continue;
+        } else if (in.op == OP_NEG) {
+            r = neg(x);
+        } else {
+            const Fr y = fetch(in.b, rf, w);
+            if (in.op == OP_MUL)
+                r = mul(x, y);
+            else if (in.op == OP_ADD)
+                r = add(x, y);
+            else
+                r = sub(x, y);
+        }
+        rf.set(in.dst, r);
+    }
+    st_vec(out + row, mul(acc, ld(inv_van + (row & nr_mask))));  // prover.rs:699
+}
+
+}  // namespace
+
+struct eon_air_program {
+    eon_ctx* ctx = nullptr;
+    uint32_t width = 0, n_public = 0, n_constraints = 0, max_degree = 0, n_regs = 0, n_consts = 0;
+    bool uses_sels = false;
+    std::vector<Instr> code;
+    std::vector<Fr> consts;
+    DevBuf d_code, d_table, d_sels, d_regs;
+    std::vector<Fr> staged;  // host copy of the table for the current launch
+};
+
+namespace {
+
+int finish(eon_ctx* ctx, const Status& s) {
+    if (s.bad()) ctx->last_error = s.msg;
+    return s.code;
+}
+
+struct Leaf {
+    uint32_t kind, a, b;
+};
+
+// compile nodes -> program; see the file comment
+Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, const eon_fr* consts,
+               uint32_t n_consts, const uint32_t* roots, uint32_t n_roots) {
+    // value numbering
+    std::vector<uint32_t> vn(n_nodes);
+    std::vector<uint32_t> degree(n_nodes);
+    struct Val {
+        uint32_t op;            // OP_* for computed values, ~0u for leaves
+        uint32_t a, b;          // operand value numbers (computed) / operand code (leaf)
+    };
+    std::vector<Val> vals;
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> memo;
+    std::map<std::vector<uint32_t>, uint32_t> const_slot;  // canonical limbs -> table index
+    auto intern = [&](uint32_t op, uint32_t a, uint32_t b) -> uint32_t {
+        auto key = std::make_tuple(op, a, b);
+        auto it = memo.find(key);
+        if (it != memo.end()) return it->second;
+        const uint32_t id = (uint32_t)vals.size();
+        vals.push_back({op, a, b});
+        memo.emplace(key, id);
+        return id;
+    };
+    constexpr uint32_t LEAF = ~0u;
+    for (uint32_t i = 0; i < n_nodes; i++) {
+        const eon_sym_node& nd = nodes[i];
+        auto operand = [&](uint32_t j) -> Status {
+            if (j >= i) return Status::err(EON_E_ARG, "node " + std::to_string(i) + ": operand must precede it");
+            return Status::ok();
+        };
+        switch (nd.kind) {
+            case EON_SYM_CONSTANT: {
+                if (nd.a >= n_consts) return Status::err(EON_E_ARG, "constant index out of range");
+                const Fr c = fr_from_abi(&consts[nd.a]);
+                if (!fr_is_canonical(c)) return Status::err(EON_E_ARG, "constant is not a canonical Fr");
+                std::vector<uint32_t> key(c.v, c.v + 8);
+                auto it = const_slot.find(key);
+                uint32_t slot;
+                if (it == const_slot.end()) {
+                    slot = (uint32_t)p->consts.size();
+                    p->consts.push_back(c);
+                    const_slot.emplace(key, slot);
+                } else {
+                    slot = it->second;
+                }
+                vn[i] = intern(LEAF, M_CONST << 29 | slot, 0);
+                degree[i] = 0;
+                break;
+            }
+            case EON_SYM_MAIN:
+                if (nd.a >= p->width || nd.b > 1) return Status::err(EON_E_ARG, "main variable out of range");
+                vn[i] = intern(LEAF, (nd.b ? M_NEXT : M_LOCAL) << 29 | nd.a, 0);
+                degree[i] = 1;
+                break;
+            case EON_SYM_PUBLIC:
+                if (nd.a >= p->n_public) return Status::err(EON_E_ARG, "public value index out of range");
+                vn[i] = intern(LEAF, 0xffffffffu, nd.a);  // resolved to a table slot below
+                degree[i] = 0;
+                break;
+            case EON_SYM_IS_FIRST_ROW:
+            case EON_SYM_IS_LAST_ROW:
+            case EON_SYM_IS_TRANSITION: {
+                const uint32_t m = nd.kind == EON_SYM_IS_FIRST_ROW ? M_FIRST
+                                   : nd.kind == EON_SYM_IS_LAST_ROW ? M_LAST : M_TRANS;
+                vn[i] = intern(LEAF, m << 29, 0);
+                degree[i] = nd.kind == EON_SYM_IS_TRANSITION ? 0 : 1;
+                break;
+            }
+            case EON_SYM_ADD:
+            case EON_SYM_MUL: {
+                EON_TRY(operand(nd.a));
+                EON_TRY(operand(nd.b));
+                uint32_t x = vn[nd.a], y = vn[nd.b];
+                if (x > y) std::swap(x, y);  // commutative
+                vn[i] = intern(nd.kind == EON_SYM_ADD ? OP_ADD : OP_MUL, x, y);
+                degree[i] = nd.kind == EON_SYM_ADD ? std::max(degree[nd.a], degree[nd.b])
+                                                   : degree[nd.a] + degree[nd.b];
+                break;
+            }
+            case EON_SYM_SUB:
+                EON_TRY(operand(nd.a));
+                EON_TRY(operand(nd.b));
+                vn[i] = intern(OP_SUB, vn[nd.a], vn[nd.b]);
+                degree[i] = std::max(degree[nd.a], degree[nd.b]);
+                break;
+            case EON_SYM_NEG:
+                EON_TRY(operand(nd.a));
+                vn[i] = intern(OP_NEG, vn[nd.a], 0);
+                degree[i] = degree[nd.a];
+                break;
+            case EON_SYM_PREPROCESSED:
+            case EON_SYM_PERMUTATION:
+            case EON_SYM_CHALLENGE:
+                return Status::err(EON_E_ARG, "preprocessed / permutation (LogUp) / challenge variables are not "
+                                              "supported by the generic quotient program");
+            default:
+                return Status::err(EON_E_ARG, "unknown node kind " + std::to_string(nd.kind));
+        }
+    }
+    p->n_consts = (uint32_t)p->consts.size();
+    // public values occupy the table slots after the constants
+    for (auto& v : vals)
+        if (v.op == LEAF && v.a == 0xffffffffu) v.a = M_CONST << 29 | (p->n_consts + v.b);
+    for (auto& v : vals)
+        if (v.op == LEAF) {
+            const uint32_t m = v.a >> 29;
+            if (m == M_FIRST || m == M_LAST || m == M_TRANS) p->uses_sels = true;
+        }
+    p->max_degree = 0;
+    for (uint32_t k = 0; k < n_roots; k++) {
+        if (roots[k] >= n_nodes) return Status::err(EON_E_ARG, "constraint index out of range");
+        p->max_degree = std::max(p->max_degree, degree[roots[k]]);
+    }
+    // schedule: per constraint, post-order of its not-yet-emitted values, then ASSERT
+    const uint32_t nv = (uint32_t)vals.size();
+    std::vector<uint32_t> order;  // emitted computed values
+    std::vector<char> done(nv, 0);
+    std::vector<std::pair<uint32_t, uint32_t>> asserts;  // (position in order, value)
+    for (uint32_t k = 0; k < n_roots; k++) {
+        std::vector<std::pair<uint32_t, bool>> st{{vn[roots[k]], false}};
+        while (!st.empty()) {
+            auto [v, ready] = st.back();
+            st.pop_back();
+            if (done[v] || vals[v].op == LEAF) continue;
+            if (!ready) {
+                st.push_back({v, true});
+                const uint32_t kids[2] = {vals[v].a, vals[v].op == OP_NEG ? LEAF : vals[v].b};
+                for (int t = 1; t >= 0; t--)
+                    if (kids[t] != LEAF && !done[kids[t]] && vals[kids[t]].op != LEAF) st.push_back({kids[t], false});
+                continue;
+            }
+            done[v] = 1;
+            order.push_back(v);
+        }
+        asserts.push_back({(uint32_t)order.size(), vn[roots[k]]});
+    }
+    // instruction stream: computed values interleaved with asserts
+    struct Item {
+        bool assert_;
+        uint32_t v;
+    };
+    std::vector<Item> items;
+    {
+        size_t ai = 0;
+        for (uint32_t pos = 0; pos <= order.size(); pos++) {
+            while (ai < asserts.size() && asserts[ai].first == pos) items.push_back({true, asserts[ai++].second});
+            if (pos < order.size()) items.push_back({false, order[pos]});
+        }
+    }
+    // liveness: last read of each computed value
+    std::vector<int64_t> last(nv, -1);
+    for (size_t t = 0; t < items.size(); t++) {
+        const Item& it = items[t];
+        if (it.assert_) {
+            last[it.v] = (int64_t)t;
+        } else {
+            const Val& x = vals[it.v];
+            last[x.a] = (int64_t)t;
+            if (x.op != OP_NEG) last[x.b] = (int64_t)t;
+        }
+    }
+    // register allocation (lowest free register; operands freed before the result is assigned)
+    std::vector<uint32_t> reg(nv, ~0u);
+    std::vector<uint32_t> free_regs;
+    uint32_t n_regs = 0;
+    auto opnd = [&](uint32_t v) { return vals[v].op == LEAF ? vals[v].a : (M_REG << 29 | reg[v]); };
+    auto release = [&](uint32_t v, size_t t) {
+        if (vals[v].op != LEAF && last[v] == (int64_t)t && reg[v] != ~0u) {
+            free_regs.push_back(reg[v]);
+            std::sort(free_regs.begin(), free_regs.end(), std::greater<uint32_t>());
+        }
+    };
+    for (size_t t = 0; t < items.size(); t++) {
+        const Item& it = items[t];
+        if (it.assert_) {
+            p->code.push_back({OP_ASSERT, 0, opnd(it.v), 0});
+            release(it.v, t);
+            continue;
+        }
+        const Val& x = vals[it.v];
+        Instr in{x.op, 0, opnd(x.a), x.op == OP_NEG ? 0u : opnd(x.b)};
+        release(x.a, t);
+        if (x.op != OP_NEG && x.b != x.a) release(x.b, t);
+        if (last[it.v] < 0) continue;  // never read (cannot happen for reachable values)
+        uint32_t r;
+        if (!free_regs.empty()) {
+            r = free_regs.back();
+            free_regs.pop_back();
+        } else {
+            r = n_regs++;
+        }
+        reg[it.v] = r;
+        in.dst = r;
+        p->code.push_back(in);
+    }
+    p->n_regs = n_regs;
+    return Status::ok();
+}
+
+}  // namespace
+
+extern "C" {
+
+int eon_air_program_create(eon_ctx* ctx, const eon_sym_node* nodes, uint32_t n_nodes, const eon_fr* consts,
+                           uint32_t n_consts, const uint32_t* constraints, uint32_t n_constraints, uint32_t width,
+                           uint32_t n_public, eon_air_program** out) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    Status s = [&]() -> Status {
+        if (!out || (n_nodes && !nodes) || (n_consts && !consts) || (n_constraints && !constraints))
+            return Status::err(EON_E_ARG, "null argument");
+        auto* p = new eon_air_program();
+        p->ctx = ctx;
+        p->width = width;
+        p->n_public = n_public;
+        p->n_constraints = n_constraints;
+        Status c = compile(p, nodes, n_nodes, consts, n_consts, constraints, n_constraints);
+        if (c.bad()) {
+            delete p;
+            return c;
+        }
+        hipError_t e = p->d_code.ensure(std::max<size_t>(1, p->code.size()) * sizeof(Instr));
+        if (e == hipSuccess && !p->code.empty())
+            e = hipMemcpy(p->d_code.p, p->code.data(), p->code.size() * sizeof(Instr), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = p->d_table.ensure(std::max<size_t>(1, p->n_consts + n_public) * sizeof(Fr));
+        if (e != hipSuccess) {
+            p->d_code.release();
+            p->d_table.release();
+            delete p;
+            EON_HIP(e);
+        }
+        *out = p;
+        return Status::ok();
+    }();
+    return finish(ctx, s);
+}
+
+void eon_air_program_destroy(eon_air_program* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(p->ctx->mu);
+    (void)hipSetDevice(p->ctx->device);
+    (void)hipStreamSynchronize(p->ctx->stream);
+    for (DevBuf* b : {&p->d_code, &p->d_table, &p->d_sels, &p->d_regs}) b->release();
+    delete p;
+}
+
+int eon_air_program_info(const eon_air_program* p, eon_air_program_stats* out) {
+    if (!p || !out) return EON_E_ARG;
+    out->width = p->width;
+    out->num_public_values = p->n_public;
+    out->num_constraints = p->n_constraints;
+    out->max_constraint_degree = p->max_degree;
+    out->num_instructions = (uint32_t)p->code.size();
+    out->num_registers = p->n_regs;
+    out->num_constants = p->n_consts;
+    return EON_OK;
+}
+
+uint32_t eon_air_program_log_quotient_degree(const eon_air_program* p, uint32_t is_zk) {
+    // symbolic_builder.rs:28-42: log2_ceil(max(max_degree + is_zk, 2) - 1)
+    if (!p) return 0;
+    const uint32_t d = std::max<uint32_t>(p->max_degree + (is_zk ? 1 : 0), 2) - 1;
+    uint32_t b = 0;
+    while ((1u << b) < d) b++;
+    return b;
+}
+
+int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const eon_fr* lde, uint32_t log_n,
+                            uint32_t log_qd, const eon_fr* alpha, const eon_fr* publics, uint32_t n_public,
+                            eon_fr* out) {
+    if (!ctx || !prog_c) return EON_E_ARG;
+    auto* prog = const_cast<eon_air_program*>(prog_c);  // device scratch only
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    Status s = [&]() -> Status {
+        if (!lde || !alpha || !out || (n_public && !publics)) return Status::err(EON_E_ARG, "null argument");
+        if (prog->ctx != ctx) return Status::err(EON_E_ARG, "program belongs to another context");
+        if (n_public != prog->n_public)
+            return Status::err(EON_E_SHAPE, "public value count differs from the program's");
+        const uint32_t log_q = log_n + log_qd;
+        EON_TRY(check_domains(log_n, log_q));
+        const Fr al = fr_from_abi(alpha);
+        if (!fr_is_canonical(al)) return Status::err(EON_E_ARG, "alpha is not a canonical Fr");
+        const uint64_t q = 1ull << log_q;
+        // constant table = program constants ++ public values
+        prog->staged.assign(prog->consts.begin(), prog->consts.end());
+        for (uint32_t i = 0; i < n_public; i++) {
+            const Fr v = fr_from_abi(&publics[i]);
+            if (!fr_is_canonical(v)) return Status::err(EON_E_ARG, "public value is not a canonical Fr");
+            prog->staged.push_back(v);
+        }
+        if (!prog->staged.empty()) {
+            EON_HIP(hipMemcpyAsync(prog->d_table.p, prog->staged.data(), prog->staged.size() * sizeof(Fr),
+                                   hipMemcpyHostToDevice, ctx->stream));
+            EON_HIP(hipStreamSynchronize(ctx->stream));  // `staged` is reused by the next launch
+        }
+        // quotient domain = trace domain (shift 1).create_disjoint_domain: shift GENERATOR
+        // (commit/src/domain.rs:155-168); selectors_on_coset over it (prover.rs:563-564)
+        const Fr g5 = from_u64<FrP>(5);
+        const Fr* inv_van;
+        if (prog->uses_sels) {
+            EON_HIP(prog->d_sels.ensure(4 * q * sizeof(Fr)));
+            EON_TRY(selectors_launch(ctx, log_n, log_q, g5, prog->d_sels.as<Fr>()));
+            inv_van = prog->d_sels.as<Fr>() + 3 * q;
+        } else {
+            Fr *zh, *zh_inv;
+            EON_TRY(vanishing_table(ctx, log_n, log_q, g5, &zh, &zh_inv));
+            inv_van = zh_inv;
+        }
+        const uint32_t nr_mask = prog->uses_sels ? (uint32_t)(q - 1) : (1u << log_qd) - 1;
+        // register file: LDS (block size shrinks with the register count), or global
+        static const bool force_global = [] {
+            const char* e = getenv("EON_AIR_REGS");
+            return e && std::string(e) == "global";
+        }();
+        const uint64_t per_thread = (uint64_t)prog->n_regs * sizeof(Fr);
+        uint32_t block = 256;
+        while (block > 64 && block * per_thread > 64 * 1024) block /= 2;
+        const bool lds = !force_global && block * per_thread <= 160 * 1024;
+        if (!lds) block = 256;
+        if (!lds) EON_HIP(prog->d_regs.ensure(std::max<uint64_t>(1, q * per_thread)));
+        const unsigned grid = (unsigned)((q + block - 1) / block);
+        const size_t shmem = lds ? (size_t)block * per_thread : 0;
+        const uint64_t mulmods = q * (uint64_t)(prog->code.size() + 1);
+        ctx->prof.begin("k_air_quotient", q * (uint64_t)prog->width * 32 + q * 32, ctx->stream, mulmods);
+        if (lds) {
+            static bool attr = false;
+            if (!attr) {
+                EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_air_quotient<true>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                attr = true;
+            }
+            hipLaunchKernelGGL(k_air_quotient<true>, dim3(grid), dim3(block), shmem, ctx->stream,
+                               prog->d_code.as<Instr>(), (uint32_t)prog->code.size(), reinterpret_cast<const Fr*>(lde),
+                               prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(),
+                               prog->uses_sels ? prog->d_sels.as<Fr>() : nullptr, inv_van, nr_mask, al,
+                               reinterpret_cast<Fr*>(out), nullptr);
+        } else {
+            hipLaunchKernelGGL(k_air_quotient<false>, dim3(grid), dim3(block), 0, ctx->stream,
+                               prog->d_code.as<Instr>(), (uint32_t)prog->code.size(), reinterpret_cast<const Fr*>(lde),
+                               prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(),
+                               prog->uses_sels ? prog->d_sels.as<Fr>() : nullptr, inv_van, nr_mask, al,
+                               reinterpret_cast<Fr*>(out), prog->d_regs.as<uint4>());
+        }
+        ctx->prof.end(ctx->stream);
+        EON_HIP(hipGetLastError());
+        return Status::ok();
+    }();
+    return finish(ctx, s);
+}
+
+}  // extern "C"

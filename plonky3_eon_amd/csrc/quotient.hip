@@ -11,7 +11,7 @@
 // acc = acc * alpha + C_k in constraint order, so no alpha-power table is read.  One thread owns
 // one (row, vector lane) pair; the VECTOR_LEN lanes of a row are adjacent threads and are
 // combined as sum_v P_v * alpha^(160 * (VL - 1 - v)) through LDS.
-#include "context.h"
+#include "quotient.h"
 #include <vector>
 
 using namespace eon;
@@ -247,6 +247,18 @@ Status check_domains(uint32_t log_n, uint32_t log_q) {
     return Status::ok();
 }
 
+Status selectors_launch(eon_ctx* ctx, uint32_t log_n, uint32_t log_q, const Fr& sh, Fr* o) {
+    Fr *zh, *zh_inv;
+    EON_TRY(vanishing_table(ctx, log_n, log_q, sh, &zh, &zh_inv));
+    const uint64_t q = 1ull << log_q;
+    const uint64_t threads = (q + SEL_CHUNK - 1) / SEL_CHUNK;
+    hipLaunchKernelGGL(k_selectors, dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, ctx->stream, q, sh,
+                       fr_two_adic_generator(log_q), inverse(fr_two_adic_generator(log_n)), zh, zh_inv,
+                       (1u << (log_q - log_n)) - 1, o, o + q, o + 2 * q, o + 3 * q);
+    EON_HIP(hipGetLastError());
+    return Status::ok();
+}
+
 }  // namespace eon
 
 namespace {
@@ -285,16 +297,7 @@ int eon_selectors_on_coset_dev(eon_ctx* ctx, uint32_t log_n, uint32_t log_q, con
         if (!fr_is_canonical(sh)) return Status::err(EON_E_ARG, "shift is not a canonical Fr");
         // selectors_on_coset asserts coset.shift != 1 (domain.rs:254)
         if (sh == Fr::one()) return Status::err(EON_E_ARG, "coset shift must not be ONE");
-        Fr *zh, *zh_inv;
-        EON_TRY(vanishing_table(ctx, log_n, log_q, sh, &zh, &zh_inv));
-        const uint64_t q = 1ull << log_q;
-        Fr* o = reinterpret_cast<Fr*>(out);
-        const uint64_t threads = (q + SEL_CHUNK - 1) / SEL_CHUNK;
-        hipLaunchKernelGGL(k_selectors, dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, ctx->stream,
-                           q, sh, fr_two_adic_generator(log_q), inverse(fr_two_adic_generator(log_n)),
-                           zh, zh_inv, (1u << (log_q - log_n)) - 1, o, o + q, o + 2 * q, o + 3 * q);
-        EON_HIP(hipGetLastError());
-        return Status::ok();
+        return selectors_launch(ctx, log_n, log_q, sh, reinterpret_cast<Fr*>(out));
     }();
     return finish(ctx, s);
 }

@@ -41,7 +41,7 @@ void copy_out(const eon_host::Proof& p, eon_proof* out);
 
 extern "C" {
 
-uint32_t eon_prove_abi_version(void) { return 2; }
+uint32_t eon_prove_abi_version(void) { return 3; }
 
 int eon_kzg_pcs_create(eon_ctx* ctx, uint64_t max_degree, const eon_fr* srs_alpha, eon_kzg_pcs** out) {
     if (!ctx || !srs_alpha || !out) return EON_E_ARG;
@@ -132,9 +132,50 @@ int eon_prove_p2air(eon_kzg_pcs* pcs, const eon_p2air* air, const eon_fr* trace,
         return EON_E_ARG;
     return guarded(pcs, [&] {
         using namespace eon_host;
-        Proof p = prove(*pcs->pcs, air, trace, height, Fr::from_abi(*alpha), Fr::from_abi(*zeta),
+        AirRef a;
+        a.p2 = air;
+        Proof p = prove(*pcs->pcs, a, trace, height, Fr::from_abi(*alpha), Fr::from_abi(*zeta),
                         max_constraint_degree, shard);
         copy_out(p, out);
+    });
+}
+
+int eon_prove_air(eon_kzg_pcs* pcs, const eon_air_program* prog, const eon_fr* trace, uint64_t height,
+                  const eon_fr* publics, uint32_t n_public, const eon_fr* alpha, const eon_fr* zeta,
+                  eon_proof* out) {
+    if (!pcs || !pcs->pcs || !prog || !trace || !alpha || !zeta || !out || (n_public && !publics))
+        return EON_E_ARG;
+    if (!out->trace_commit || !out->quotient_commit || !out->trace_opened || !out->trace_witnesses ||
+        !out->quotient_opened || !out->quotient_witnesses)
+        return EON_E_ARG;
+    return guarded(pcs, [&] {
+        using namespace eon_host;
+        AirRef a;
+        a.prog = prog;
+        a.publics = publics;
+        a.n_public = n_public;
+        Proof p = prove(*pcs->pcs, a, trace, height, Fr::from_abi(*alpha), Fr::from_abi(*zeta), 0, nullptr);
+        copy_out(p, out);
+    });
+}
+
+int eon_prove_air_fs(eon_kzg_pcs* pcs, const eon_air_program* prog, const eon_fr* trace, uint64_t height,
+                     const eon_fr* publics, uint32_t n_public, eon_challenger* challenger, eon_proof* out,
+                     eon_fr* alpha_out, eon_fr* zeta_out) {
+    if (!pcs || !pcs->pcs || !prog || !trace || !challenger || !out || (n_public && !publics)) return EON_E_ARG;
+    if (!out->trace_commit || !out->quotient_commit || !out->trace_opened || !out->trace_witnesses ||
+        !out->quotient_opened || !out->quotient_witnesses)
+        return EON_E_ARG;
+    return guarded(pcs, [&] {
+        using namespace eon_host;
+        AirRef a;
+        a.prog = prog;
+        a.publics = publics;
+        a.n_public = n_public;
+        Proof p = prove(*pcs->pcs, a, trace, height, Fr::zero(), Fr::zero(), 0, nullptr, &challenger->ch);
+        copy_out(p, out);
+        if (alpha_out) *alpha_out = p.alpha.abi();
+        if (zeta_out) *zeta_out = p.zeta.abi();
     });
 }
 
@@ -147,7 +188,9 @@ int eon_prove_p2air_fs(eon_kzg_pcs* pcs, const eon_p2air* air, const eon_fr* tra
         return EON_E_ARG;
     return guarded(pcs, [&] {
         using namespace eon_host;
-        Proof p = prove(*pcs->pcs, air, trace, height, Fr::zero(), Fr::zero(), max_constraint_degree, shard,
+        AirRef a;
+        a.p2 = air;
+        Proof p = prove(*pcs->pcs, a, trace, height, Fr::zero(), Fr::zero(), max_constraint_degree, shard,
                         &challenger->ch);
         copy_out(p, out);
         if (alpha_out) *alpha_out = p.alpha.abi();

@@ -45,7 +45,14 @@ void hip_ok(hipError_t e, const char* what) {
 
 }  // namespace
 
-Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t height, const Fr& alpha_in,
+uint32_t AirRef::width() const {
+    if (p2) return eon_p2air_width(p2);
+    eon_air_program_stats st{};
+    if (prog && eon_air_program_info(prog, &st) == EON_OK) return st.width;
+    return 0;
+}
+
+Proof prove(KzgPcs& pcs, const AirRef& air, const eon_fr* trace, uint64_t height, const Fr& alpha_in,
             const Fr& zeta_in, uint32_t max_constraint_degree, const eon_collective* shard,
             DuplexChallenger* challenger) {
     eon_ctx* ctx = pcs.ctx();
@@ -58,16 +65,22 @@ Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t hei
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
     if (height == 0 || (height & (height - 1))) throw Error(EON_E_SHAPE, "trace height must be a power of two");
-    const uint32_t width = eon_p2air_width(air);
-    const uint32_t local_vl = eon_p2air_vector_len(air);
-    const uint32_t k_lane = eon_p2air_constraints_per_perm(air);
+    if ((air.p2 == nullptr) == (air.prog == nullptr)) throw Error(EON_E_ARG, "exactly one of p2air / program");
+    if (air.n_public && !air.publics) throw Error(EON_E_ARG, "null public values");
+    if (air.p2 && air.n_public) throw Error(EON_E_SHAPE, "the Poseidon2-AIR has no public values");
+    const uint32_t width = air.width();
+    const uint32_t local_vl = air.p2 ? eon_p2air_vector_len(air.p2) : 1;
+    const uint32_t k_lane = air.p2 ? eon_p2air_constraints_per_perm(air.p2) : 0;
     if (shard && shard->world <= 1) shard = nullptr;
     if (shard && (!shard->all_gather || shard->rank >= shard->world))
         throw Error(EON_E_ARG, "invalid collective");
+    if (shard && !air.p2) throw Error(EON_E_ARG, "lane sharding needs the (vectorized) Poseidon2-AIR");
     const uint32_t world = shard ? shard->world : 1, rank = shard ? shard->rank : 0;
     const uint32_t vector_len = local_vl * world;
     const uint32_t log_n = 63 - __builtin_clzll(height);
-    const uint32_t log_qd = log_quotient_degree(max_constraint_degree);
+    // get_log_quotient_degree (prover.rs:150-157): the program's own constraint degrees
+    const uint32_t log_qd =
+        air.prog ? eon_air_program_log_quotient_degree(air.prog, 0) : log_quotient_degree(max_constraint_degree);
     const uint32_t num_chunks = 1u << log_qd;
     hipStream_t st = static_cast<hipStream_t>(eon_ctx_stream(ctx));
 
@@ -143,7 +156,9 @@ Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t hei
             challenger->observe(fr_from_u64(log_n));  // log_degree
             challenger->observe(fr_from_u64(0));      // preprocessed width
             challenger->observe_g1(full_commit.data(), full_commit.size());
-            alpha = challenger->sample();  // no public values, no lookups
+            for (uint32_t i = 0; i < air.n_public; i++)  // observe_slice(public_values), prover.rs:208
+                challenger->observe(Fr::from_abi(air.publics[i]));
+            alpha = challenger->sample();  // no lookups
         });
     }
     if (!(overlap && pcs.aux_ctx())) {
@@ -159,8 +174,14 @@ Proof prove(KzgPcs& pcs, const eon_p2air* air, const eon_fr* trace, uint64_t hei
     {
         t2 = tick();
         const eon_fr a = alpha.abi();
-        check(ctx, eon_p2air_quotient_values_dev(ctx, air, lde.data(), log_n, log_qd, &a, qv.mutable_data()),
-              "quotient_values");
+        if (air.p2)
+            check(ctx, eon_p2air_quotient_values_dev(ctx, air.p2, lde.data(), log_n, log_qd, &a, qv.mutable_data()),
+                  "quotient_values");
+        else
+            check(ctx,
+                  eon_quotient_values_dev(ctx, air.prog, lde.data(), log_n, log_qd, &a, air.publics, air.n_public,
+                                          qv.mutable_data()),
+                  "quotient_values");
     }
     check(ctx, eon_ctx_synchronize(ctx), "quotient_values");
     lde = DeviceMatrix();  // back to the buffer cache before the opening

@@ -70,6 +70,8 @@ SIGNATURES = {
     "eon_challenger_state": (_INT, [_P, _P]),
     "eon_prove_p2air_fs": (_INT, [_P, _P, _P, _U64, _P, _U32, ctypes.POINTER(eon_collective),
                                   ctypes.POINTER(eon_proof), _P, _P]),
+    "eon_prove_air": (_INT, [_P, _P, _P, _U64, _P, _U32, _P, _P, ctypes.POINTER(eon_proof)]),
+    "eon_prove_air_fs": (_INT, [_P, _P, _P, _U64, _P, _U32, _P, ctypes.POINTER(eon_proof), _P, _P]),
 }
 
 _plib = None
@@ -274,14 +276,21 @@ class Challenger:
 
 
 def prove_native(air, pcs: NativeKzgPcs, trace, alpha: int | None, zeta: int | None,
-                 max_constraint_degree: int = 3, collective=None, challenger: Challenger | None = None) -> Proof:
-    """prover.prove through the C++ driver.  `trace`: (N, width, 4) device tensor; with a
-    collective (world > 1) `air`/`trace` are this rank's lanes and the proof is the full one.
-    With `challenger` (eon_prove_p2air_fs) alpha and zeta are sampled from the transcript and
-    returned in proof.alpha / proof.zeta (canonical ints); the arguments are ignored."""
+                 max_constraint_degree: int = 3, collective=None, challenger: Challenger | None = None,
+                 public_values=()) -> Proof:
+    """prover.prove through the C++ driver.  `air` is a Poseidon2Air (fused quotient kernel) or an
+    air.AirProgram (any AIR, with `public_values`: canonical ints).  `trace`: (N, width, 4) device
+    tensor; with a collective (world > 1, Poseidon2 only) `air`/`trace` are this rank's lanes and
+    the proof is the full one.  With `challenger` (eon_prove_*_fs) alpha and zeta are sampled from
+    the transcript and returned in proof.alpha / proof.zeta (canonical ints); the arguments are
+    ignored."""
+    from .air import AirProgram, _publics_limbs
+
+    generic = isinstance(air, AirProgram)
     world = collective.c.world if collective is not None else 1
     w = air.width * world
-    chunks = 1 << log_quotient_degree(max_constraint_degree)
+    log_qd = air.log_quotient_degree() if generic else log_quotient_degree(max_constraint_degree)
+    chunks = 1 << log_qd
     tc = np.zeros((w, 8), np.uint64)
     qc = np.zeros((chunks, 8), np.uint64)
     to = np.zeros((2, w, 4), np.uint64)
@@ -295,16 +304,30 @@ def prove_native(air, pcs: NativeKzgPcs, trace, alpha: int | None, zeta: int | N
     torch.cuda.synchronize(t.device)  # the trace was produced on torch's stream
     pcs.ctx.set_stream(None)
     coll = ctypes.byref(collective.c) if collective is not None else None
+    pub = _publics_limbs(public_values)
+    npub = len(public_values)
+    if not generic and npub:
+        raise ValueError("the Poseidon2-AIR has no public values")
+    tp = ctypes.c_void_p(t.data_ptr())
     if challenger is None:
         a, z = fr_to_abi(alpha), fr_to_abi(zeta)
-        pcs.check(pcs.lib.eon_prove_p2air(pcs._h, air.handle, ctypes.c_void_p(t.data_ptr()), int(t.shape[0]),
-                                          ctypes.byref(a), ctypes.byref(z), max_constraint_degree, coll,
-                                          ctypes.byref(out)))
+        if generic:
+            pcs.check(pcs.lib.eon_prove_air(pcs._h, air.handle, tp, int(t.shape[0]), _p(pub), npub, ctypes.byref(a),
+                                            ctypes.byref(z), ctypes.byref(out)))
+        else:
+            pcs.check(pcs.lib.eon_prove_p2air(pcs._h, air.handle, tp, int(t.shape[0]), ctypes.byref(a),
+                                              ctypes.byref(z), max_constraint_degree, coll, ctypes.byref(out)))
     else:
         a_out, z_out = np.zeros(4, np.uint64), np.zeros(4, np.uint64)
-        pcs.check(pcs.lib.eon_prove_p2air_fs(pcs._h, air.handle, ctypes.c_void_p(t.data_ptr()), int(t.shape[0]),
-                                             challenger.handle, max_constraint_degree, coll, ctypes.byref(out),
-                                             _p(a_out), _p(z_out)))
+        if generic:
+            if collective is not None:
+                raise ValueError("the generic AIR path is not lane-sharded")
+            pcs.check(pcs.lib.eon_prove_air_fs(pcs._h, air.handle, tp, int(t.shape[0]), _p(pub), npub,
+                                               challenger.handle, ctypes.byref(out), _p(a_out), _p(z_out)))
+        else:
+            pcs.check(pcs.lib.eon_prove_p2air_fs(pcs._h, air.handle, tp, int(t.shape[0]), challenger.handle,
+                                                 max_constraint_degree, coll, ctypes.byref(out), _p(a_out),
+                                                 _p(z_out)))
         alpha = fr_unmont(sum(int(v) << (64 * i) for i, v in enumerate(a_out)))
         zeta = fr_unmont(sum(int(v) << (64 * i) for i, v in enumerate(z_out)))
     opened_trace = Opened(values=[[to[0], to[1]]], witnesses=[[tw[0], tw[1]]])

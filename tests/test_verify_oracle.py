@@ -79,3 +79,19 @@ def test_rejects_tampered(setup, what):
         p.quotient_commit[0] = C.g1_add(np.asarray(p.quotient_commit[0]).reshape(8), C.g1_generator())
     res = _verify(setup, p)
     assert not all(res.values()), res
+
+
+@pytest.mark.parametrize("n,x,ok", [(1, 1, True), (8, 21, True), (8, 123123, False)])
+def test_fibonacci_oracle_prove_verifies(n, x, ok):
+    """fib_air.rs:112-155 on the CPU restatement: prove + verify for n = 1 and 8 with publics
+    (0, 1, F_n); the incorrect public value yields a proof whose OOD identity fails."""
+    chc = O.p2_constants(77, 4, 22)
+    pis = [0, 1, x]
+    trace = np.stack([np.stack([lim(v) for v in r]) for r in O.fib_trace(0, 1, n)])
+    srs = C.g1_srs(1025, C.fr_from_u64(12345))
+    d = prove_oracle.prove(trace, srs, None, None, None, None, log_qd=0, challenger=O.DuplexChallenger(chc),
+                           constraint_fn=O.fib_constraints, publics=pis)
+    res = V.verify_kzg_proof(V.proof_from_oracle(d), V.fib_constraint_fn(pis), n.bit_length() - 1, 0, 12345,
+                             challenger=O.DuplexChallenger(chc), trace=trace, publics=pis)
+    assert res["transcript"] and res["kzg"] and res["opened_vs_trace"]
+    assert res["ood"] == ok

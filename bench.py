@@ -19,9 +19,10 @@ Workloads (--workload):
 Inputs are synthetic, resident in HBM before the timed region.
 
 Also reported:
-  roofline     -- for the dominant kernel (largest total time): algorithmic bytes per launch /
-                  average launch duration (HIP events on the launch stream, eon_ctx_profile) vs
-                  8 TB/s HBM, `traffic` from the committed PMC pass (profiles/traffic_*.json);
+  roofline     -- for the dominant kernel (largest total time): algorithmic bytes per launch
+                   / average launch duration (HIP events on the launch
+                  stream, eon_ctx_profile, over serialized profiled steps after the timed region)
+                  vs 8 TB/s HBM, `traffic` from the committed PMC pass (profiles/traffic_*.json);
                   `valu` is the binding integer roofline of the same kernel: its algorithmic
                   256-bit Montgomery products per launch / launch duration vs the measured
                   mulmod peak (tools/ubench_mulmod.hip).
@@ -123,6 +124,8 @@ class LdeWorkload:
         self.x = torch.from_numpy(synthetic_fr(self.n, self.w, 1234 + rank).view(np.int64)).to(dev)
         self.out = torch.empty((self.n << self.b, self.w, 4), dtype=torch.int64, device=dev)
         self.shift = fr_to_abi(5)
+        # read N W 32 B + write 2^b N W 32 B
+        self.alg_bytes_per_step = self.n * self.w * 32 + (self.n << self.b) * self.w * 32
 
     def step(self):
         import ctypes
@@ -370,6 +373,8 @@ class FourStepWorkload:
         log_n1, log_n2 = D.fourstep_split(self.log_n)
         cols = (1 << log_n2) // self.world
         self.local = torch.from_numpy(synthetic_fr(1 << log_n1, cols, 4321 + rank).view(np.int64)).to(dev)
+        # 2 N 32 B (read + write once), this rank's 1/world share
+        self.alg_bytes_per_step = 2 * (1 << self.log_n) * 32 // self.world
 
     def step(self):
         from plonky3_eon_amd import distributed as D
@@ -484,6 +489,9 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--log-msm", type=int, default=20)
     ap.add_argument("--cpu-sample-cols", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--serial", action="store_true",
+                    help="every step in serial mode (eon_ctx_set_serial): for rocprofv3 kernel traces "
+                         "whose per-kernel durations are isolated")
     ap.add_argument("--host", choices=["native", "python"], default="native",
                     help="prove: C++ driver (libeonprove.so) or the Python mirror")
     ap.add_argument("--transcript", choices=["fs", "fixed"], default="fs",
@@ -521,6 +529,8 @@ def main() -> int:
     wl = {"lde": LdeWorkload, "msm": MsmWorkload, "prove": ProveWorkload, "ntt4": FourStepWorkload,
           "msm-shard": MsmShardWorkload}[args.workload](args, ctx, dev, rank)
 
+    if args.serial:
+        ctx.set_serial(True)
     for _ in range(args.warmup):
         wl.step()
     torch.cuda.synchronize()
@@ -535,16 +545,24 @@ def main() -> int:
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    # per-launch HIP-event timings come from extra steps after the timed region: recording two
-    # events around every launch on three streams perturbs the stream overlap of the MSM pipeline,
-    # so the timed steps above run without them
+    # per-launch HIP-event timings come from extra steps after the timed region, run in serial
+    # mode (eon_ctx_set_serial: every kernel on the context stream, none on the MSM / opening side
+    # streams), so that each launch's duration is its own and not shared with the kernels of the
+    # other streams -- the same durations `rocprofv3 --kernel-trace` reports for `--serial`
+    # (profiles/r02_*_kernel_stats.csv)
     prof_steps = max(1, min(args.steps, 2))
+    ctx.set_serial(True)
+    wl.step()  # warm the serial path's workspaces
+    torch.cuda.synchronize()
     ctx.profile(True)
+    t_p0 = time.perf_counter()
     for _ in range(prof_steps):
         wl.step()
     torch.cuda.synchronize()
+    serial_ms = (time.perf_counter() - t_p0) * 1e3 / prof_steps
     prof = ctx.profile_report()
     ctx.profile(False)
+    ctx.set_serial(args.serial)
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
@@ -572,8 +590,28 @@ def main() -> int:
         "traffic": None,
         "avg_launch_ms": round(avg_ms, 4),
         "alg_bytes_per_launch": int(bytes_per_launch),
+        "timing": "HIP events on the launch stream over %d serialized profiled steps after the timed "
+                  "region (eon_ctx_set_serial: no kernel overlap), %.1f ms per serialized step" % (prof_steps, serial_ms),
+        "kernel_ms_per_step": round(kst["total_ms"] / prof_steps, 3),
         "kernels": prof,
     }
+    step_bytes = getattr(wl, "alg_bytes_per_step", None)
+    if step_bytes:
+        # a DFT/LDE is a chain of NTT passes (k_ntt_pass29 variants, the twiddle pack of the
+        # four-step): section 8(d) prices the whole transform, so the roofline is its algorithmic
+        # bytes over the step's total (serialized) kernel time
+        roof["kernel"] = "all %d launches of the step (%s)" % (
+            sum(v["launches"] for v in prof.values()) // prof_steps, ", ".join(sorted(prof)))
+        roof["avg_launch_ms"] = round(gpu_total_ms, 4)
+        roof["alg_bytes_per_launch"] = int(step_bytes)
+        roof["achieved"] = round(step_bytes / (gpu_total_ms * 1e-3) / 1e9, 2)
+        roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBPS, 4)
+        roof["kernel_ms_per_step"] = round(gpu_total_ms, 3)
+    if kst.get("design_bytes"):
+        # what the kernel's access pattern moves (fixed-base table gathers) vs section 8(d)'s bytes
+        dpl = kst["design_bytes"] / kst["launches"]
+        roof["design_bytes_per_launch"] = int(dpl)
+        roof["design_GBps"] = round(dpl / (avg_ms * 1e-3) / 1e9, 2)
     kmm = kst.get("alg_mulmods", 0)
     if kmm:
         rate = kmm / kst["launches"] / (avg_ms * 1e-3)
@@ -584,13 +622,6 @@ def main() -> int:
             "peak_mulmod_per_s": MULMOD_PEAK_PER_S,
             "frac": round(rate / MULMOD_PEAK_PER_S, 4),
         }
-        if kst.get("busy_ms"):
-            # launches of this kernel overlap on several streams (the MSM pipeline): the rate over
-            # the union of their intervals is what the chip sustained for it
-            rb = kmm / (kst["busy_ms"] * 1e-3)
-            roof["valu"]["busy_ms_per_step"] = round(kst["busy_ms"] / prof_steps, 3)
-            roof["valu"]["achieved_mulmod_per_s_busy"] = round(rb, 1)
-            roof["valu"]["frac_busy"] = round(rb / MULMOD_PEAK_PER_S, 4)
     if mulmods is not None:
         roof["valu_whole_step"] = {
             "achieved_mulmod_per_s": round(mulmods / (gpu_total_ms * 1e-3), 1),

@@ -96,6 +96,12 @@ int eon_ctx_synchronize(eon_ctx* ctx);
  * {kernel: {launches, total_ms, alg_bytes}} into buf (synchronizes on the recorded events). */
 int eon_ctx_profile(eon_ctx* ctx, int enable);
 int eon_ctx_profile_report(eon_ctx* ctx, char* buf, uint64_t len);
+/* Serial mode (also EON_SERIAL=1 at creation): every kernel of this context on its one stream,
+ * none on the MSM / opening side streams, so that each launch runs alone on the device and its
+ * event-timed or profiler duration is isolated.  For measurement only: results are identical,
+ * the prove is slower (no overlap of digit sorts with piece sums). */
+int eon_ctx_set_serial(eon_ctx* ctx, int serial);
+int eon_ctx_serial(const eon_ctx* ctx);
 /* ABI version; bumped on any signature change */
 uint32_t eon_abi_version(void);
 

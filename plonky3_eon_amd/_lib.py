@@ -80,6 +80,8 @@ SIGNATURES = {
     "eon_ctx_synchronize": (_INT, [_P]),
     "eon_ctx_profile": (_INT, [_P, _INT]),
     "eon_ctx_profile_report": (_INT, [_P, ctypes.c_char_p, _U64]),
+    "eon_ctx_set_serial": (_INT, [_P, _INT]),
+    "eon_ctx_serial": (_INT, [_P]),
     "eon_dft_batch": (_INT, [_P, _P, _P, _U64, _U32, _INT]),
     "eon_idft_batch": (_INT, [_P, _P, _P, _U64, _U32]),
     "eon_coset_dft_batch": (_INT, [_P, _P, _P, _U64, _U32, _P, _INT]),

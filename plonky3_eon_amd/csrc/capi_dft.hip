@@ -314,6 +314,7 @@ int eon_ctx_create(int device_ordinal, eon_ctx** out) {
         delete c;
         return EON_E_DEVICE;
     }
+    if (const char* e = getenv("EON_SERIAL")) c->serial = e[0] == '1';
     if (const char* e = getenv("EON_NTT_MAX_STAGES")) c->ntt_max_stages = (uint32_t)atoi(e);
     if (const char* e = getenv("EON_NTT_TPB")) c->ntt_tpb = (uint32_t)atoi(e);
     if (const char* e = getenv("EON_NTT_TILE")) c->ntt_log_tile = (uint32_t)atoi(e);
@@ -375,6 +376,19 @@ int eon_ctx_set_stream(eon_ctx* ctx, void* hip_stream) {
 
 int eon_ctx_device(const eon_ctx* ctx) { return ctx ? ctx->device : -1; }
 
+int eon_ctx_set_serial(eon_ctx* ctx, int serial) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    (void)hipSetDevice(ctx->device);
+    // drain the side streams before their work moves to `stream` (or back)
+    for (hipStream_t st : {ctx->stream, ctx->msm_side, ctx->msm_side2, ctx->msm_sort})
+        (void)hipStreamSynchronize(st);
+    ctx->serial = serial != 0;
+    return EON_OK;
+}
+
+int eon_ctx_serial(const eon_ctx* ctx) { return ctx && ctx->serial ? 1 : 0; }
+
 int eon_ctx_set_collective(eon_ctx* ctx, const eon_collective* coll) {
     if (!ctx) return EON_E_ARG;
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -420,14 +434,15 @@ int eon_ctx_profile(eon_ctx* ctx, int enable) {
 }
 
 int eon_ctx_profile_report(eon_ctx* ctx, char* buf, uint64_t len) {
-    // JSON: {"kernel name": {"launches": n, "total_ms": t, "alg_bytes": b, "alg_mulmods": m}, ...}
+    // JSON: {"kernel name": {"launches": n, "total_ms": t, "busy_ms": u, "alg_bytes": b,
+    //        "alg_mulmods": m, "design_bytes": d}, ...}
     if (!ctx || !buf || len == 0) return EON_E_ARG;
     std::lock_guard<std::mutex> lk(ctx->mu);
     (void)hipSetDevice(ctx->device);
     // busy_ms: the union of a kernel's launch intervals (launches on several streams overlap, so
     // total_ms / launches overstates what one launch would take alone)
     struct Agg {
-        uint64_t n = 0, bytes = 0, mulmods = 0;
+        uint64_t n = 0, bytes = 0, mulmods = 0, design = 0;
         double ms = 0;
         std::vector<std::pair<double, double>> iv;
     };
@@ -442,6 +457,7 @@ int eon_ctx_profile_report(eon_ctx* ctx, char* buf, uint64_t len) {
         a.ms += ms;
         a.bytes += r.alg_bytes;
         a.mulmods += r.alg_mulmods;
+        a.design += r.design_bytes;
         if (hipEventElapsedTime(&a0, t0, r.start) == hipSuccess && hipEventElapsedTime(&a1, t0, r.stop) == hipSuccess)
             a.iv.emplace_back(a0, a1);
     }
@@ -461,14 +477,14 @@ int eon_ctx_profile_report(eon_ctx* ctx, char* buf, uint64_t len) {
         return tot;
     };
     std::string out = "{";
-    char tmp[256];
+    char tmp[384];
     for (auto& kv : agg) {
         snprintf(tmp, sizeof tmp,
                  "%s\"%s\": {\"launches\": %llu, \"total_ms\": %.6f, \"busy_ms\": %.6f, "
-                 "\"alg_bytes\": %llu, \"alg_mulmods\": %llu}",
+                 "\"alg_bytes\": %llu, \"alg_mulmods\": %llu, \"design_bytes\": %llu}",
                  out.size() > 1 ? ", " : "", kv.first.c_str(), (unsigned long long)kv.second.n,
                  kv.second.ms, busy(kv.second.iv), (unsigned long long)kv.second.bytes,
-                 (unsigned long long)kv.second.mulmods);
+                 (unsigned long long)kv.second.mulmods, (unsigned long long)kv.second.design);
         out += tmp;
     }
     out += "}";

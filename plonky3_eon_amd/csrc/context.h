@@ -116,6 +116,11 @@ struct eon_ctx {
     // per-launch HIP-event timing (eon_ctx_profile_*)
     eon::Profiler prof;
 
+    // serial mode (EON_SERIAL=1 at creation, eon_ctx_set_serial): every launch of this context on
+    // `stream`, no side streams -- kernel durations are then isolated (profiling), not overlapped
+    bool serial = false;
+    hipStream_t side(hipStream_t s) const { return serial ? stream : s; }
+
     // process group for work replicated on every rank (eon_ctx_set_collective; world 0 = none)
     eon_collective coll{0, 0, nullptr, nullptr};
 

@@ -871,11 +871,14 @@ static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt
     if (b->r29) EON_HIP(wk.piece_raw.ensure(bt.max_pieces * sizeof(G1Raw29)));
     if (!wk.host_counts) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&wk.host_counts), 64));
     const G1Affine* pts = b->piece_source();
-    // algorithmic bytes: every nonzero digit reads its 4-byte key, 4-byte reference and 64-byte
-    // affine base; every piece writes one 128-byte XYZZ partial
+    // algorithmic bytes: n (64 + 32) B per MSM of n terms -- each
+    // base and scalar read once; design bytes: what this kernel's access pattern moves instead,
+    // a 4-byte key, a 4-byte reference and a 64-byte table entry per nonzero digit plus one
+    // 144-byte partial per piece
     // mulmods: one XYZZ mixed addition (madd-2008-s, 8M + 2S) per nonzero digit
-    ctx->prof.begin("k_piece_sum", (uint64_t)bt.n_pairs * 72 + (uint64_t)bt.n_pieces * 128, st,
-                    (uint64_t)bt.n_pairs * 10);
+    const uint64_t msm_n = bt.E / ((uint64_t)bt.W * bt.cols);
+    ctx->prof.begin("k_piece_sum", (uint64_t)bt.cols * msm_n * 96, st, (uint64_t)bt.n_pairs * 10,
+                    (uint64_t)bt.n_pairs * 72 + (uint64_t)bt.n_pieces * 144);
     uint32_t blocks = blocks_for(((uint64_t)bt.n_pairs + (1u << bt.log_chunk) - 1) >> bt.log_chunk, 64);
     if (ctx->piece_block_cap) blocks = std::min(blocks, ctx->piece_block_cap);
     if (bt.n_pairs && b->r29)
@@ -1359,8 +1362,9 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
     // k % 3): sort(k+1) only waits for reduce(k-2).  Events order sort(k) after reduce(k - 3)
     // and pieces(k) after sort(k).
     const bool masked = ctx->msm_sort_cus > 0;
-    hipStream_t comp[2] = {masked ? ctx->msm_comp[0] : ctx->stream, masked ? ctx->msm_comp[1] : ctx->msm_side};
-    hipStream_t sort_st = ctx->msm_sort;
+    hipStream_t comp[2] = {ctx->side(masked ? ctx->msm_comp[0] : ctx->stream),
+                           ctx->side(masked ? ctx->msm_comp[1] : ctx->msm_side)};
+    hipStream_t sort_st = ctx->side(ctx->msm_sort);
     MsmWork* wks[3] = {&ctx->msm, &ctx->msm_b, &ctx->msm_c};
     EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));  // scalars and earlier work are ready
     EON_HIP(hipStreamWaitEvent(sort_st, ctx->msm_ev[0], 0));
@@ -1447,7 +1451,7 @@ Status msm_run_prepared(eon_ctx* ctx, const eon_msm_bases* const* bases, uint32_
         const char* e = getenv("EON_MSM_PIECE_CHAIN");
         return e && e[0] == '1';
     }();
-    hipStream_t comp[4] = {ctx->stream, ctx->msm_side, ctx->msm_side2, ctx->msm_sort};
+    hipStream_t comp[4] = {ctx->stream, ctx->side(ctx->msm_side), ctx->side(ctx->msm_side2), ctx->side(ctx->msm_sort)};
     MsmWork* wks[4] = {&ctx->msm, &ctx->msm_b, &ctx->msm_c, &ctx->msm_d};
     EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));
     for (uint32_t i = 1; i < NS; i++) EON_HIP(hipStreamWaitEvent(comp[i], ctx->msm_ev[0], 0));

@@ -50,6 +50,9 @@ struct LaunchRecord {
     uint64_t alg_bytes;  // algorithmic bytes of this launch (each element read + written once)
     hipEvent_t start, stop;
     uint64_t alg_mulmods;  // algorithmic 256-bit Montgomery products of this launch (0: not counted)
+    // bytes the kernel's own access pattern implies beyond alg_bytes' definition (e.g. the
+    // fixed-base table gathers of k_piece_sum: 64 B per nonzero digit); 0 when equal
+    uint64_t design_bytes;
 };
 struct Profiler {
     bool enabled = false;
@@ -65,9 +68,10 @@ struct Profiler {
         (void)hipEventCreate(&e);
         return e;
     }
-    void begin(const char* kernel, uint64_t bytes, hipStream_t st, uint64_t mulmods = 0) {
+    void begin(const char* kernel, uint64_t bytes, hipStream_t st, uint64_t mulmods = 0,
+               uint64_t design_bytes = 0) {
         if (!enabled) return;
-        LaunchRecord r{kernel, bytes, get(), get(), mulmods};
+        LaunchRecord r{kernel, bytes, get(), get(), mulmods, design_bytes};
         (void)hipEventRecord(r.start, st);
         recs.push_back(r);
     }

@@ -367,7 +367,7 @@ Status opening_bases_sharded(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
     const eon_collective& coll = ctx->coll;
     const uint32_t world = coll.world, rank = coll.rank, np = (uint32_t)zs.size();
     const uint64_t m = (n + world - 1) / world, lo = (uint64_t)rank * m;
-    hipStream_t streams[3] = {ctx->stream, ctx->msm_side, ctx->msm_side2};
+    hipStream_t streams[3] = {ctx->stream, ctx->side(ctx->msm_side), ctx->side(ctx->msm_side2)};
     // per point: slice points (+1 for the total), scan scratch, affine slice, table slice
     std::vector<Scratch> sc(np);
     DevBuf totals_x, totals_a, all_totals, send, recv;
@@ -478,7 +478,7 @@ Status opening_bases_many(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, co
     bool fast = !slow && bases_table29(srs) && bases_window(srs) == TC && bases_windows(srs) == TW && n >= 2;
     for (const Fr& z : zs) fast = fast && !z.is_zero();
     if (fast && !no_shard && ctx->coll.world > 1 && npoints) return opening_bases_sharded(ctx, srs, n, zs, outs);
-    hipStream_t streams[3] = {ctx->stream, ctx->msm_side, ctx->msm_side2};
+    hipStream_t streams[3] = {ctx->stream, ctx->side(ctx->msm_side), ctx->side(ctx->msm_side2)};
     EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));
     EON_HIP(hipStreamWaitEvent(ctx->msm_side, ctx->msm_ev[0], 0));
     EON_HIP(hipStreamWaitEvent(ctx->msm_side2, ctx->msm_ev[0], 0));

@@ -57,6 +57,11 @@ class Context:
         """Start (clearing) or stop per-launch HIP-event timing (eon_ctx_profile)."""
         self.check(self.lib.eon_ctx_profile(self._h, 1 if enable else 0))
 
+    def set_serial(self, serial: bool = True):
+        """Serial mode (eon_ctx_set_serial): every kernel on the context stream, none on the MSM /
+        opening side streams -- isolated launch durations for profiles; same results."""
+        self.check(self.lib.eon_ctx_set_serial(self._h, 1 if serial else 0))
+
     def profile_report(self) -> dict:
         import json
 

@@ -224,7 +224,7 @@ void KzgPcs::commit(std::vector<std::pair<Domain, DeviceMatrix>> evaluations,
 
 DeviceMatrix KzgPcs::get_evaluations_on_domain(const std::vector<MatrixProverData>& data, size_t idx,
                                                const Domain& domain, bool aux) {
-    eon_ctx* ctx = aux && aux_ ? aux_ : ctx_;
+    eon_ctx* ctx = aux && aux_live() ? aux_ : ctx_;
     const MatrixProverData& m = data.at(idx);
     if (m.domain == domain) return DeviceMatrix::borrow(m.evals.data(), m.evals.height, m.evals.width);
     if (domain.log_size < m.domain.log_size)
@@ -305,7 +305,7 @@ std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
     // f(z) of every column at every point (the remainder of quotient_and_eval, util.rs:100-111):
     // enqueued on the auxiliary context, whose HBM-bound passes over the coefficients run beside
     // the VALU-bound opening-bases construction; read back after the witnesses
-    eon_ctx* vctx = aux_ ? aux_ : ctx_;
+    eon_ctx* vctx = aux_live() ? aux_ : ctx_;
     hipStream_t vst = static_cast<hipStream_t>(eon_ctx_stream(vctx));
     std::vector<std::vector<DeviceBuffer>> vals(rounds.size());
     struct DrainOnExit {  // an error path must not free `vals` under the kernels writing them
@@ -381,7 +381,7 @@ std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
         const char* e = getenv("EON_OPEN_OVERLAP");
         return e && e[0] == '1';
     }();
-    if (!overlap || !aux_ || keys.size() < 2) {
+    if (!overlap || !aux_live() || keys.size() < 2) {
         build(ctx_, keys);
         run_ready();
         collect_values();

@@ -125,7 +125,10 @@ class KzgPcs {
     DeviceMatrix get_evaluations_on_domain(const std::vector<MatrixProverData>& data, size_t idx,
                                            const Domain& domain, bool aux = false);
     // a second context on the same device for work concurrent with this one's (null if none)
-    eon_ctx* aux_ctx() const { return aux_; }
+    eon_ctx* aux_ctx() const { return aux_live(); }
+    // the auxiliary context, unless the main one is in serial mode (eon_ctx_set_serial: every
+    // kernel alone on the device, for isolated profiles)
+    eon_ctx* aux_live() const { return aux_ && !eon_ctx_serial(ctx_) ? aux_ : nullptr; }
     // commit/src/pcs.rs:82-101 with split_evals (domain.rs:188-221)
     void commit_quotient(const Domain& quotient_domain, const DeviceMatrix& quotient_evals, uint32_t num_chunks,
                          std::vector<std::vector<eon_g1_affine>>& commitments, std::vector<MatrixProverData>& data);

@@ -348,6 +348,8 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     ctx->sorted_cache.clear();
     ctx->sel_tab.release();
     ctx->kzg_tmp.release();
+    ctx->fin_T.release();
+    ctx->fin_U.release();
     ctx->scratch.release();
     ctx->stage_in.release();
     ctx->stage_out.release();

@@ -147,6 +147,9 @@ struct eon_ctx {
     // hipMalloc/hipFree of it per proof); trimmed past MSM_SORTED_CACHE_CAP bytes
     std::vector<eon::SortedBufs> sorted_cache;
 
+    // call-wide first-level segment sums of the MSM bucket reduction (msm.hip DeferredFinish)
+    eon::DevBuf fin_T, fin_U;
+
     // quotient: vanishing-polynomial table; KZG opening scan workspace
     eon::DevBuf sel_tab, kzg_tmp;
 

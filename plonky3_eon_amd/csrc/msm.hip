@@ -938,13 +938,84 @@ static Status reduce_segments(eon_ctx* ctx, const MsmLayout& L, const Batch& bt,
     return write_columns(L, bt, cur, st);
 }
 
+// Deferred group finish: the batches of one call leave their first-level segment sums (T, U of
+// k_bucket_reduce29) in call-wide arrays, row = the group's output index, and ONE k_group_finish
+// launch over every row runs after the last batch.  Per batch, that finish was 120 groups x 256
+// threads -- under one wave per SIMD, a chain of ~75 dependent additions (1.1 ms per batch,
+// latency-bound); over the whole call (1312 or 2624 groups) it is throughput-bound.
+struct DeferredFinish {
+    G1Xyzz* T = nullptr;
+    G1Xyzz* U = nullptr;
+    G1Xyzz* out_base = nullptr;  // row r's result goes to out_base[r]
+    uint32_t nseg = 0, log_seg = 0;
+    std::vector<std::pair<uint64_t, uint64_t>> rows;  // deferred [row0, row0 + n)
+};
+
+static bool defer_finish_enabled() {
+    static const bool off = getenv("EON_MSM_FINISH_PER_BATCH") != nullptr;
+    return !off;
+}
+
+// k_group_finish over the deferred rows (merged into maximal runs) on `st`
+static hipError_t launch_group_finish(const G1Xyzz* T, const G1Xyzz* U, uint32_t nseg, uint32_t lsg,
+                                      G1Xyzz* out, uint32_t groups, hipStream_t st);
+
+static Status run_deferred_finish(eon_ctx* ctx, DeferredFinish& df, hipStream_t st) {
+    if (df.rows.empty()) return Status::ok();
+    std::sort(df.rows.begin(), df.rows.end());
+    std::vector<std::pair<uint64_t, uint64_t>> runs;
+    for (auto& r : df.rows) {
+        if (!runs.empty() && runs.back().first + runs.back().second == r.first)
+            runs.back().second += r.second;
+        else
+            runs.push_back(r);
+    }
+    for (auto& r : runs) {
+        ctx->prof.begin("k_group_finish", r.second * df.nseg * 256ull, st, r.second * df.nseg * 3ull * 14);
+        EON_HIP(launch_group_finish(df.T + r.first * df.nseg, df.U + r.first * df.nseg, df.nseg, df.log_seg,
+                                    df.out_base + r.first, (uint32_t)r.second, st));
+        ctx->prof.end(st);
+    }
+    df.rows.clear();
+    return Status::ok();
+}
+
+static Status prepare_deferred(eon_ctx* ctx, const MsmLayout& L, uint64_t rows, G1Xyzz* out_base,
+                               DeferredFinish& df) {
+    df = DeferredFinish{};
+    if (!defer_finish_enabled() || !L.precomputed) return Status::ok();
+    const uint32_t B = 1u << (L.c - 1);
+    if (B < SEG) return Status::ok();
+    df.nseg = B / SEG;
+    df.log_seg = 31 - __builtin_clz(SEG);
+    EON_HIP(ctx->fin_T.ensure(rows * df.nseg * sizeof(G1Xyzz)));
+    EON_HIP(ctx->fin_U.ensure(rows * df.nseg * sizeof(G1Xyzz)));
+    df.T = ctx->fin_T.as<G1Xyzz>();
+    df.U = ctx->fin_U.as<G1Xyzz>();
+    df.out_base = out_base;
+    return Status::ok();
+}
+
 // combine levels, bucket sums and the weighted bucket reduction of one batch's pieces (read-back
 // of each level's count synchronises `st`); leaves one XYZZ point per column at bt.out.  The
 // sorted piece offsets are only read (a prepared batch is reduced once per bases object).
 static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, const SortedRef& sr,
-                           MsmWork& wk, hipStream_t st, bool fused) {
+                           MsmWork& wk, hipStream_t st, bool fused, DeferredFinish* df = nullptr) {
     Profiler* prof = &ctx->prof;
     const uint32_t nb = bt.nb, groups = bt.groups, B = bt.B;
+    if (df && df->T && fused && groups >= 64 && B >= SEG && L.precomputed &&
+        getenv("EON_MSM_SEG_LEVELS") == nullptr) {
+        // first level only; the finish runs once per call (run_deferred_finish)
+        const uint64_t row0 = (uint64_t)(bt.out - df->out_base);
+        prof->begin("bucket_reduce", (uint64_t)nb * 128 + (uint64_t)nb / SEG * 256, st);
+        hipLaunchKernelGGL(k_bucket_reduce29, dim3(blocks_for((uint64_t)df->nseg * groups, 64)), dim3(64), 0, st,
+                           wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, SEG, groups, df->T + row0 * df->nseg,
+                           df->U + row0 * df->nseg);
+        prof->end(st);
+        EON_HIP(hipGetLastError());
+        df->rows.emplace_back(row0, groups);
+        return Status::ok();
+    }
     // combine levels until every bucket holds one partial (skewed scalars put many pieces in a
     // bucket: all-equal scalars put n pieces in one bucket per window)
     const uint32_t* off_cur = sr.piece_off;
@@ -1058,6 +1129,22 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
     prof->end(st);
     EON_HIP(hipGetLastError());
     return write_columns(L, bt, per_group, st);
+}
+
+static hipError_t launch_group_finish(const G1Xyzz* T, const G1Xyzz* U, uint32_t nseg, uint32_t lsg,
+                                      G1Xyzz* out, uint32_t groups, hipStream_t st) {
+    static const uint32_t gf = [] {
+        const char* e = getenv("EON_MSM_GF_THREADS");
+        const int v = e ? atoi(e) : 256;
+        return (uint32_t)(v == 512 || v == 1024 ? v : 256);
+    }();
+    if (gf == 1024)
+        hipLaunchKernelGGL(k_group_finish<1024>, dim3(groups), dim3(1024), 0, st, T, U, nseg, lsg, out);
+    else if (gf == 512)
+        hipLaunchKernelGGL(k_group_finish<512>, dim3(groups), dim3(512), 0, st, T, U, nseg, lsg, out);
+    else
+        hipLaunchKernelGGL(k_group_finish<256>, dim3(groups), dim3(256), 0, st, T, U, nseg, lsg, out);
+    return hipGetLastError();
 }
 
 }  // namespace eon
@@ -1388,6 +1475,8 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
         const char* e = getenv("EON_MSM_SORT_AHEAD");
         return e && e[0] == '1';
     }();
+    DeferredFinish df;
+    EON_TRY(prepare_deferred(ctx, L, width, res_xyzz, df));
     EON_TRY(sort_batch(0));
     for (size_t k = 0; k < batches.size(); k++) {
         const int i = (int)(k & 1), w = (int)(k % 3);
@@ -1397,7 +1486,7 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
         EON_TRY(pieces(k));
         if (!sort_ahead && k + 1 < batches.size()) EON_TRY(sort_batch(k + 1));
         EON_TRY(batch_reduce(ctx, L, batches[k], sorted_ref(sorted_of(k)), *wks[w], comp[i],
-                             fused_reduce(b, batches[k])));
+                             fused_reduce(b, batches[k]), &df));
         EON_HIP(hipEventRecord(ctx->msm_reduced[w], comp[i]));
     }
     // the context stream resumes after both compute streams' last reductions
@@ -1406,6 +1495,7 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
         EON_HIP(hipEventRecord(ctx->msm_ev[1 + i], comp[i]));
         EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[1 + i], 0));
     }
+    EON_TRY(run_deferred_finish(ctx, df, ctx->stream));
     if (keep) {
         keep->batches = batches;
         for (Batch& bt : keep->batches) bt.scalars = nullptr;
@@ -1453,6 +1543,8 @@ Status msm_run_prepared(eon_ctx* ctx, const eon_msm_bases* const* bases, uint32_
     }();
     hipStream_t comp[4] = {ctx->stream, ctx->side(ctx->msm_side), ctx->side(ctx->msm_side2), ctx->side(ctx->msm_sort)};
     MsmWork* wks[4] = {&ctx->msm, &ctx->msm_b, &ctx->msm_c, &ctx->msm_d};
+    DeferredFinish df;
+    EON_TRY(prepare_deferred(ctx, s->layout, total, res_xyzz, df));
     EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));
     for (uint32_t i = 1; i < NS; i++) EON_HIP(hipStreamWaitEvent(comp[i], ctx->msm_ev[0], 0));
     for (size_t k = 0; k < s->batches.size(); k++)
@@ -1465,12 +1557,13 @@ Status msm_run_prepared(eon_ctx* ctx, const eon_msm_bases* const* bases, uint32_
             if (chain && j > 0) EON_HIP(hipStreamWaitEvent(st, ctx->msm_pdone[(j - 1) % 4], 0));
             EON_TRY(batch_pieces(ctx, bases[t], bt, sr, *wks[j % NS], st));
             if (chain) EON_HIP(hipEventRecord(ctx->msm_pdone[j % 4], st));
-            EON_TRY(batch_reduce(ctx, s->layout, bt, sr, *wks[j % NS], st, fused_reduce(bases[t], bt)));
+            EON_TRY(batch_reduce(ctx, s->layout, bt, sr, *wks[j % NS], st, fused_reduce(bases[t], bt), &df));
         }
     for (uint32_t i = 1; i < NS; i++) {
         EON_HIP(hipEventRecord(ctx->msm_ev[1], comp[i]));
         EON_HIP(hipStreamWaitEvent(ctx->stream, ctx->msm_ev[1], 0));
     }
+    EON_TRY(run_deferred_finish(ctx, df, ctx->stream));
     (void)res;
     return results_to_host_affine(res_xyzz, total, out_host, ctx->stream);
 }

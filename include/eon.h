@@ -43,16 +43,21 @@ typedef struct {
 
 typedef struct eon_ctx eon_ctx;
 
-/* An all-gather over DEVICE buffers among `world` processes (one per GPU): recv receives `world`
- * blocks of `bytes`, in rank order.  Called with a context's stream; it must leave recv complete
- * and ordered before that stream's later work (an RCCL all-gather enqueued on `hip_stream` does; a
- * host-staged one synchronizes).  The lane-sharded prove (eon_prove.h) and a context's sharded
- * work (eon_ctx_set_collective) use it. */
+/* Collectives over DEVICE buffers among `world` processes (one per GPU), called with a context's
+ * stream; each must leave recv complete and ordered before that stream's later work (an RCCL call
+ * enqueued on `hip_stream` does; a host-staged one synchronizes).
+ *   all_gather: recv receives `world` blocks of `bytes`, in rank order.  Used by the lane-sharded
+ *               prove (eon_prove.h), a context's sharded work (eon_ctx_set_collective) and
+ *               eon_msm_sharded_dev.
+ *   all_to_all: send holds `world` blocks of `bytes` (block h goes to rank h); recv receives
+ *               `world` blocks, block g from rank g (ncclAllToAll).  Used by
+ *               eon_fourstep_dft_dev; may be NULL when no four-step transform runs. */
 typedef struct {
     uint32_t rank;
     uint32_t world;
     int (*all_gather)(void* user, const void* send, void* recv, uint64_t bytes, void* hip_stream);
     void* user;
+    int (*all_to_all)(void* user, const void* send, void* recv, uint64_t bytes, void* hip_stream);
 } eon_collective;
 typedef struct eon_msm_bases eon_msm_bases;
 typedef struct eon_msm_scalars eon_msm_scalars;
@@ -71,6 +76,14 @@ enum {
     EON_ORDER_BITREV = 1   /* storage of Radix2DitParallel's BitReversedMatrixView: storage row
                               reverse_bits_len(k, log2 h) holds logical row k
                               (dft/src/radix_2_dit_parallel.rs:146,165,227) */
+};
+
+/* output layouts of eon_fourstep_dft_dev */
+enum {
+    EON_FOURSTEP_NATURAL = 0,    /* rank g holds X[g N/G, (g+1) N/G): its contiguous natural slice
+                                    (a second all_to_all) */
+    EON_FOURSTEP_TRANSPOSED = 1  /* rank g holds the N2 x N1/G row-major block of the N2 x N1 view:
+                                    row k2, column k1' = X[N1 k2 + g N1/G + k1'] (one all_to_all) */
 };
 
 /* ---- context ---------------------------------------------------------------------------- */
@@ -341,6 +354,29 @@ int eon_fr_lincomb_dev(eon_ctx* ctx, const eon_fr* in, uint32_t k, uint64_t rows
  * contiguous cols x (N1/parts) blocks, one per destination rank (device pointers). */
 int eon_fourstep_twiddle_pack_dev(eon_ctx* ctx, const eon_fr* y, uint32_t log_n, uint32_t log_n1,
                                   uint64_t col0, uint32_t cols, uint32_t parts, eon_fr* send);
+
+/* The whole sharded forward DFT: dft_batch (dft/src/traits.rs:61, natural order; the reference
+ * has no multi-GPU path -- this is SURVEY.md 8(e)'s four-step scheme) of ONE column of N = 2^log_n
+ * elements spread over the collective's `world` ranks (every rank calls with the same log_n,
+ * layout and collective; world must divide N2 and N1, N1 = 2^ceil(log_n / 2), N2 = N / N1).
+ *   in:  the rank's N1 x (N2/world) row-major block of the N1 x N2 view x[N2 i1 + i2]: columns
+ *        [rank N2/world, (rank+1) N2/world) -- i.e. in[i1 C + c] = x[N2 i1 + rank C + c];
+ *   out: N/world elements in `layout` (EON_FOURSTEP_NATURAL or EON_FOURSTEP_TRANSPOSED).
+ * Steps: size-N1 column DFTs, twiddles w_N^(i2 k1) fused with the pack per destination,
+ * all_to_all, size-N2 DFTs, and for the natural layout a second all_to_all plus a block
+ * interleave.  coll NULL = the context's bound collective (eon_ctx_set_collective), or one rank.
+ * Device pointers; `in` is not modified.  Synchronous with respect to the collective calls. */
+int eon_fourstep_dft_dev(eon_ctx* ctx, const eon_fr* in, eon_fr* out, uint32_t log_n, int layout,
+                         const eon_collective* coll);
+
+/* G1::multi_exp (bn254/src/curve.rs:158-179) of ONE MSM whose terms are split over the ranks by
+ * contiguous range (SURVEY.md 8(e), configs[4] (ii)): every rank passes its bases (over its own
+ * range) and its n_local scalars (device pointer); each runs a full Pippenger, the `world` affine
+ * partial points are all-gathered (64 B per rank) and summed (EC additions -- not an RCCL
+ * reduction).  Every rank receives the same result in *out (host).  coll NULL = the context's
+ * bound collective, or one rank. */
+int eon_msm_sharded_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* scalars, uint64_t n_local,
+                        const eon_collective* coll, eon_g1_affine* out);
 
 /* ---- test SRS (setup, not prove time) --------------------------------------------------------
  * init_srs_unsafe's g1_powers (kzg/src/params.rs:123-139): out[i] = alpha^i * G1::generator(),

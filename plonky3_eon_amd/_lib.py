@@ -20,6 +20,8 @@ EON_E_OOM = -4
 EON_E_ARG = -5
 EON_ORDER_NATURAL = 0
 EON_ORDER_BITREV = 1
+EON_FOURSTEP_NATURAL = 0
+EON_FOURSTEP_TRANSPOSED = 1
 EON_MSM_PRECOMPUTE = 1
 
 _ERRNAMES = {
@@ -81,6 +83,8 @@ SIGNATURES = {
     "eon_ctx_profile": (_INT, [_P, _INT]),
     "eon_ctx_profile_report": (_INT, [_P, ctypes.c_char_p, _U64]),
     "eon_ctx_set_serial": (_INT, [_P, _INT]),
+    "eon_fourstep_dft_dev": (_INT, [_P, _P, _P, _U32, _INT, _P]),
+    "eon_msm_sharded_dev": (_INT, [_P, _P, _P, _U64, _P, _P]),
     "eon_ctx_serial": (_INT, [_P]),
     "eon_dft_batch": (_INT, [_P, _P, _P, _U64, _U32, _INT]),
     "eon_idft_batch": (_INT, [_P, _P, _P, _U64, _U32]),

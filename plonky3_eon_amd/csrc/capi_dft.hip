@@ -259,9 +259,17 @@ int entry(eon_ctx* ctx, bool dev, Op op, const eon_fr* in, eon_fr* out, uint64_t
 
 }  // namespace
 
+namespace eon {
+
+Status dft_natural_dev(eon_ctx* ctx, const Fr* in, Fr* out, uint64_t height, uint32_t width) {
+    return dft_dev(ctx, Op::Dft, in, out, height, width, 0, nullptr, EON_ORDER_NATURAL);
+}
+
+}  // namespace eon
+
 extern "C" {
 
-uint32_t eon_abi_version(void) { return 2; }
+uint32_t eon_abi_version(void) { return 3; }
 
 int eon_ctx_create(int device_ordinal, eon_ctx** out) {
     if (!out) return EON_E_ARG;
@@ -350,6 +358,8 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     ctx->kzg_tmp.release();
     ctx->fin_T.release();
     ctx->fin_U.release();
+    ctx->fs_a.release();
+    ctx->fs_b.release();
     ctx->scratch.release();
     ctx->stage_in.release();
     ctx->stage_out.release();

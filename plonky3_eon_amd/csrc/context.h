@@ -150,6 +150,9 @@ struct eon_ctx {
     // call-wide first-level segment sums of the MSM bucket reduction (msm.hip DeferredFinish)
     eon::DevBuf fin_T, fin_U;
 
+    // four-step DFT working blocks (sharded.hip)
+    eon::DevBuf fs_a, fs_b;
+
     // quotient: vanishing-polynomial table; KZG opening scan workspace
     eon::DevBuf sel_tab, kzg_tmp;
 
@@ -163,6 +166,12 @@ Status ensure_twiddles(eon_ctx* ctx, uint32_t log_n);
 // table[j] = scale * base^j (natural) or table[j] = scale * base^reverse_bits(j, log_n) (bitrev)
 Status get_power_table(eon_ctx* ctx, uint32_t log_n, const Fr& base, const Fr& scale, bool bitrev,
                        const Fr** out);
+
+// forward dft_batch (natural order in and out) of a height x width device matrix on ctx->stream
+Status dft_natural_dev(eon_ctx* ctx, const Fr* in, Fr* out, uint64_t height, uint32_t width);
+// four-step middle step (fourstep.hip): twiddle and pack the rank's size-N1 column DFTs
+Status fourstep_twiddle_pack(eon_ctx* ctx, const Fr* y, uint32_t log_n, uint32_t log_n1, uint64_t col0,
+                             uint32_t cols, uint32_t parts, Fr* send);
 
 inline Fr fr_two_adic_generator(uint32_t bits) {
     // bn254/src/field.rs:556-573: square TWO_ADIC_GENERATOR (order 2^28) 28 - bits times

@@ -66,6 +66,35 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+Status fourstep_twiddle_pack(eon_ctx* ctx, const Fr* y, uint32_t log_n, uint32_t log_n1, uint64_t col0,
+                             uint32_t cols, uint32_t parts, Fr* send) {
+    if (log_n > 28 || log_n1 > log_n)
+        return Status::err(EON_E_SHAPE, "need log_n1 <= log_n <= Fr::TWO_ADICITY = 28");
+    const uint32_t n1 = 1u << log_n1;
+    const uint64_t n2 = 1ull << (log_n - log_n1);
+    if (parts == 0 || n1 % parts) return Status::err(EON_E_SHAPE, "parts must divide N1");
+    if (col0 + cols > n2) return Status::err(EON_E_SHAPE, "column block exceeds N2");
+    if (cols == 0) return Status::ok();
+    if (!y || !send) return Status::err(EON_E_ARG, "null argument");
+    const uint32_t lo_bits = (log_n + 1) / 2, hi_bits = log_n - lo_bits;
+    const Fr w = fr_two_adic_generator(log_n);
+    Fr w_hi = w;
+    for (uint32_t i = 0; i < lo_bits; i++) w_hi = sqr(w_hi);
+    const Fr *t_lo = nullptr, *t_hi = nullptr;
+    EON_TRY(get_power_table(ctx, lo_bits, w, Fr::one(), false, &t_lo));
+    EON_TRY(get_power_table(ctx, hi_bits, w_hi, Fr::one(), false, &t_hi));
+    // the bounded table cache may have been flushed while building t_hi: look t_lo up again
+    EON_TRY(get_power_table(ctx, lo_bits, w, Fr::one(), false, &t_lo));
+    const dim3 grid((cols + FS_TILE - 1) / FS_TILE, (n1 + FS_TILE - 1) / FS_TILE);
+    ctx->prof.begin("k_fourstep_twiddle_pack", (uint64_t)n1 * cols * 64, ctx->stream,
+                    (uint64_t)n1 * cols * 2);
+    hipLaunchKernelGGL(k_fourstep_twiddle_pack, grid, dim3(FS_TILE, FS_ROWS), 0, ctx->stream, y, n1, cols,
+                       col0, n1 / parts, log_n, lo_bits, t_lo, t_hi, send);
+    ctx->prof.end(ctx->stream);
+    EON_HIP(hipGetLastError());
+    return Status::ok();
+}
+
 }  // namespace eon
 
 extern "C" {
@@ -75,34 +104,8 @@ int eon_fourstep_twiddle_pack_dev(eon_ctx* ctx, const eon_fr* y, uint32_t log_n,
     if (!ctx) return EON_E_ARG;
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
-    Status s = [&]() -> Status {
-        if (log_n > 28 || log_n1 > log_n)
-            return Status::err(EON_E_SHAPE, "need log_n1 <= log_n <= Fr::TWO_ADICITY = 28");
-        const uint32_t n1 = 1u << log_n1;
-        const uint64_t n2 = 1ull << (log_n - log_n1);
-        if (parts == 0 || n1 % parts) return Status::err(EON_E_SHAPE, "parts must divide N1");
-        if (col0 + cols > n2) return Status::err(EON_E_SHAPE, "column block exceeds N2");
-        if (cols == 0) return Status::ok();
-        if (!y || !send) return Status::err(EON_E_ARG, "null argument");
-        const uint32_t lo_bits = (log_n + 1) / 2, hi_bits = log_n - lo_bits;
-        const Fr w = fr_two_adic_generator(log_n);
-        Fr w_hi = w;
-        for (uint32_t i = 0; i < lo_bits; i++) w_hi = sqr(w_hi);
-        const Fr *t_lo = nullptr, *t_hi = nullptr;
-        EON_TRY(get_power_table(ctx, lo_bits, w, Fr::one(), false, &t_lo));
-        EON_TRY(get_power_table(ctx, hi_bits, w_hi, Fr::one(), false, &t_hi));
-        // the bounded table cache may have been flushed while building t_hi: look t_lo up again
-        EON_TRY(get_power_table(ctx, lo_bits, w, Fr::one(), false, &t_lo));
-        const dim3 grid((cols + FS_TILE - 1) / FS_TILE, (n1 + FS_TILE - 1) / FS_TILE);
-        ctx->prof.begin("k_fourstep_twiddle_pack", (uint64_t)n1 * cols * 64, ctx->stream,
-                        (uint64_t)n1 * cols * 2);
-        hipLaunchKernelGGL(k_fourstep_twiddle_pack, grid, dim3(FS_TILE, FS_ROWS), 0, ctx->stream,
-                           reinterpret_cast<const Fr*>(y), n1, cols, col0, n1 / parts, log_n, lo_bits,
-                           t_lo, t_hi, reinterpret_cast<Fr*>(send));
-        ctx->prof.end(ctx->stream);
-        EON_HIP(hipGetLastError());
-        return Status::ok();
-    }();
+    Status s = fourstep_twiddle_pack(ctx, reinterpret_cast<const Fr*>(y), log_n, log_n1, col0, cols, parts,
+                                     reinterpret_cast<Fr*>(send));
     if (s.bad()) ctx->last_error = s.msg;
     return s.code;
 }

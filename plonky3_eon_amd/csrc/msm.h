@@ -35,6 +35,10 @@ Status bases_alloc_table(eon_ctx* ctx, uint64_t n, uint32_t c, eon_msm_bases** o
 G1Affine* bases_table_mut(eon_msm_bases* b);
 Status bases_seal_table(eon_msm_bases* b, hipStream_t st);
 
+// XYZZ -> affine on the host (Montgomery batch inversion, 64-bit limbs; the same bytes as the
+// device conversion)
+void host_xyzz_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out);
+
 constexpr uint32_t BATCH = 32;  // points per thread in batched XYZZ -> affine conversion
 hipError_t launch_batch_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out, hipStream_t st);
 

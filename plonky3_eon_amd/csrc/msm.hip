@@ -1384,6 +1384,8 @@ static Status results_to_host_affine(const G1Xyzz* dev, uint64_t m, G1Affine* ou
     return Status::ok();
 }
 
+void host_xyzz_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out) { hostq::batch_to_affine(in, m, out); }
+
 static Status identity_columns(uint32_t width, G1Affine* out_host) {
     // G1::multi_exp returns the identity for empty input (curve.rs:163-165)
     for (uint32_t j = 0; j < width; j++) {

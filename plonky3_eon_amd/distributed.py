@@ -164,14 +164,17 @@ def fourstep_split(log_n: int):
     return log_n1, log_n - log_n1
 
 
-def fourstep_dft(ctx, local, log_n: int, rank: int = 0, world: int = 1, group=None):
+def fourstep_dft(ctx, local, log_n: int, rank: int = 0, world: int = 1, group=None, natural: bool = False,
+                 collective=None):
     """Forward DFT of length N = 2^log_n (Radix2Dit natural order, dft/src/traits.rs:27-61) split
-    over `world` ranks as a four-step N1 x N2 transform.
+    over `world` ranks as a four-step N1 x N2 transform: eon_fourstep_dft_dev (include/eon.h).
 
     local: this rank's (N1, N2/world, 4) int64 device block -- columns [rank C, (rank+1) C) of the
-    N1 x N2 view M[i1][i2] = x[N2 i1 + i2].  Returns the (N2, N1/world, 4) block of the N2 x N1 view
-    of X: out[k2][k1'] = X[N1 k2 + rank N1/world + k1'].  One all_to_all (the transpose) is the only
-    exchange."""
+    N1 x N2 view M[i1][i2] = x[N2 i1 + i2].  Returns (natural=False) the (N2, N1/world, 4) block of
+    the N2 x N1 view of X: out[k2][k1'] = X[N1 k2 + rank N1/world + k1'] -- one all_to_all -- or
+    (natural=True) the rank's contiguous slice X[rank N/world, (rank+1) N/world) as (N/world, 4),
+    after a second all_to_all.  `collective`: an eon_collective provider (TorchCollective over
+    `group` by default, or native.RcclCollective)."""
     import torch
 
     log_n1, log_n2 = fourstep_split(log_n)
@@ -182,25 +185,18 @@ def fourstep_dft(ctx, local, log_n: int, rank: int = 0, world: int = 1, group=No
     if tuple(local.shape[:2]) != (n1, cols):
         raise _lib.EonError(_lib.EON_E_SHAPE, f"local block must be ({n1}, {cols}, 4)")
     local = local.contiguous()
-    stream = torch.cuda.current_stream(local.device).cuda_stream
-    ctx.set_stream(stream)
-    # 1. size-N1 DFTs of the rank's columns
-    y = torch.empty_like(local)
-    ctx.check(ctx.lib.eon_dft_batch_dev(ctx.handle, ctypes.c_void_p(local.data_ptr()),
-                                        ctypes.c_void_p(y.data_ptr()), n1, cols, 0))
-    # 2. twiddles, packed per destination rank
-    send = torch.empty((world, cols, n1 // world, 4), dtype=torch.int64, device=local.device)
-    ctx.check(ctx.lib.eon_fourstep_twiddle_pack_dev(ctx.handle, ctypes.c_void_p(y.data_ptr()), log_n, log_n1,
-                                                    rank * cols, cols, world, ctypes.c_void_p(send.data_ptr())))
-    del y
-    # 3. transpose across ranks
-    recv = all_to_all_blocks(send, group) if world > 1 else send
-    z = recv.reshape(n2, n1 // world, 4)
-    # 4. size-N2 DFTs over i2
-    out = torch.empty_like(z)
-    ctx.set_stream(stream)
-    ctx.check(ctx.lib.eon_dft_batch_dev(ctx.handle, ctypes.c_void_p(z.data_ptr()),
-                                        ctypes.c_void_p(out.data_ptr()), n2, n1 // world, 0))
+    ctx.set_stream(torch.cuda.current_stream(local.device).cuda_stream)
+    coll = None
+    if world > 1:
+        from .collective import TorchCollective
+
+        coll = collective or TorchCollective(rank, world, group, local.device.index)
+    shape = ((n1 * n2) // world, 4) if natural else (n2, n1 // world, 4)
+    out = torch.empty(shape, dtype=torch.int64, device=local.device)
+    layout = _lib.EON_FOURSTEP_NATURAL if natural else _lib.EON_FOURSTEP_TRANSPOSED
+    ctx.check(ctx.lib.eon_fourstep_dft_dev(ctx.handle, ctypes.c_void_p(local.data_ptr()),
+                                           ctypes.c_void_p(out.data_ptr()), log_n, layout,
+                                           ctypes.byref(coll.c) if coll is not None else None))
     return out
 
 
@@ -231,21 +227,27 @@ def shard_range(n: int, rank: int, world: int):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def msm_sharded(bases, scalars_local, device, group=None):
-    """sum_i s_i P_i over every rank's range: a full Pippenger per rank on its contiguous range
-    (`bases` = MsmBases over that range), then an all-gather of the G affine partial points and
-    their sum.  RCCL reductions cannot express EC addition, so the sum is one more device MSM
-    with unit scalars (eon_g1_multi_exp).  Returns the (8,) affine result on every rank."""
+def msm_sharded(bases, scalars_local, device, group=None, collective=None):
+    """sum_i s_i P_i over every rank's range: eon_msm_sharded_dev (include/eon.h) -- a full
+    Pippenger per rank on its contiguous range (`bases` = MsmBases over that range), an all-gather
+    of the G affine partial points and their sum by EC additions (RCCL reductions cannot add curve
+    points).  Returns the (8,) affine result (u64 limbs) on every rank."""
     import torch
+    import torch.distributed as dist
 
-    from .field import fr_mont
-    from .msm import multi_exp
+    from .collective import TorchCollective
 
-    part = bases.msm(scalars_local)
-    t = torch.from_numpy(np.ascontiguousarray(part).view(np.int64)).to(device)
-    parts = all_gather_rows(t, group).cpu().numpy().view(np.uint64).reshape(-1, 8)
-    ones = np.zeros((parts.shape[0], 4), dtype=np.uint64)
-    one = fr_mont(1)
-    for i in range(4):
-        ones[:, i] = (one >> (64 * i)) & 0xFFFFFFFFFFFFFFFF
-    return multi_exp(parts, ones, bases.ctx)
+    ctx = bases.ctx
+    dev = torch.device(device)
+    s = torch.as_tensor(np.ascontiguousarray(scalars_local).view(np.int64)) if isinstance(scalars_local, np.ndarray) \
+        else scalars_local
+    s = s.reshape(-1, 4).contiguous().to(dev)
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    coll = None
+    if world > 1:
+        coll = collective or TorchCollective(dist.get_rank(group), world, group, dev.index or 0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    out = (_lib.eon_g1_affine)()
+    ctx.check(ctx.lib.eon_msm_sharded_dev(ctx.handle, bases._h, ctypes.c_void_p(s.data_ptr()), int(s.shape[0]),
+                                          ctypes.byref(coll.c) if coll is not None else None, ctypes.byref(out)))
+    return np.array(list(out.x) + list(out.y), dtype=np.uint64)

@@ -20,6 +20,7 @@ from pathlib import Path
 import numpy as np
 
 from . import _lib
+from .collective import ALL_GATHER_FN, TorchCollective, eon_collective  # noqa: F401 (re-exported)
 from .dft import Context, default_context
 from .field import fr_to_abi, fr_unmont
 from .kzg import Opened
@@ -35,13 +36,6 @@ _INT = ctypes.c_int
 STAGES = ["commit to trace data", "trace LDE (get_evaluations_on_domain)", "quotient_values",
           "exchange partial quotients", "commit to quotient poly chunks", "open", "assemble columns"]
 EON_STAGES = 8
-
-ALL_GATHER_FN = ctypes.CFUNCTYPE(_INT, _P, _P, _P, _U64, _P)
-
-
-class eon_collective(ctypes.Structure):
-    _fields_ = [("rank", _U32), ("world", _U32), ("all_gather", ALL_GATHER_FN), ("user", _P)]
-
 
 class eon_proof(ctypes.Structure):
     _fields_ = [("trace_commit", _P), ("quotient_commit", _P), ("trace_opened", _P), ("trace_witnesses", _P),
@@ -121,43 +115,6 @@ class NativeKzgPcs:
             self.close()
         except Exception:
             pass
-
-
-class _DevBytes:
-    """A raw device allocation seen as a uint8 torch tensor (zero-copy, __cuda_array_interface__)."""
-
-    def __init__(self, ptr: int, nbytes: int):
-        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
-                                         "version": 2}
-
-
-class TorchCollective:
-    """eon_collective whose all-gather is torch.distributed over `group` (any backend)."""
-
-    def __init__(self, rank: int, world: int, group=None, device=0):
-        self.group = group
-        self.device = device
-
-        def all_gather(user, send, recv, nbytes, stream):
-            try:
-                import torch
-
-                from .distributed import all_gather_rows
-
-                torch.cuda.synchronize(self.device)  # the driver's stream has produced `send`
-                s = torch.as_tensor(_DevBytes(send, nbytes), device=f"cuda:{self.device}")
-                r = torch.as_tensor(_DevBytes(recv, nbytes * world), device=f"cuda:{self.device}")
-                r.copy_(all_gather_rows(s, self.group).reshape(-1))
-                torch.cuda.synchronize(self.device)
-                return 0
-            except Exception:  # a Python exception must not unwind through the C caller
-                import traceback
-
-                traceback.print_exc()
-                return 1
-
-        self._fn = ALL_GATHER_FN(all_gather)  # keep the thunk alive
-        self.c = eon_collective(rank, world, self._fn, None)
 
 
 class RcclCollective:

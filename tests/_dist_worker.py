@@ -246,11 +246,18 @@ def run_fourstep(rank, world, group):
         n = 1 << log_n
         x = C.random_fr(log_n + 40, n).reshape(n, 4)
         local = torch.from_numpy(np.ascontiguousarray(D.fourstep_scatter(x, log_n, rank, world)).view(np.int64))
+        full = C.dft_batch(x.reshape(n, 1, 4)).reshape(n, 4)
+        # one all_to_all: the rank's block of the N2 x N1 view
         out = D.fourstep_dft(ctx, local.to("cuda:0"), log_n, rank, world, group)
         got = out.cpu().numpy().view(np.uint64).reshape(-1, 4)
-        want = C.dft_batch(x.reshape(n, 1, 4)).reshape(n, 4)[D.fourstep_gather_index(log_n, rank, world)]
-        if not np.array_equal(got, want):
-            return f"four-step DFT 2^{log_n} rank {rank}/{world}"
+        if not np.array_equal(got, full[D.fourstep_gather_index(log_n, rank, world)]):
+            return f"four-step DFT 2^{log_n} rank {rank}/{world} (transposed layout)"
+        # second all_to_all: the rank's contiguous natural slice
+        out = D.fourstep_dft(ctx, local.to("cuda:0"), log_n, rank, world, group, natural=True)
+        got = out.cpu().numpy().view(np.uint64).reshape(-1, 4)
+        per = n // world
+        if not np.array_equal(got, full[rank * per:(rank + 1) * per]):
+            return f"four-step DFT 2^{log_n} rank {rank}/{world} (natural layout)"
     return None
 
 

@@ -81,3 +81,14 @@ def test_prove_driver_calls_only_the_c_abi():
     for p in (ROOT / "plonky3_eon_amd" / "host").glob("*"):
         text = p.read_text()
         assert "csrc/" not in text and '#include "field.h"' not in text and '#include "context.h"' not in text, p
+
+
+def test_collective_struct_layout():
+    """eon_collective (include/eon.h) as the Python binding lays it out: a Rust / C caller's struct
+    must match (rank, world, all_gather, user, all_to_all)."""
+    import ctypes
+
+    from plonky3_eon_amd.collective import eon_collective
+
+    offs = [getattr(eon_collective, f).offset for f, _ in eon_collective._fields_]
+    assert offs == [0, 4, 8, 16, 24] and ctypes.sizeof(eon_collective) == 32

@@ -22,14 +22,16 @@ def test_native_sharded_prove_matches_single(world, log_n, vl):
     assert all(r["ok"] for r in res), [r["why"] for r in res]
 
 
-@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_fourstep_dft_matches_oracle(world):
+    """eon_fourstep_dft_dev over a TorchCollective (gloo ranks sharing cuda:0), both layouts."""
     res = run_world("fourstep", world, timeout=900)
     assert all(r["ok"] for r in res), [r["why"] for r in res]
 
 
-@pytest.mark.parametrize("world", [1, 3])
+@pytest.mark.parametrize("world", [1, 3, 8])
 def test_sharded_msm_matches_full(world):
+    """eon_msm_sharded_dev: per-rank Pippenger + all-gather of partials + EC sum == the full MSM."""
     res = run_world("msmshard", world, timeout=900)
     assert all(r["ok"] for r in res), [r["why"] for r in res]
 

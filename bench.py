@@ -272,8 +272,9 @@ class ProveWorkload:
     them constant).  At N > 1 the ONE proof is split
     by vector lane over the ranks (plonky3_eon_amd/distributed.py): strong scaling.
 
-    --host native (default) runs the C++ prove driver (libeonprove.so, include/eon_prove.h; at N > 1
-    its own RCCL all-gathers); --host python the Python mirror (prover.py).  Same proof."""
+    The prove runs in the C++ driver (libeonprove.so, include/eon_prove.h; at N > 1 its
+    all-gathers go through torch.distributed's RCCL group or, --collective rccl, its own
+    communicator)."""
 
     scaling = "strong"
 
@@ -282,7 +283,6 @@ class ProveWorkload:
 
         from plonky3_eon_amd.air import Poseidon2Air
         from plonky3_eon_amd.distributed import Shard
-        from plonky3_eon_amd.kzg import GpuKzgPcs
 
         self.args, self.ctx = args, ctx
         self.log_n, self.vl = args.log_trace, args.vector_len
@@ -292,21 +292,15 @@ class ProveWorkload:
         l0, l1 = self.shard.lanes if self.shard else (0, self.vl)
         self.consts = p2_constants_limbs(99)
         self.air = Poseidon2Air(*self.consts, l1 - l0, ctx)
-        self.native = args.host == "native"
-        if self.native:
-            from plonky3_eon_amd.native import NativeKzgPcs, RcclCollective
+        from plonky3_eon_amd.native import NativeKzgPcs, RcclCollective, TorchCollective
 
-            from plonky3_eon_amd.native import TorchCollective
-
-            self.pcs = NativeKzgPcs(n, 12345, ctx)
-            self.coll = None
-            if world > 1:
-                # torch's RCCL process group (all_gather_into_tensor on device) by default; the
-                # driver's own communicator with --collective rccl
-                self.coll = (RcclCollective(rank, world) if args.collective == "rccl"
-                             else TorchCollective(rank, world, None, device=dev.index))
-        else:
-            self.pcs = GpuKzgPcs(n, 12345, ctx)
+        self.pcs = NativeKzgPcs(n, 12345, ctx)
+        self.coll = None
+        if world > 1:
+            # torch's RCCL process group (all_gather_into_tensor on device) by default; the
+            # driver's own communicator with --collective rccl
+            self.coll = (RcclCollective(rank, world) if args.collective == "rccl"
+                         else TorchCollective(rank, world, None, device=dev.index))
         # the same 2^(log_n) x VECTOR_LEN permutation inputs on every rank; rank g takes its lanes
         # (permutation j sits at row j / VECTOR_LEN, lane j % VECTOR_LEN)
         inputs = synthetic_fr(n * self.vl, 3, 5).reshape(n, self.vl, 3, 4)[:, l0:l1]
@@ -319,18 +313,12 @@ class ProveWorkload:
         self.timings = []
 
     def step(self):
-        from plonky3_eon_amd.native import Challenger, Poseidon2Constants
-        from plonky3_eon_amd.prover import prove
+        from plonky3_eon_amd.native import Challenger, Poseidon2Constants, prove_native
 
         # config.initialise_challenger() per proof (prover.rs:164)
         ch = Challenger(Poseidon2Constants(*self.ch_consts)) if self.fs else None
-        if self.native:
-            from plonky3_eon_amd.native import prove_native
-
-            p = prove_native(self.air, self.pcs, self.trace, self.alpha, self.zeta, collective=self.coll,
-                             challenger=ch)
-        else:
-            p = prove(self.air, self.pcs, self.trace, self.alpha, self.zeta, shard=self.shard, challenger=ch)
+        p = prove_native(self.air, self.pcs, self.trace, self.alpha, self.zeta, collective=self.coll,
+                         challenger=ch)
         self.timings.append(p.timings_ms)
 
     def describe(self, world):
@@ -492,12 +480,10 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--serial", action="store_true",
                     help="every step in serial mode (eon_ctx_set_serial): for rocprofv3 kernel traces "
                          "whose per-kernel durations are isolated")
-    ap.add_argument("--host", choices=["native", "python"], default="native",
-                    help="prove: C++ driver (libeonprove.so) or the Python mirror")
     ap.add_argument("--transcript", choices=["fs", "fixed"], default="fs",
                     help="prove: alpha/zeta from the Fiat-Shamir transcript (default) or fixed")
     ap.add_argument("--collective", choices=["torch", "rccl"], default="torch",
-                    help="prove --host native at N > 1: all-gathers through torch.distributed (RCCL "
+                    help="prove at N > 1: all-gathers through torch.distributed (RCCL "
                          "process group) or the driver's own RCCL communicator")
     return ap
 

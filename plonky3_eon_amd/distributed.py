@@ -2,7 +2,8 @@
 RCCL over xGMI on the MI355X node; "gloo" for the CPU tests and for several ranks sharing one
 GPU).  Three shardings:
 
-* the eon-uni-stark prove split by vector lane (below; `prover.prove(..., shard=Shard(...))`);
+* the eon-uni-stark prove split by vector lane (below; the C++ driver's `eon_prove_p2air(_fs)` with
+  an eon_collective, and the test-only Python mirror `tests/mirror_prover.prove(..., shard=)`);
 * a single large forward DFT as a four-step N1 x N2 transform with one all_to_all
   (`fourstep_dft`, BASELINE configs[4] (i));
 * an MSM split by point range with an all-gather of per-rank partial points

@@ -1,8 +1,8 @@
 """ctypes binding of the native prove driver libeonprove.so (include/eon_prove.h).
 
 The driver is the C++ host side above eon.h (plonky3_eon_amd/host/): KzgPcs + prove for the
-Poseidon2-AIR, the same orchestration as prover.py/kzg.py but without the Python interpreter in the
-loop.  Its Proof has prover.Proof's shape, so the two are compared field by field in the tests.
+Poseidon2-AIR, the product host (tests/mirror_prover.py is a test-only Python mirror of the same
+orchestration).  Its Proof has prover.Proof's shape, so the two are compared field by field in the tests.
 
 Sharded prove: an eon_collective is either
 * ``TorchCollective(group)`` -- a ctypes callback over torch.distributed (gloo stages through host
@@ -23,8 +23,7 @@ from . import _lib
 from .collective import ALL_GATHER_FN, TorchCollective, eon_collective  # noqa: F401 (re-exported)
 from .dft import Context, default_context
 from .field import fr_to_abi, fr_unmont
-from .kzg import Opened
-from .prover import Proof, log_quotient_degree
+from .proof import Opened, Proof, log_quotient_degree
 
 PROVE_LIB_PATH = Path(__file__).resolve().parent / "libeonprove.so"
 

@@ -4,7 +4,7 @@ RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment, backend gloo).
   cpu  -- the sharding arithmetic and exchange with the C restatement oracle as the per-rank
           compute: per-lane trace slices, partial quotients, all_gather_rows, lane weights and
           gather_columns must reproduce the single-process oracle quotient.
-  gpu  -- the product path (plonky3_eon_amd.prover.prove with a Shard) on cuda:0 for every rank;
+  gpu  -- the product path (tests/mirror_prover.prove with a Shard) on cuda:0 for every rank;
           rank 0 also runs the unsharded prove and every proof field must match bit for bit.
   a2a  -- all_to_all_blocks layout, and the four-step decomposition with oracle DFTs standing in
           for the kernels (CPU).
@@ -100,8 +100,8 @@ def run_gpu(rank, world, group):
     from plonky3_eon_amd import Context
     from plonky3_eon_amd import distributed as D
     from plonky3_eon_amd.air import Poseidon2Air
-    from plonky3_eon_amd.kzg import GpuKzgPcs
-    from plonky3_eon_amd.prover import prove
+    from mirror_kzg import GpuKzgPcs
+    from mirror_prover import prove
 
     log_n, vl = int(os.environ.get("EON_T_LOG_N", "5")), int(os.environ.get("EON_T_VL", "4"))
     n = 1 << log_n
@@ -152,9 +152,9 @@ def run_native(rank, world, group):
     from plonky3_eon_amd import Context
     from plonky3_eon_amd import distributed as D
     from plonky3_eon_amd.air import Poseidon2Air
-    from plonky3_eon_amd.kzg import GpuKzgPcs
+    from mirror_kzg import GpuKzgPcs
     from plonky3_eon_amd.native import Challenger, NativeKzgPcs, Poseidon2Constants, TorchCollective, prove_native
-    from plonky3_eon_amd.prover import prove
+    from mirror_prover import prove
 
     log_n, vl = int(os.environ.get("EON_T_LOG_N", "5")), int(os.environ.get("EON_T_VL", "4"))
     n = 1 << log_n

@@ -1,4 +1,5 @@
-"""Host-side mirror of p3-kzg's KzgPcs over the C ABI, with every matrix device-resident.
+"""TEST-ONLY Python mirror of p3-kzg's KzgPcs over the C ABI, with every matrix device-resident
+(the product is the C++ KzgPcs in plonky3_eon_amd/host/pcs.cpp; this one cross-checks it).
 
 Reference: ``KzgPcs`` (kzg/src/pcs.rs:143-402) implementing ``Pcs<Fr, Challenger>``
 (commit/src/pcs.rs:21-187) over ``TwoAdicMultiplicativeCoset`` domains (commit/src/domain.rs).
@@ -29,10 +30,11 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import _lib
-from .dft import Context, Radix2Dit, default_context
-from .field import FR_MODULUS, fr_mont, fr_to_abi, fr_unmont
-from .msm import MsmBases, srs_powers
+from plonky3_eon_amd import _lib
+from plonky3_eon_amd.dft import Context, Radix2Dit, default_context
+from plonky3_eon_amd.field import FR_MODULUS, fr_mont, fr_to_abi, fr_unmont  # noqa: F401
+from plonky3_eon_amd.msm import MsmBases, srs_powers
+from plonky3_eon_amd.proof import Opened
 
 GENERATOR = 5
 _TWO_ADIC_GENERATOR_MONT = (0x636E735580D13D9C, 0xA22BF3742445FFD6, 0x56452AC01EB203D8, 0x1860EF942963F9E7)
@@ -83,12 +85,6 @@ class MatrixProverData:
     evals: object
     coeffs: object
     prepared: object = None  # msm.PreparedScalars of coeffs (the commitment's sorted digits)
-
-
-@dataclass
-class Opened:
-    values: list = field(default_factory=list)     # [matrix][point] -> (width, 4) u64 Fr
-    witnesses: list = field(default_factory=list)  # [matrix][point] -> (width, 8) u64 G1
 
 
 class GpuKzgPcs:

@@ -1,4 +1,8 @@
-"""Host-side mirror of eon_uni_stark::prove for the Poseidon2-AIR with KzgPcs, on device.
+"""TEST-ONLY Python mirror of eon_uni_stark::prove for the Poseidon2-AIR with KzgPcs, on device.
+
+The product host is the C++ driver (plonky3_eon_amd/host, libeonprove.so); this second host over
+the same C ABI stays in tests/ to cross-check it field by field (tests/test_gpu_prove.py) and to
+exercise the lane-sharded Python orchestration (tests/_dist_worker.py).
 
 Reference: prove / prove_with_preprocessed (eon-uni-stark/src/prover.rs:28-534), specialised to
 what the benchmark AIR exercises: no preprocessed columns, no lookups, ZK off
@@ -17,31 +21,12 @@ the reference's span names ("commit to trace data", "commit to quotient poly chu
 from __future__ import annotations
 
 import time
-from dataclasses import dataclass, field
 
 import numpy as np
 
-from .field import FR_MODULUS, fr_mont, fr_unmont
-from .kzg import Domain, GpuKzgPcs
-
-
-@dataclass
-class Proof:
-    """eon-uni-stark/src/proof.rs:19-44 (commitments, opened values, opening proof, degree bits)."""
-
-    trace_commit: object
-    quotient_commit: object
-    opened: object
-    degree_bits: int
-    timings_ms: dict = field(default_factory=dict)
-    alpha: int | None = None  # the challenges used (canonical ints)
-    zeta: int | None = None
-
-
-def log_quotient_degree(max_constraint_degree: int) -> int:
-    """get_log_quotient_degree (eon-uni-stark/src/symbolic_builder.rs:15-43), ZK off."""
-    d = max(max_constraint_degree, 2) - 1
-    return (d - 1).bit_length()
+from mirror_kzg import Domain, GpuKzgPcs
+from plonky3_eon_amd.field import FR_MODULUS, fr_mont, fr_unmont
+from plonky3_eon_amd.proof import Proof, log_quotient_degree  # noqa: F401 (re-exported)
 
 
 def prove(air, pcs: GpuKzgPcs, trace, alpha: int | None, zeta: int | None, max_constraint_degree: int = 3,
@@ -58,7 +43,7 @@ def prove(air, pcs: GpuKzgPcs, trace, alpha: int | None, zeta: int | None, max_c
     """
     import torch
 
-    from . import distributed as D
+    from plonky3_eon_amd import distributed as D
 
     def tick():
         torch.cuda.synchronize(trace.device)

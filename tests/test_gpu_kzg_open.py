@@ -72,7 +72,7 @@ def test_eval_columns_multi_point(gpu_ctx, rows, width, npts):
     import torch
 
     from plonky3_eon_amd import _lib
-    from plonky3_eon_amd.kzg import fr_to_abi
+    from plonky3_eon_amd.field import fr_to_abi
 
     coeffs = C.random_fr(rows + npts, rows * width).reshape(rows, width, 4)
     points = [C.fr_from_u64(0)] + list(C.random_fr(rows + 7, npts - 1)) if npts > 1 else [C.fr_from_u64(5)]
@@ -96,7 +96,7 @@ def test_eval_columns_edge_cases(gpu_ctx):
     import torch
 
     from plonky3_eon_amd import _lib
-    from plonky3_eon_amd.kzg import fr_to_abi
+    from plonky3_eon_amd.field import fr_to_abi
 
     lib, h = gpu_ctx.lib, gpu_ctx.handle
     out = torch.full((2, 3, 4), 7, dtype=torch.int64, device="cuda:0")

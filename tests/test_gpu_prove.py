@@ -30,7 +30,7 @@ def test_open_kernel_vs_oracle(gpu_ctx, prepared):
     the committed coefficients against the opening bases."""
     import torch
 
-    from plonky3_eon_amd.kzg import GpuKzgPcs, MatrixProverData, Domain
+    from mirror_kzg import GpuKzgPcs, MatrixProverData, Domain
 
     pcs = GpuKzgPcs(600, 12345, gpu_ctx)
     for rows, w in [(1, 2), (2, 3), (257, 5), (600, 3)]:
@@ -53,8 +53,8 @@ def test_prove_vs_oracle(gpu_ctx, consts, log_n, vl):
     import torch
 
     from plonky3_eon_amd.air import Poseidon2Air
-    from plonky3_eon_amd.kzg import GpuKzgPcs
-    from plonky3_eon_amd.prover import prove
+    from mirror_kzg import GpuKzgPcs
+    from mirror_prover import prove
 
     n = 1 << log_n
     alpha_srs = 12345
@@ -86,8 +86,8 @@ def test_open_routes_agree_full_height(gpu_ctx, consts):
     import torch
 
     from plonky3_eon_amd.air import Poseidon2Air
-    from plonky3_eon_amd.kzg import GpuKzgPcs
-    from plonky3_eon_amd.prover import prove
+    from mirror_kzg import GpuKzgPcs
+    from mirror_prover import prove
 
     log_n, vl = 17, 1
     n = 1 << log_n
@@ -165,8 +165,8 @@ def test_native_prove_fiat_shamir_vs_oracle(gpu_ctx, consts, log_n, vl):
     assert (proof.alpha, proof.zeta) == (want["alpha"], want["zeta"])
     np.testing.assert_array_equal(ch.state(), np.stack([lim(x) for x in ref.state]))
     # the Python mirror (prover.py) with its own challenger samples the same challenges
-    from plonky3_eon_amd.kzg import GpuKzgPcs
-    from plonky3_eon_amd.prover import prove
+    from mirror_kzg import GpuKzgPcs
+    from mirror_prover import prove
 
     ch2 = Challenger(Poseidon2Constants([[lim(x) for x in r] for r in pyc[0]], [lim(x) for x in pyc[1]],
                                         [[lim(x) for x in r] for r in pyc[2]]))

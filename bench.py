@@ -211,12 +211,42 @@ def p2_constants_limbs(seed: int, hf: int = 4, pr: int = 56):
     return x[:3 * hf].reshape(hf, 3, 4), x[3 * hf:3 * hf + pr], x[3 * hf + pr:].reshape(hf, 3, 4)
 
 
-def cpu_baseline_prove(log_n: int, vl: int, consts) -> dict:
-    """Projected reference-algorithm prove time on this host from full-size component samples
-    (a full CPU run is infeasible: get_evaluations_on_domain's Horner is ~4.5e13 mulmods)."""
+def _cpu_prove_e2e(log_n: int, vl: int, consts, horner: bool) -> dict:
+    """One end-to-end prove of the C restatement (oracle/prove_oracle.py: commit, LDE, quotient,
+    quotient commit, open with the reference's per-column quotient_and_eval + commit_column) at
+    log-trace log_n; horner=False substitutes the coset-DFT LDE for the reference's Horner
+    get_evaluations_on_domain (kzg/src/pcs.rs:267-287)."""
+    from oracle import coracle as C
+    from oracle import prove_oracle
+
+    n = 1 << log_n
+    k = C.P2Constants(*consts)
+    tr = C.p2_generate_trace(synthetic_fr(n * vl, 3, 5).reshape(-1, 3, 4), vl, k)
+    srs = C.g1_srs(n + 1, C.fr_from_u64(12345))
+
+    def lde_sub(coeffs, log_q, shift):
+        pad = np.zeros(((1 << log_q) - coeffs.shape[0],) + coeffs.shape[1:], dtype=np.uint64)
+        return C.coset_dft_batch(np.concatenate([coeffs, pad]), shift)
+
+    st = {}
+    t0 = time.perf_counter()
+    prove_oracle.prove(tr, srs, k, vl, 7, 11, lde_fn=None if horner else lde_sub, timings=st)
+    dt = time.perf_counter() - t0
+    return {"log_trace": log_n, "lde": "horner (reference)" if horner else "coset DFT (substituted)",
+            "ms": round(dt * 1e3, 1), "stage_ms": {a: round(b * 1e3, 1) for a, b in st.items()}}
+
+
+def cpu_baseline_prove(log_n: int, vl: int, consts, full: bool = False) -> dict:
+    """CPU restatement of the prove on this host: MEASURED end-to-end proves at small log-trace
+    sizes, and the full-size figure PROJECTED from measured full-size
+    components (C4 (ii); a full CPU run is infeasible: get_evaluations_on_domain's Horner is
+    ~4.5e13 mulmods)."""
     from oracle import coracle as C
 
     C.build()
+    measured = [_cpu_prove_e2e(8, vl, consts, True), _cpu_prove_e2e(10, vl, consts, False)]
+    if full:  # --cpu-full: the larger C4 (i) points (minutes)
+        measured += [_cpu_prove_e2e(10, vl, consts, True), _cpu_prove_e2e(12, vl, consts, False)]
     n = 1 << log_n
     w = 164 * vl
     q = 2 * n
@@ -226,13 +256,15 @@ def cpu_baseline_prove(log_n: int, vl: int, consts) -> dict:
     x = synthetic_fr(n, 16, 11)
     t0 = time.perf_counter(); C.idft_batch(x); dt = time.perf_counter() - t0
     comp["trace idft"] = dt * w / 16
-    # one MSM of n points; prove runs w (trace) + 2 (quotient) + 2w + 2 (open) of them
+    # one full-size MSM of n points (signed-window Pippenger, OpenMP inside, as the reference runs
+    # each commit_column); prove runs w (trace) + 2 (quotient) + 2w + 2 (open) of them
     pts = C.g1_srs(1 << 12, alpha)
     pts = np.concatenate([pts] * (n >> 12))
     s = synthetic_fr(n, 1, 12).reshape(n, 4)
     t0 = time.perf_counter(); C.g1_msm(pts, s); dt = time.perf_counter() - t0
     n_msm = 3 * w + 4
     comp["msm x%d" % n_msm] = dt * n_msm
+    msm_ms = dt * 1e3  # noqa
     # get_evaluations_on_domain by Horner (kzg/src/pcs.rs:267-287): Q * w evaluations of degree n
     coeffs = synthetic_fr(n, 1, 13)
     t0 = time.perf_counter()
@@ -256,11 +288,14 @@ def cpu_baseline_prove(log_n: int, vl: int, consts) -> dict:
         "cores": C.num_threads(),
         "kind": "port",
         "projected": True,
-        "sample": "projected = sum of full-size component samples of the C restatement (trace idft 16/%d "
-                  "cols, one 2^%d MSM x %d, Horner LDE 16 points, quotient 4096 rows); reference "
-                  "algorithms incl. the Horner get_evaluations_on_domain" % (w, log_n, n_msm),
+        "sample": "value = full-size prove PROJECTED as the sum of full-size component samples of the C "
+                  "restatement (trace idft 16/%d cols, one measured 2^%d MSM x %d, Horner LDE 16 points, "
+                  "quotient 4096 rows), reference algorithms incl. the Horner get_evaluations_on_domain; "
+                  "`measured` holds end-to-end proves of the same AIR run here" % (w, log_n, n_msm),
         "components_ms": {k2: round(v * 1e3, 1) for k2, v in comp.items()},
+        "msm_2_%d_measured_ms" % log_n: round(msm_ms, 1),
         "with_coset_lde_ms": round(alt * 1e3, 1),
+        "measured": measured,
     }
 
 
@@ -339,7 +374,7 @@ class ProveWorkload:
         }, None
 
     def cpu_baseline(self):
-        return cpu_baseline_prove(self.log_n, self.vl, self.consts)
+        return cpu_baseline_prove(self.log_n, self.vl, self.consts, full=self.args.cpu_full)
 
 
 
@@ -477,6 +512,8 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--log-msm", type=int, default=20)
     ap.add_argument("--cpu-sample-cols", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="prove: also the larger end-to-end CPU restatement runs (2^10 Horner, 2^12; minutes)")
     ap.add_argument("--serial", action="store_true",
                     help="every step in serial mode (eon_ctx_set_serial): for rocprofv3 kernel traces "
                          "whose per-kernel durations are isolated")

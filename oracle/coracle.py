@@ -61,13 +61,15 @@ def lib():
         l.or_kzg_evaluations_on_domain.argtypes = [P, U64, U64, U32, fr_t, P]
         l.or_kzg_evaluations_on_domain.restype = None
         for k, a in {"or_g1_generator": [P], "or_g1_mul": [P, P, P], "or_g1_add": [P, P, P],
-                     "or_g1_srs": [U64, P, P], "or_g1_msm": [P, P, U64, P]}.items():
+                     "or_g1_srs": [U64, P, P], "or_g1_msm": [P, P, U64, P],
+                     "or_g1_msm_columns": [P, P, U64, U64, P]}.items():
             getattr(l, k).argtypes = a
             getattr(l, k).restype = None
         for k, a in {"or_p2_generate_trace": [P, U64, U32, U32, U32, P, P, P, P],
                      "or_selectors_on_coset": [U32, U32, fr_t, P, P, P, P],
                      "or_p2_quotient_values": [P, U32, U32, U32, U32, U32, P, P, P, fr_t, P],
                      "or_quotient_and_eval": [P, U64, U64, fr_t, P, P],
+                     "or_open_columns": [P, P, U64, U64, fr_t, P, P],
                      "or_bary_eval_cols": [P, U64, U64, P, U32, P]}.items():
             getattr(l, k).argtypes = a
             getattr(l, k).restype = None
@@ -226,6 +228,30 @@ def g1_msm(points, scalars):
     out = np.zeros(8, dtype=np.uint64)
     lib().or_g1_msm(_ptr(p), _ptr(s), p.shape[0], _ptr(out))
     return out
+
+
+def g1_msm_columns(points, mat):
+    """KzgPcs::commit's per-column commit_column (kzg/src/pcs.rs:244-251) of an (n, w, 4) matrix
+    against points[:n] -> (w, 8); columns in parallel."""
+    p = np.ascontiguousarray(points, dtype=np.uint64)
+    m = np.ascontiguousarray(mat, dtype=np.uint64)
+    n, w = m.shape[0], m.shape[1]
+    out = np.zeros((w, 8), dtype=np.uint64)
+    lib().or_g1_msm_columns(_ptr(p), _ptr(m), n, w, _ptr(out))
+    return out
+
+
+def open_columns(points, coeffs, z_limbs):
+    """KzgPcs::open of one (n, w, 4) coefficient matrix at one point (kzg/src/pcs.rs:289-335):
+    per column quotient_and_eval and commit_column(quotient) over points[:n-1] -> (values (w, 4),
+    witnesses (w, 8)); columns in parallel."""
+    p = np.ascontiguousarray(points, dtype=np.uint64)
+    c = np.ascontiguousarray(coeffs, dtype=np.uint64)
+    n, w = c.shape[0], c.shape[1]
+    vals = np.zeros((w, 4), dtype=np.uint64)
+    wits = np.zeros((w, 8), dtype=np.uint64)
+    lib().or_open_columns(_ptr(p), _ptr(c), n, w, fr(z_limbs), _ptr(vals), _ptr(wits))
+    return vals, wits
 
 
 # --- Poseidon2-AIR / quotient / open ----------------------------------------------------------

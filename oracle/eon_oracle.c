@@ -686,49 +686,215 @@ void or_g1_srs(uint64_t n, const fr_t* alpha, g1_affine_t* out) {
     }
 }
 
-void or_g1_msm(const g1_affine_t* pts, const fr_t* scalars, uint64_t n, g1_affine_t* out) {
-    /* Pippenger (bucket method), unsigned c-bit windows, OpenMP over windows; the value of
-     * G1::multi_exp (bn254/src/curve.rs:158-179).  Empty input -> identity. */
+/* XYZZ coordinates (x = X / ZZ, y = Y / ZZZ; ZZ = 0 is the identity) for the Pippenger buckets */
+typedef struct {
+    fq_t X, Y, ZZ, ZZZ;
+} g1x_t;
+
+static g1x_t xinf(void) {
+    g1x_t r;
+    memset(&r, 0, sizeof r);
+    r.X = qone();
+    r.Y = qone();
+    return r;
+}
+
+static g1x_t xdbl(g1x_t p) { /* dbl-2008-s-1, a = 0 */
+    if (qzero(p.ZZ)) return p;
+    fq_t U = qadd(p.Y, p.Y), V = qmul(U, U), W = qmul(U, V), S = qmul(p.X, V);
+    fq_t X2 = qmul(p.X, p.X), M = qadd(qadd(X2, X2), X2);
+    g1x_t r;
+    r.X = qsub(qmul(M, M), qadd(S, S));
+    r.Y = qsub(qmul(M, qsub(S, r.X)), qmul(W, p.Y));
+    r.ZZ = qmul(V, p.ZZ);
+    r.ZZZ = qmul(W, p.ZZZ);
+    return r;
+}
+
+static g1x_t xdbl_affine(fq_t x, fq_t y) { /* mdbl-2008-s-1 */
+    fq_t U = qadd(y, y), V = qmul(U, U), W = qmul(U, V), S = qmul(x, V);
+    fq_t X2 = qmul(x, x), M = qadd(qadd(X2, X2), X2);
+    g1x_t r;
+    r.X = qsub(qmul(M, M), qadd(S, S));
+    r.Y = qsub(qmul(M, qsub(S, r.X)), qmul(W, y));
+    r.ZZ = V;
+    r.ZZZ = W;
+    return r;
+}
+
+static void xmadd(g1x_t* p, fq_t x, fq_t y) { /* madd-2008-s: p += (x, y) affine, 8M + 2S */
+    if (qzero(p->ZZ)) {
+        p->X = x;
+        p->Y = y;
+        p->ZZ = qone();
+        p->ZZZ = qone();
+        return;
+    }
+    fq_t U2 = qmul(x, p->ZZ), S2 = qmul(y, p->ZZZ);
+    fq_t P = qsub(U2, p->X), R = qsub(S2, p->Y);
+    if (qzero(P)) {
+        if (qzero(R))
+            *p = xdbl_affine(x, y);
+        else
+            *p = xinf();
+        return;
+    }
+    fq_t PP = qmul(P, P), PPP = qmul(P, PP), Q = qmul(p->X, PP);
+    fq_t X3 = qsub(qsub(qmul(R, R), PPP), qadd(Q, Q));
+    p->Y = qsub(qmul(R, qsub(Q, X3)), qmul(p->Y, PPP));
+    p->X = X3;
+    p->ZZ = qmul(p->ZZ, PP);
+    p->ZZZ = qmul(p->ZZZ, PPP);
+}
+
+static void xadd(g1x_t* p, const g1x_t* q) { /* add-2008-s: p += q */
+    if (qzero(q->ZZ)) return;
+    if (qzero(p->ZZ)) {
+        *p = *q;
+        return;
+    }
+    fq_t U1 = qmul(p->X, q->ZZ), U2 = qmul(q->X, p->ZZ), S1 = qmul(p->Y, q->ZZZ), S2 = qmul(q->Y, p->ZZZ);
+    fq_t P = qsub(U2, U1), R = qsub(S2, S1);
+    if (qzero(P)) {
+        if (qzero(R))
+            *p = xdbl(*p);
+        else
+            *p = xinf();
+        return;
+    }
+    fq_t PP = qmul(P, P), PPP = qmul(P, PP), Q = qmul(U1, PP);
+    fq_t X3 = qsub(qsub(qmul(R, R), PPP), qadd(Q, Q));
+    p->Y = qsub(qmul(R, qsub(Q, X3)), qmul(S1, PPP));
+    p->X = X3;
+    p->ZZ = qmul(qmul(p->ZZ, q->ZZ), PP);
+    p->ZZZ = qmul(qmul(p->ZZZ, q->ZZZ), PPP);
+}
+
+static void xto_affine(g1x_t p, g1_affine_t* out) {
+    if (qzero(p.ZZ)) {
+        memset(out, 0, sizeof *out);
+        return;
+    }
+    fq_t x = qmul(p.X, qinv(p.ZZ)), y = qmul(p.Y, qinv(p.ZZZ));
+    memcpy(out->x, x.v, 32);
+    memcpy(out->y, y.v, 32);
+}
+
+/* Pippenger core: scalars[i * stride]; `par` = OpenMP inside (one large MSM) or serial (the
+ * caller parallelises over many MSMs: or_g1_msm_columns / or_open_columns) */
+static void msm_core(const g1_affine_t* pts, const fr_t* scalars, uint64_t stride, uint64_t n, g1_affine_t* out,
+                     int par) {
+    /* The value of G1::multi_exp (bn254/src/curve.rs:158-179; halo2curves' msm_best is not in the
+     * tree).  Pippenger with SIGNED c-bit windows (digits in [-2^(c-1), 2^(c-1)], 2^(c-1) buckets
+     * per window), XYZZ buckets with mixed additions of the affine bases (madd-2008-s), and OpenMP
+     * over (window, point chunk) tasks so that every thread has work at any window count; the
+     * chunks' buckets of a window are merged, then each window's running sum, then the windows by
+     * doublings.  Empty input -> identity. */
     if (n == 0) {
         memset(out, 0, sizeof *out);
         return;
     }
     uint32_t lg = 0;
     while ((1ull << (lg + 1)) <= n) lg++;
-    uint32_t c = lg > 3 ? lg - 2 : 2;
+    uint32_t c = lg > 5 ? lg - 3 : 2; /* ~n / 8 buckets per window */
     if (c > 16) c = 16;
-    uint32_t nw = (254 + c - 1) / c;
-    uint64_t* ks = (uint64_t*)malloc(sizeof(uint64_t) * 4 * n);
-    for (uint64_t i = 0; i < n; i++) fr_canonical(&scalars[i], ks + 4 * i);
-    g1j_t* wsum = (g1j_t*)malloc(sizeof(g1j_t) * nw);
-#pragma omp parallel for schedule(dynamic, 1)
-    for (uint32_t w = 0; w < nw; w++) {
-        uint64_t nb = (1ull << c) - 1;
-        g1j_t* buckets = (g1j_t*)malloc(sizeof(g1j_t) * nb);
-        for (uint64_t b = 0; b < nb; b++) buckets[b] = jinf();
-        for (uint64_t i = 0; i < n; i++) {
-            uint32_t pos = w * c, li = pos / 64, off = pos % 64;
-            unsigned __int128 v = ks[4 * i + li];
-            if (li + 1 < 4) v |= (unsigned __int128)ks[4 * i + li + 1] << 64;
-            uint64_t d = (uint64_t)(v >> off) & ((1ull << c) - 1);
-            if (d) buckets[d - 1] = jadd(buckets[d - 1], jfrom_affine(&pts[i]));
+    const uint32_t nw = (254 + c) / c; /* signed digits need the carry bit of the top window */
+    const uint64_t nb = 1ull << (c - 1);
+    /* signed digits, window-major: dg[w * n + i] in [-2^(c-1), 2^(c-1)] */
+    int32_t* dg = (int32_t*)malloc(sizeof(int32_t) * nw * n);
+#pragma omp parallel for schedule(static) if (par)
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t k[4];
+        fr_canonical(&scalars[i * stride], k);
+        int32_t carry = 0;
+        for (uint32_t w = 0; w < nw; w++) {
+            const uint32_t pos = w * c, li = pos / 64, off = pos % 64;
+            uint64_t v = li < 4 ? k[li] >> off : 0;
+            if (off && li + 1 < 4) v |= k[li + 1] << (64 - off);
+            int32_t d = (int32_t)(v & ((1ull << c) - 1)) + carry;
+            carry = 0;
+            if (d > (int32_t)nb) {
+                d -= (int32_t)(1u << c);
+                carry = 1;
+            }
+            dg[(uint64_t)w * n + i] = d;
         }
-        g1j_t run = jinf(), acc = jinf();
-        for (uint64_t b = nb; b-- > 0;) {
-            run = jadd(run, buckets[b]);
-            acc = jadd(acc, run);
+    }
+    extern int omp_get_max_threads(void);
+    const int T = par ? omp_get_max_threads() : 1;
+    uint32_t chunks = (uint32_t)((2 * T + nw - 1) / nw);
+    if ((uint64_t)chunks > n / 64 + 1) chunks = (uint32_t)(n / 64 + 1);
+    const uint64_t per = (n + chunks - 1) / chunks;
+    g1x_t* bk = (g1x_t*)malloc(sizeof(g1x_t) * nb * nw * chunks);
+#pragma omp parallel for schedule(dynamic, 1) if (par)
+    for (uint64_t task = 0; task < (uint64_t)nw * chunks; task++) {
+        const uint32_t w = (uint32_t)(task / chunks), ch = (uint32_t)(task % chunks);
+        g1x_t* b = bk + task * nb;
+        for (uint64_t j = 0; j < nb; j++) b[j] = xinf();
+        const uint64_t i0 = ch * per, i1 = i0 + per < n ? i0 + per : n;
+        for (uint64_t i = i0; i < i1; i++) {
+            const int32_t d = dg[(uint64_t)w * n + i];
+            if (!d) continue;
+            fq_t x, y;
+            memcpy(x.v, pts[i].x, 32);
+            memcpy(y.v, pts[i].y, 32);
+            if (qzero(x) && qzero(y)) continue; /* identity base */
+            if (d < 0) y = qsub((fq_t){{0, 0, 0, 0}}, y);
+            xmadd(&b[(d < 0 ? -d : d) - 1], x, y);
+        }
+    }
+    g1x_t* wsum = (g1x_t*)malloc(sizeof(g1x_t) * nw);
+#pragma omp parallel for schedule(dynamic, 1) if (par)
+    for (uint32_t w = 0; w < nw; w++) {
+        g1x_t* b0 = bk + (uint64_t)w * chunks * nb;
+        for (uint32_t ch = 1; ch < chunks; ch++)
+            for (uint64_t j = 0; j < nb; j++) xadd(&b0[j], &b0[ch * nb + j]);
+        g1x_t run = xinf(), acc = xinf();
+        for (uint64_t j = nb; j-- > 0;) {
+            xadd(&run, &b0[j]);
+            xadd(&acc, &run);
         }
         wsum[w] = acc;
-        free(buckets);
     }
-    g1j_t acc = wsum[nw - 1];
+    g1x_t acc = wsum[nw - 1];
     for (int w = (int)nw - 2; w >= 0; w--) {
-        for (uint32_t k = 0; k < c; k++) acc = jdbl(acc);
-        acc = jadd(acc, wsum[w]);
+        for (uint32_t k = 0; k < c; k++) acc = xdbl(acc);
+        xadd(&acc, &wsum[w]);
     }
-    jto_affine(acc, out);
+    xto_affine(acc, out);
     free(wsum);
-    free(ks);
+    free(bk);
+    free(dg);
+}
+
+void or_g1_msm(const g1_affine_t* pts, const fr_t* scalars, uint64_t n, g1_affine_t* out) {
+    msm_core(pts, scalars, 1, n, out, 1);
+}
+
+/* KzgPcs::commit's per-column loop (kzg/src/pcs.rs:244-251): out[j] = commit_column(column j of the
+ * n x w row-major matrix) = sum_i mat[i][j] pts[i]; OpenMP over columns, each MSM serial -- the
+ * schedule a CPU prover with many columns uses (the reference runs the columns one after another,
+ * each multi_exp parallel inside). */
+void or_g1_msm_columns(const g1_affine_t* pts, const fr_t* mat, uint64_t n, uint64_t w, g1_affine_t* out) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (uint64_t j = 0; j < w; j++) msm_core(pts, mat + j, w, n, &out[j], 0);
+}
+
+/* KzgPcs::open for one matrix and one point (kzg/src/pcs.rs:289-335): per column,
+ * quotient_and_eval (kzg/src/util.rs:100-111) and the witness commit_column(quotient) over the
+ * first n - 1 bases; OpenMP over columns.  values[j], witnesses[j]. */
+void or_open_columns(const g1_affine_t* pts, const fr_t* coeffs, uint64_t n, uint64_t w, fr_t point,
+                     fr_t* values, g1_affine_t* witnesses) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (uint64_t j = 0; j < w; j++) {
+        fr_t* q = (fr_t*)malloc(sizeof(fr_t) * (n > 1 ? n - 1 : 1));
+        or_quotient_and_eval(coeffs + j, n, w, point, q, &values[j]);
+        if (n > 1)
+            msm_core(pts, q, 1, n - 1, &witnesses[j], 0);
+        else
+            memset(&witnesses[j], 0, sizeof witnesses[j]);
+        free(q);
+    }
 }
 
 /* ---- Poseidon2-AIR over BN254 Fr: WIDTH 3, SBOX_DEGREE 5, SBOX_REGISTERS 1 ----

@@ -44,6 +44,9 @@ void or_g1_add(const g1_affine_t* a, const g1_affine_t* b, g1_affine_t* out);
 int or_g1_on_curve(const g1_affine_t* a);
 void or_g1_srs(uint64_t n, const fr_t* alpha, g1_affine_t* out);
 void or_g1_msm(const g1_affine_t* pts, const fr_t* scalars, uint64_t n, g1_affine_t* out);
+void or_g1_msm_columns(const g1_affine_t* pts, const fr_t* mat, uint64_t n, uint64_t w, g1_affine_t* out);
+void or_open_columns(const g1_affine_t* pts, const fr_t* coeffs, uint64_t n, uint64_t w, fr_t point,
+                     fr_t* values, g1_affine_t* witnesses);
 
 /* KzgPcs::get_evaluations_on_domain's Horner evaluation (kzg/src/pcs.rs:267-287) */
 fr_t or_eval_poly_col(const fr_t* coeffs, uint64_t h, uint64_t w, uint64_t col, fr_t point);

@@ -24,13 +24,22 @@ def _points(abi_rows):
     return [O.g1_from_bytes(np.ascontiguousarray(r, dtype=np.uint64).tobytes()) for r in abi_rows]
 
 
-def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1, challenger=None, constraint_fn=None, publics=()):
+def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1, challenger=None, constraint_fn=None, publics=(),
+          lde_fn=None, timings=None):
     """consts / vl: the Poseidon2-AIR (C restatement of its quotient); or constraint_fn (the
-    signature of pyoracle.quotient_values_fn) for any other AIR, with its public values."""
+    signature of pyoracle.quotient_values_fn) for any other AIR, with its public values.
+
+    lde_fn: None = the reference's Horner get_evaluations_on_domain; or a substitute (coeffs,
+    log_q, shift) -> LDE (the coset-DFT restatement), for CPU baselines at sizes the Horner loop
+    cannot reach.  timings: an optional dict that receives per-stage seconds."""
+    import time
+
+    t0 = time.perf_counter()
     n, w = trace.shape[0], trace.shape[1]
     log_n = n.bit_length() - 1
     coeffs = C.idft_batch(trace)  # coset_idft_batch(evals, shift 1) (kzg/src/pcs.rs:242)
-    trace_commit = np.stack([C.g1_msm(srs[:n], coeffs[:, j]) for j in range(w)])
+    trace_commit = C.g1_msm_columns(srs[:n], coeffs)  # commit_column per column (pcs.rs:244-251)
+    t1 = time.perf_counter()
     if challenger is not None:
         for v in (log_n, log_n, 0):
             challenger.observe(v)
@@ -39,13 +48,15 @@ def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1, challenger=None
             challenger.observe(v)
         alpha_int = challenger.sample()
     alpha = _lim(alpha_int)
-    lde = C.kzg_evaluations_on_domain(coeffs, log_n + log_qd, _lim(O.GENERATOR))
+    lde = (lde_fn or C.kzg_evaluations_on_domain)(coeffs, log_n + log_qd, _lim(O.GENERATOR))
+    t2 = time.perf_counter()
     if constraint_fn is None:
         qv = C.p2_quotient_values(lde, log_n, log_qd, vl, consts, alpha)
     else:
         rows = [[O.from_mont(O.limbs_to_int([int(v) for v in e])) for e in r] for r in lde]
         qv = np.stack([_lim(v) for v in O.quotient_values_fn(rows, log_n, log_qd, constraint_fn, alpha_int,
                                                                list(publics))])
+    t3 = time.perf_counter()
     chunks = 1 << log_qd
     g_q = O.two_adic_generator(log_n + log_qd)
     q_coeffs, quotient_commit = [], []
@@ -59,21 +70,23 @@ def prove(trace, srs, consts, vl, alpha_int, zeta_int, log_qd=1, challenger=None
         challenger.observe_g1(_points(quotient_commit))
         zeta_int = challenger.sample()
     zeta_next = zeta_int * O.two_adic_generator(log_n) % O.P
+    t4 = time.perf_counter()
 
     def open_matrix(cf, points):
+        # per (point, column): quotient_and_eval + commit_column(quotient) (pcs.rs:289-335)
         vals, wits = [], []
         for z in points:
-            v, wt = [], []
-            for j in range(cf.shape[1]):
-                q, val = C.quotient_and_eval(cf[:, j], _lim(z))
-                v.append(val)
-                wt.append(C.g1_msm(srs[:n - 1], q) if n > 1 else np.zeros(8, np.uint64))
-            vals.append(np.stack(v))
-            wits.append(np.stack(wt))
+            v, wt = C.open_columns(srs[:max(n - 1, 1)], cf, _lim(z))
+            vals.append(v)
+            wits.append(wt)
         return vals, wits
 
     trace_open = open_matrix(coeffs, [zeta_int, zeta_next])
     quot_open = [open_matrix(cc, [zeta_int]) for cc in q_coeffs]
+    t5 = time.perf_counter()
+    if timings is not None:
+        timings.update({"commit to trace data": t1 - t0, "trace LDE (get_evaluations_on_domain)": t2 - t1,
+                        "quotient_values": t3 - t2, "commit to quotient poly chunks": t4 - t3, "open": t5 - t4})
     return {
         "trace_commit": trace_commit,
         "quotient_commit": np.stack(quotient_commit),

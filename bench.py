@@ -104,8 +104,8 @@ def cpu_baseline_msm(bases_host: np.ndarray, scalars_host: np.ndarray) -> dict:
         "unit": "ms",
         "cores": coracle.num_threads(),
         "kind": "port",
-        "sample": f"full input: {n} points (C Pippenger restatement, unsigned windows, OpenMP over "
-        f"windows; halo2curves msm_best is not in the reference tree)",
+        "sample": f"full input: {n} points (C Pippenger restatement: signed windows, XYZZ mixed additions, OpenMP over "
+        f"window x point-chunk tasks; halo2curves msm_best is not in the reference tree)",
     }
 
 

@@ -265,7 +265,13 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
                 b = k;
             }
             const uint32_t v = vals[e];
+#ifdef EON_PIECE_PROBE_MASK
+            // memory-sensitivity probe (tuning builds only, wrong results): every gather from a
+            // cache-resident slice of the table
+            G1Affine a = ld_affine(pts29 + (v & EON_PIECE_PROBE_MASK));
+#else
             G1Affine a = ld_affine(pts29 + (v & 0x7fffffffu));
+#endif
             if (is_inf(a)) continue;
             if (v >> 31) a.y = neg(a.y);
             const F29 ax = unpack29(a.x), ay = unpack29(a.y);
@@ -377,9 +383,20 @@ __global__ void __launch_bounds__(64) k_seg_level(const G1Xyzz* X, uint32_t L, u
 // b' = m groups + g (<= PIECE of them: used when no combine level is needed).  Same T / U as
 // k_seg_level over the bucket sums, at T[g nseg + s] / U[g nseg + s]; a wave covers consecutive
 // groups of one segment, so its piece reads are adjacent.
+// OutT = G1Xyzz (radix-2^32, canonical: the per-batch k_group_finish) or G1Raw29 (the raw lazy
+// accumulator, ZZ = 0 for the identity: the call-wide k_group_finish29)
+__device__ __forceinline__ void st_point(G1Xyzz* p, const G1X29& a, bool inf) { st_xyzz(p, x29_to_xyzz(a, inf)); }
+__device__ __forceinline__ void st_point(G1Raw29* p, const G1X29& a, bool inf) {
+    if (inf)
+        st_raw29_inf(p);
+    else
+        st_raw29(p, a);
+}
+
+template <class OutT>
 __global__ void __launch_bounds__(64) k_bucket_reduce29(const G1Raw29* pieces, const uint32_t* piece_off,
-                                                        uint32_t B, uint32_t seg, uint32_t groups, G1Xyzz* T,
-                                                        G1Xyzz* U) {
+                                                        uint32_t B, uint32_t seg, uint32_t groups, OutT* T,
+                                                        OutT* U) {
     const uint32_t nseg = B / seg;
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nseg * groups) return;
@@ -395,8 +412,68 @@ __global__ void __launch_bounds__(64) k_bucket_reduce29(const G1Raw29* pieces, c
         }
         if (k >= 1) acc29(acc, acc_inf, run, run_inf);
     }
-    st_xyzz(T + (uint64_t)g * nseg + s, x29_to_xyzz(run, run_inf));
-    st_xyzz(U + (uint64_t)g * nseg + s, x29_to_xyzz(acc, acc_inf));
+    st_point(T + (uint64_t)g * nseg + s, run, run_inf);
+    st_point(U + (uint64_t)g * nseg + s, acc, acc_inf);
+}
+
+// k_group_finish in radix 2^29 over raw segment sums (k_bucket_reduce29<G1Raw29>): the same
+// out[g] = sum_j U_j + 2^log_seg sum_j j T_j + sum_j T_j, with the 1.4x faster carry-free product
+// and no radix conversion of the inputs; the LDS tree holds raw accumulators (144 B per thread).
+template <uint32_t GF_THREADS>
+__global__ void __launch_bounds__(GF_THREADS) k_group_finish29(const G1Raw29* T, const G1Raw29* U, uint32_t S,
+                                                              uint32_t log_seg, G1Xyzz* out) {
+    __shared__ G1Raw29 sh[GF_THREADS];
+    const uint32_t g = blockIdx.x, t = threadIdx.x;
+    const uint32_t nt = S < GF_THREADS ? S : GF_THREADS;
+    const uint32_t Q = S / nt;
+    G1X29 c, x;
+    bool c_inf = true;
+    if (t < nt) {
+        const G1Raw29* Tg = T + (uint64_t)g * S + (uint64_t)t * Q;
+        const G1Raw29* Ug = U + (uint64_t)g * S + (uint64_t)t * Q;
+        G1X29 run, acc, us;
+        bool run_inf = true, acc_inf = true, us_inf = true;
+        for (uint32_t k = Q - 1; k >= 1; k--) {
+            const bool inf = ld_raw29(Tg + k, x);
+            acc29(run, run_inf, x, inf);
+            acc29(acc, acc_inf, run, run_inf);
+        }
+        {
+            const bool inf = ld_raw29(Tg, x);
+            acc29(run, run_inf, x, inf);
+        }
+        for (uint32_t k = 0; k < Q; k++) {
+            const bool inf = ld_raw29(Ug + k, x);
+            acc29(us, us_inf, x, inf);
+        }
+        const uint32_t lo = t * Q;
+        if (lo && !run_inf) {  // acc += lo * run (double-and-add, MSB first)
+            G1X29 m;
+            bool m_inf = true;
+            for (int bit = 31 - __builtin_clz(lo); bit >= 0; bit--) {
+                if (!m_inf) dbl29(m);
+                if ((lo >> bit) & 1) acc29(m, m_inf, run, false);
+            }
+            acc29(acc, acc_inf, m, m_inf);
+        }
+        if (!acc_inf)
+            for (uint32_t d = 0; d < log_seg; d++) dbl29(acc);
+        acc29(us, us_inf, acc, acc_inf);
+        acc29(us, us_inf, run, run_inf);
+        c = us;
+        c_inf = us_inf;
+    }
+    st_point(sh + t, c, c_inf);
+    __syncthreads();
+    for (uint32_t w = GF_THREADS / 2; w > 0; w >>= 1) {
+        if (t < w) {
+            const bool inf = ld_raw29(sh + t + w, x);
+            acc29(c, c_inf, x, inf);
+            st_point(sh + t, c, c_inf);
+        }
+        __syncthreads();
+    }
+    if (t == 0) st_xyzz(out + g, x29_to_xyzz(c, c_inf));
 }
 
 // After the first level (T_j, U_j of the S segments of each group): one block per group does
@@ -944,8 +1021,8 @@ static Status reduce_segments(eon_ctx* ctx, const MsmLayout& L, const Batch& bt,
 // threads -- under one wave per SIMD, a chain of ~75 dependent additions (1.1 ms per batch,
 // latency-bound); over the whole call (1312 or 2624 groups) it is throughput-bound.
 struct DeferredFinish {
-    G1Xyzz* T = nullptr;
-    G1Xyzz* U = nullptr;
+    G1Raw29* T = nullptr;
+    G1Raw29* U = nullptr;
     G1Xyzz* out_base = nullptr;  // row r's result goes to out_base[r]
     uint32_t nseg = 0, log_seg = 0;
     std::vector<std::pair<uint64_t, uint64_t>> rows;  // deferred [row0, row0 + n)
@@ -957,8 +1034,8 @@ static bool defer_finish_enabled() {
 }
 
 // k_group_finish over the deferred rows (merged into maximal runs) on `st`
-static hipError_t launch_group_finish(const G1Xyzz* T, const G1Xyzz* U, uint32_t nseg, uint32_t lsg,
-                                      G1Xyzz* out, uint32_t groups, hipStream_t st);
+static hipError_t launch_group_finish29(const G1Raw29* T, const G1Raw29* U, uint32_t nseg, uint32_t lsg,
+                                        G1Xyzz* out, uint32_t groups, hipStream_t st);
 
 static Status run_deferred_finish(eon_ctx* ctx, DeferredFinish& df, hipStream_t st) {
     if (df.rows.empty()) return Status::ok();
@@ -972,8 +1049,8 @@ static Status run_deferred_finish(eon_ctx* ctx, DeferredFinish& df, hipStream_t 
     }
     for (auto& r : runs) {
         ctx->prof.begin("k_group_finish", r.second * df.nseg * 256ull, st, r.second * df.nseg * 3ull * 14);
-        EON_HIP(launch_group_finish(df.T + r.first * df.nseg, df.U + r.first * df.nseg, df.nseg, df.log_seg,
-                                    df.out_base + r.first, (uint32_t)r.second, st));
+        EON_HIP(launch_group_finish29(df.T + r.first * df.nseg, df.U + r.first * df.nseg, df.nseg, df.log_seg,
+                                      df.out_base + r.first, (uint32_t)r.second, st));
         ctx->prof.end(st);
     }
     df.rows.clear();
@@ -988,10 +1065,10 @@ static Status prepare_deferred(eon_ctx* ctx, const MsmLayout& L, uint64_t rows, 
     if (B < SEG) return Status::ok();
     df.nseg = B / SEG;
     df.log_seg = 31 - __builtin_clz(SEG);
-    EON_HIP(ctx->fin_T.ensure(rows * df.nseg * sizeof(G1Xyzz)));
-    EON_HIP(ctx->fin_U.ensure(rows * df.nseg * sizeof(G1Xyzz)));
-    df.T = ctx->fin_T.as<G1Xyzz>();
-    df.U = ctx->fin_U.as<G1Xyzz>();
+    EON_HIP(ctx->fin_T.ensure(rows * df.nseg * sizeof(G1Raw29)));
+    EON_HIP(ctx->fin_U.ensure(rows * df.nseg * sizeof(G1Raw29)));
+    df.T = ctx->fin_T.as<G1Raw29>();
+    df.U = ctx->fin_U.as<G1Raw29>();
     df.out_base = out_base;
     return Status::ok();
 }
@@ -1008,8 +1085,8 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
         // first level only; the finish runs once per call (run_deferred_finish)
         const uint64_t row0 = (uint64_t)(bt.out - df->out_base);
         prof->begin("bucket_reduce", (uint64_t)nb * 128 + (uint64_t)nb / SEG * 256, st);
-        hipLaunchKernelGGL(k_bucket_reduce29, dim3(blocks_for((uint64_t)df->nseg * groups, 64)), dim3(64), 0, st,
-                           wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, SEG, groups, df->T + row0 * df->nseg,
+        hipLaunchKernelGGL(k_bucket_reduce29<G1Raw29>, dim3(blocks_for((uint64_t)df->nseg * groups, 64)), dim3(64),
+                           0, st, wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, SEG, groups, df->T + row0 * df->nseg,
                            df->U + row0 * df->nseg);
         prof->end(st);
         EON_HIP(hipGetLastError());
@@ -1069,8 +1146,8 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
         const uint32_t nseg = B / seg;
         G1Xyzz* T = t_buf[0];
         if (fused)
-            hipLaunchKernelGGL(k_bucket_reduce29, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
-                               wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, seg, groups, T, u_buf);
+            hipLaunchKernelGGL(k_bucket_reduce29<G1Xyzz>, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0,
+                               st, wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, seg, groups, T, u_buf);
         else
             hipLaunchKernelGGL(k_seg_level, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st, X, B,
                                seg, groups, T, u_buf);
@@ -1097,8 +1174,8 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
         const uint32_t nseg = Lb / seg;
         G1Xyzz* T = t_buf[m & 1];
         if (fused && m == 0)
-            hipLaunchKernelGGL(k_bucket_reduce29, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
-                               wk.piece_raw.as<G1Raw29>(), sr.piece_off, Lb, seg, groups, T, u_buf);
+            hipLaunchKernelGGL(k_bucket_reduce29<G1Xyzz>, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0,
+                               st, wk.piece_raw.as<G1Raw29>(), sr.piece_off, Lb, seg, groups, T, u_buf);
         else
             hipLaunchKernelGGL(k_seg_level, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
                                X, Lb, seg, groups, T, u_buf);
@@ -1131,19 +1208,18 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
     return write_columns(L, bt, per_group, st);
 }
 
-static hipError_t launch_group_finish(const G1Xyzz* T, const G1Xyzz* U, uint32_t nseg, uint32_t lsg,
-                                      G1Xyzz* out, uint32_t groups, hipStream_t st) {
+static hipError_t launch_group_finish29(const G1Raw29* T, const G1Raw29* U, uint32_t nseg, uint32_t lsg,
+                                        G1Xyzz* out, uint32_t groups, hipStream_t st) {
+    // EON_MSM_GF29_THREADS (128 / 256): threads per column of the call-wide finish
     static const uint32_t gf = [] {
-        const char* e = getenv("EON_MSM_GF_THREADS");
+        const char* e = getenv("EON_MSM_GF29_THREADS");
         const int v = e ? atoi(e) : 256;
-        return (uint32_t)(v == 512 || v == 1024 ? v : 256);
+        return (uint32_t)(v == 128 ? v : 256);
     }();
-    if (gf == 1024)
-        hipLaunchKernelGGL(k_group_finish<1024>, dim3(groups), dim3(1024), 0, st, T, U, nseg, lsg, out);
-    else if (gf == 512)
-        hipLaunchKernelGGL(k_group_finish<512>, dim3(groups), dim3(512), 0, st, T, U, nseg, lsg, out);
+    if (gf == 128)
+        hipLaunchKernelGGL(k_group_finish29<128>, dim3(groups), dim3(128), 0, st, T, U, nseg, lsg, out);
     else
-        hipLaunchKernelGGL(k_group_finish<256>, dim3(groups), dim3(256), 0, st, T, U, nseg, lsg, out);
+        hipLaunchKernelGGL(k_group_finish29<256>, dim3(groups), dim3(256), 0, st, T, U, nseg, lsg, out);
     return hipGetLastError();
 }
 

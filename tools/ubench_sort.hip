@@ -76,16 +76,18 @@ int main() {
     const uint32_t n = 1u << 28;
     uint32_t *k, *v, *k2, *v2;
     CK(hipMalloc(&k, n * 4ull)); CK(hipMalloc(&v, n * 4ull)); CK(hipMalloc(&k2, n * 4ull)); CK(hipMalloc(&v2, n * 4ull));
-    run_seg(k, v, k2, v2, n, 128, 15);
-    run_seg(k, v, k2, v2, n, 128, 16);
-    run_seg(k, v, k2, v2, n, 1024, 15);
-    for (uint32_t bits : {16u, 22u}) {
+    // the MSM digit sort: 2^28 pairs, low 16 key bits (c = 16)
+    for (uint32_t bits : {16u}) {
         run<rocprim::default_config>("default", k, v, k2, v2, n, bits);
-        run<OneCfg<11, 512, 12>>("rb11_512x12", k, v, k2, v2, n, bits);
-        run<OneCfg<11, 256, 16>>("rb11_256x16", k, v, k2, v2, n, bits);
-        run<OneCfg<11, 1024, 8>>("rb11_1024x8", k, v, k2, v2, n, bits);
-
+        run<OneCfg<8, 256, 16>>("rb8_256x16", k, v, k2, v2, n, bits);
         run<OneCfg<8, 512, 12>>("rb8_512x12", k, v, k2, v2, n, bits);
+        run<OneCfg<8, 512, 16>>("rb8_512x16", k, v, k2, v2, n, bits);
+        run<OneCfg<8, 1024, 8>>("rb8_1024x8", k, v, k2, v2, n, bits);
+        run<OneCfg<8, 1024, 12>>("rb8_1024x12", k, v, k2, v2, n, bits);
+        run<OneCfg<8, 256, 24>>("rb8_256x24", k, v, k2, v2, n, bits);
+        run<OneCfg<8, 512, 20>>("rb8_512x20", k, v, k2, v2, n, bits);
+        run<OneCfg<7, 512, 16>>("rb7_512x16", k, v, k2, v2, n, bits);
+        run<OneCfg<6, 512, 16>>("rb6_512x16", k, v, k2, v2, n, bits);
     }
     return 0;
 }

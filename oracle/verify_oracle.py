@@ -159,11 +159,14 @@ def kzg_claims_identity(claims, srs_alpha: int, seed: int = 2024, extra=()) -> b
 
 def verify_kzg_proof(proof, constraint_fn, log_n: int, log_qd: int, srs_alpha: int, alpha: int | None = None,
                      zeta: int | None = None, challenger: O.DuplexChallenger | None = None, trace=None,
-                     seed: int = 2024, publics=()) -> dict:
+                     seed: int = 2024, publics=(), pairing: bool = False) -> dict:
     """Verify a prove() output.  With `challenger` (a fresh pyoracle.DuplexChallenger with the
     config's permutation) alpha / zeta are re-derived from the transcript; otherwise the given
-    ones are used.  `trace`: the (n, w, 4) host trace, for the check against the trace.  Returns
-    the named checks (all must be True)."""
+    ones are used.  `trace`: the (n, w, 4) host trace, for the check against the trace.
+    `pairing`: also run KzgPcs::verify exactly as the reference does -- every opening into ONE
+    verify_batch multi-pairing (kzg/src/pcs.rs:337-400, kzg/src/util.rs:245-292) with the pairing
+    restatement (oracle/pairing.py; ~0.15 s per Miller loop: small proofs only).  Returns the
+    named checks (all must be True)."""
     tc = np.asarray(proof.trace_commit[0], dtype=np.uint64).reshape(-1, 8)
     qc = np.stack([np.asarray(c, dtype=np.uint64).reshape(8) for c in proof.quotient_commit])
     w = tc.shape[0]
@@ -195,6 +198,14 @@ def verify_kzg_proof(proof, constraint_fn, log_n: int, log_qd: int, srs_alpha: i
                                       and np.array_equal(ev[1], np.asarray(tr.values[0][1]).reshape(-1, 4)))
         extra = [(tc[c], fr_int(ev[2][c])) for c in range(w)]
     res["kzg"] = kzg_claims_identity(claims, srs_alpha, seed, extra)
+    if pairing:
+        from . import pairing as E
+
+        def pt(row):
+            return O.g1_from_bytes(np.ascontiguousarray(row, dtype=np.uint64).reshape(8).tobytes())
+
+        openings = [(pt(c), pt(wr), v, z) for c, z, v, wr in claims]
+        res["kzg_pairing"] = E.verify_batch(openings, E.g2_alpha(srs_alpha))
     return res
 
 

@@ -181,8 +181,9 @@ def test_fibonacci_prove_vs_oracle_and_verify(gpu_ctx, ch_consts, n, x):
     np.testing.assert_array_equal(proof.opened[1].values[0][0], want["quotient_open"][0][0][0])
     np.testing.assert_array_equal(proof.opened[1].witnesses[0][0], want["quotient_open"][0][1][0])
     res = V.verify_kzg_proof(proof, V.fib_constraint_fn(pis), n.bit_length() - 1, 0, 12345,
-                             challenger=O.DuplexChallenger(py), trace=trace, publics=pis)
-    assert res == {"transcript": True, "ood": True, "opened_vs_trace": True, "kzg": True}, res
+                             challenger=O.DuplexChallenger(py), trace=trace, publics=pis, pairing=True)
+    assert res == {"transcript": True, "ood": True, "opened_vs_trace": True, "kzg": True,
+                   "kzg_pairing": True}, res
 
 
 def test_fibonacci_incorrect_public_value_does_not_verify(gpu_ctx, ch_consts):

@@ -58,3 +58,27 @@ def test_headline_proof_valid(gpu_ctx, log_n, vl):
     res = V.verify_kzg_proof(proof, V.p2air_constraint_fn(_py_consts(consts), vl), log_n, 1, 12345,
                              challenger=O.DuplexChallenger(_py_consts(ch_consts)), trace=host_trace)
     assert res == {"transcript": True, "ood": True, "opened_vs_trace": True, "kzg": True}, res
+    # the reference's own verifier equation with a real pairing (KzgPcs::verify -> verify_batch,
+    # kzg/src/pcs.rs:337-400, kzg/src/util.rs:245-292) on a sample of the openings: 3 trace columns
+    # at zeta and zeta h, and the quotient chunks at zeta (oracle/pairing.py, ~0.15 s per loop)
+    from oracle import pairing as E
+
+    def pt(row):
+        return O.g1_from_bytes(np.ascontiguousarray(row, dtype=np.uint64).reshape(8).tobytes())
+
+    tc = np.asarray(proof.trace_commit[0]).reshape(-1, 8)
+    zn = proof.zeta * O.two_adic_generator(log_n) % O.P
+    tr, qo = proof.opened
+    openings = []
+    for c in (0, tc.shape[0] // 2, tc.shape[0] - 1):
+        for p, z in enumerate((proof.zeta, zn)):
+            openings.append((pt(tc[c]), pt(np.asarray(tr.witnesses[0][p]).reshape(-1, 8)[c]),
+                             V.fr_int(np.asarray(tr.values[0][p]).reshape(-1, 4)[c]), z))
+    for c, qc in enumerate(proof.quotient_commit):
+        openings.append((pt(qc), pt(qo.witnesses[c][0]), V.fr_int(np.asarray(qo.values[c][0]).reshape(-1, 4)[0]),
+                         proof.zeta))
+    g2a = E.g2_alpha(12345)
+    assert E.verify_batch(openings, g2a)
+    bad = list(openings)
+    bad[0] = (bad[0][0], bad[0][1], (bad[0][2] + 1) % O.P, bad[0][3])
+    assert not E.verify_batch(bad, g2a)

@@ -92,6 +92,7 @@ def test_fibonacci_oracle_prove_verifies(n, x, ok):
     d = prove_oracle.prove(trace, srs, None, None, None, None, log_qd=0, challenger=O.DuplexChallenger(chc),
                            constraint_fn=O.fib_constraints, publics=pis)
     res = V.verify_kzg_proof(V.proof_from_oracle(d), V.fib_constraint_fn(pis), n.bit_length() - 1, 0, 12345,
-                             challenger=O.DuplexChallenger(chc), trace=trace, publics=pis)
+                             challenger=O.DuplexChallenger(chc), trace=trace, publics=pis, pairing=True)
     assert res["transcript"] and res["kzg"] and res["opened_vs_trace"]
+    assert res["kzg_pairing"]  # KzgPcs::verify's verify_batch with the pairing restatement
     assert res["ood"] == ok

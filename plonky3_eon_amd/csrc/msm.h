@@ -28,6 +28,9 @@ bool bases_precomputed(const eon_msm_bases* b);
 void bases_free(eon_msm_bases* b);
 // the window table in 29-Montgomery form (precomputed radix-2^29 bases; else null), its windows
 const G1Affine* bases_table29(const eon_msm_bases* b);
+// 3 x that table (same layout, 29-form), built on the first call (synchronises `st` then); null
+// when the bases have no radix-2^29 table or the allocation fails
+const G1Affine* bases_table3_29(const eon_msm_bases* b, hipStream_t st);
 uint32_t bases_windows(const eon_msm_bases* b);
 // fixed-base bases whose window table the caller writes (affine, radix-2^32 ABI form, entry
 // i * windows + w = 2^(c w) P_i), then seals: points <- the w = 0 entries, table -> 29-form

@@ -59,6 +59,9 @@ struct eon_msm_bases {
     // in the ABI form (the KZG opening bases are derived from it)
     bool r29 = false;
     DevBuf points29;
+    // 3 * table (29-form affine, same layout), built on first use by the KZG opening bases'
+    // radix-4 fixed-base multiplications (bases_table3_29)
+    DevBuf table3;
     const G1Affine* piece_source() const {
         if (precomputed) return table.as<G1Affine>();
         return r29 ? points29.as<G1Affine>() : points.as<G1Affine>();
@@ -1258,6 +1261,49 @@ namespace eon {
 
 const G1Affine* bases_points(const eon_msm_bases* b) { return b->points.as<G1Affine>(); }
 
+// out[e] = 3 tab[e] (tab: 29-form canonical affine; out radix-2^32 XYZZ for the batched affine
+// conversion)
+__global__ void k_triple29(const G1Affine* tab, uint64_t m, G1Xyzz* out) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const G1Affine a = ld_affine(tab + e);
+    if (is_inf(a)) {
+        st_xyzz(out + e, xyzz_inf());
+        return;
+    }
+    const F29 x = unpack29(a.x), y = unpack29(a.y);
+    G1X29 acc = dbl29_affine(x, y);  // 2T (T has odd order r: 2T != -T, != O)
+    bool inf = false;
+    if (!madd29(acc, x, y)) inf = madd29_exceptional(acc, x, y);
+    st_xyzz(out + e, x29_to_xyzz(acc, inf));
+}
+
+const G1Affine* bases_table3_29(const eon_msm_bases* cb, hipStream_t st) {
+    eon_msm_bases* b = const_cast<eon_msm_bases*>(cb);  // a cache filled once
+    if (!b->precomputed || !b->r29 || b->n == 0) return nullptr;
+    if (b->table3.p) return b->table3.as<G1Affine>();
+    const uint64_t m = b->n * b->windows;
+    DevBuf tmp;
+    if (tmp.ensure(m * sizeof(G1Xyzz)) != hipSuccess || b->table3.ensure(m * sizeof(G1Affine)) != hipSuccess) {
+        tmp.release();
+        b->table3.release();
+        return nullptr;
+    }
+    hipLaunchKernelGGL(k_triple29, dim3(blocks_for(m, 128)), dim3(128), 0, st, b->table.as<G1Affine>(), m,
+                       tmp.as<G1Xyzz>());
+    hipError_t e = launch_batch_to_affine(tmp.as<G1Xyzz>(), m, b->table3.as<G1Affine>(), st);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_table_to29, dim3(blocks_for(m, 256)), dim3(256), 0, st, b->table3.as<G1Affine>(), m);
+        e = hipStreamSynchronize(st);  // tmp is released below
+    }
+    tmp.release();
+    if (e != hipSuccess) {
+        b->table3.release();
+        return nullptr;
+    }
+    return b->table3.as<G1Affine>();
+}
+
 const G1Affine* bases_table29(const eon_msm_bases* b) {
     return b->precomputed && b->r29 ? b->table.as<G1Affine>() : nullptr;
 }
@@ -1299,6 +1345,7 @@ Status bases_seal_table(eon_msm_bases* b, hipStream_t st) {
 void bases_free(eon_msm_bases* b) {
     b->points.release();
     b->table.release();
+    b->table3.release();
     b->points29.release();
     delete b;
 }

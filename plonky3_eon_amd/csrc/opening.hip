@@ -137,14 +137,15 @@ __device__ __forceinline__ void madd29_any(G1X29& acc, bool& inf, const F29& x, 
     }
 }
 
-// P_i = z^-i G_i from the SRS window table T_(i,w) = 2^(16 w) G_i (29-form): k = z^-i made odd
-// (k + 1 when even, G_i subtracted at the end) is recoded into 16 odd signed 16-bit digits,
-// each written as 16 digits +-1, so that every bit level adds every window's entry (no lane
-// divergence): 15 doublings + 256 mixed additions, against ~254 + ~254 divergent ones for
-// double-and-add.
+// P_i = z^-i G_i from the SRS window table T_(i,w) = 2^(16 w) G_i (29-form) and its triple
+// 3 T_(i,w) (bases_table3_29): k = z^-i made odd (k + 1 when even, G_i subtracted at the end) is
+// recoded into 16 odd signed 16-bit digits d_w, each written in radix 4 with digits in
+// {-3, -1, 1, 3} (bit pairs of (d_w + 2^16 - 1) / 2, every bit read as +-1), so that every level
+// adds every window's entry +-T or +-3T (no lane divergence): 14 doublings + 128 mixed
+// additions, against 15 + 256 with +-1 digits (tab3 == null keeps that radix-2 form).
 // rows i = lo + t, t < cnt (a rank's slice; rows >= n - 1 are the identity)
-__global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, uint64_t n, uint64_t lo, uint64_t cnt,
-                                                     Fr zinv, G1Xyzz* out_slice) {
+__global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, const G1Affine* tab3, uint64_t n,
+                                                     uint64_t lo, uint64_t cnt, Fr zinv, G1Xyzz* out_slice) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     const uint64_t i = lo + t;
@@ -209,11 +210,28 @@ __global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, uint64
     G1X29 acc;
     bool inf = true;
     F29 x, y;
-    for (int b = (int)TC - 1; b >= 0; b--) {
-        if (!inf) dbl29(acc);
-        for (uint32_t w = 0; w < TW; w++) {
-            ld_affine29(row + w, ((u[w] >> b) & 1) == 0, x, y);
-            madd29_any(acc, inf, x, y);
+    if (tab3) {
+        const G1Affine* row3 = tab3 + i * TW;
+        for (int b = (int)TC / 2 - 1; b >= 0; b--) {
+            if (!inf) {
+                dbl29(acc);
+                dbl29(acc);
+            }
+            for (uint32_t w = 0; w < TW; w++) {
+                // bit pair (hi, lo) of u_w: f = 2 e_hi + e_lo, e = +-1: 3 -> +3, 2 -> +1, 1 -> -1, 0 -> -3
+                const uint32_t two = (u[w] >> (2 * b)) & 3u;
+                const bool three = two == 3u || two == 0u;
+                ld_affine29((three ? row3 : row) + w, two <= 1u, x, y);
+                madd29_any(acc, inf, x, y);
+            }
+        }
+    } else {
+        for (int b = (int)TC - 1; b >= 0; b--) {
+            if (!inf) dbl29(acc);
+            for (uint32_t w = 0; w < TW; w++) {
+                ld_affine29(row + w, ((u[w] >> b) & 1) == 0, x, y);
+                madd29_any(acc, inf, x, y);
+            }
         }
     }
     if (even) {
@@ -223,11 +241,18 @@ __global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, uint64
     st_xyzz(out + i, x29_to_xyzz(acc, inf));
 }
 
-// H_j = z^(j-1) S_j (double-and-add in radix 2^29; S_j affine, radix-2^32 ABI form), then its
-// window table 2^(16 w) H_j, w < TW, by doublings: tmp[j TW + w] (radix-2^32 XYZZ)
+// H_j = z^(j-1) S_j, then its window table 2^(16 w) H_j, w < TW, by doublings: tmp[j TW + w]
+// (radix-2^32 XYZZ).  The scalar multiplication uses REGULAR signed 4-bit windows (no lane
+// divergence: every lane adds at every window): k = z^(j-1) made odd (k + 1 when even, S_j
+// subtracted at the end) is recoded into 64 odd digits in [-15, 15] (d = (k mod 32) - 16,
+// k <- (k - d) / 16), and the odd multiples S, 3S, .., 15S live in the thread's column of `mtab`
+// (MTAB raw accumulators per thread, coalesced across threads): 256 doublings + 64 additions,
+// against ~254 + ~254 (divergent) for double-and-add.
 // rows j = lo + t, t < cnt; s and tmp are the slice's (rows >= n are the identity)
+constexpr uint32_t MTAB = 8;
+
 __global__ void __launch_bounds__(64) k_open_finish29(const G1Affine* s_slice, uint64_t n, uint64_t lo, uint64_t cnt,
-                                                      Fr z, G1Xyzz* tmp_slice) {
+                                                      Fr z, G1Raw29* mtab, G1Xyzz* tmp_slice) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     const uint64_t j = lo + t;
@@ -238,13 +263,78 @@ __global__ void __launch_bounds__(64) k_open_finish29(const G1Affine* s_slice, u
     const G1Affine a = (j && j < n) ? ld_affine(s + j) : G1Affine{Fq::zero(), Fq::zero()};
     if (!is_inf(a)) {
         const F29 x = unpack29(to_fq261(a.x)), y = unpack29(to_fq261(a.y));
-        const Fr k = to_canonical(pow_u64(z, j - 1));
-        for (int w = 7; w >= 0; w--) {
-            const uint32_t word = k.v[w];
-            for (int bit = 31; bit >= 0; bit--) {
-                if (!inf) dbl29(acc);
-                if ((word >> bit) & 1) madd29_any(acc, inf, x, y);
+        Fr k = to_canonical(pow_u64(z, j - 1));
+        const bool even = (k.v[0] & 1) == 0;
+        if (even) k.v[0] += 1;  // no carry: k even
+        // the odd multiples (2m + 1) S, m < MTAB
+        {
+            G1X29 two = dbl29_affine(x, y), m;
+            m.X = x;
+            m.Y = y;
+            m.ZZ = const29<FqP>(R29<FqP>::ONE);
+            m.ZZZ = m.ZZ;
+            bool m_inf = false;
+            st_raw29(mtab + t, m);
+            for (uint32_t q = 1; q < MTAB; q++) {
+                acc29(m, m_inf, two, false);  // S has odd order: the multiples are never O
+                st_raw29(mtab + (uint64_t)q * cnt + t, m);
             }
+        }
+        // recoding: 64 odd digits, nibble i of dg[] = (|d_i| - 1) / 2 | sign << 3
+        uint32_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint32_t kw[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) kw[q] = k.v[q];
+#pragma unroll
+        for (int i = 0; i < 63; i++) {
+            const int32_t d = (int32_t)(kw[0] & 31u) - 16;
+            // k - d (|d| <= 15, odd), then >> 4 (exact)
+            if (d >= 0) {
+                uint64_t c = (uint64_t)kw[0] - (uint32_t)d;
+                kw[0] = (uint32_t)c;
+                uint32_t br = (uint32_t)(c >> 63);
+#pragma unroll
+                for (int q = 1; q < 8; q++) {
+                    c = (uint64_t)kw[q] - br;
+                    kw[q] = (uint32_t)c;
+                    br = (uint32_t)(c >> 63);
+                }
+            } else {
+                uint64_t c = (uint64_t)kw[0] + (uint32_t)(-d);
+                kw[0] = (uint32_t)c;
+                uint32_t cy = (uint32_t)(c >> 32);
+#pragma unroll
+                for (int q = 1; q < 8; q++) {
+                    c = (uint64_t)kw[q] + cy;
+                    kw[q] = (uint32_t)c;
+                    cy = (uint32_t)(c >> 32);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 7; q++) kw[q] = (kw[q] >> 4) | (kw[q + 1] << 28);
+            kw[7] >>= 4;
+            const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+            dg[i >> 3] |= (((mag - 1) >> 1) | (d < 0 ? 8u : 0u)) << (4 * (i & 7));
+        }
+        // the top digit: the rest, odd, in [1, 15] (k < 2^254)
+        dg[7] |= ((kw[0] - 1) >> 1) << 28;
+        G1X29 e;
+        (void)ld_raw29(mtab + (uint64_t)((dg[7] >> 28) & 7u) * cnt + t, e);
+        acc = e;
+        inf = false;
+        for (int i = 62; i >= 0; i--) {
+            dbl29(acc);
+            dbl29(acc);
+            dbl29(acc);
+            dbl29(acc);
+            const uint32_t nib = (dg[i >> 3] >> (4 * (i & 7))) & 15u;
+            (void)ld_raw29(mtab + (uint64_t)(nib & 7u) * cnt + t, e);
+            if (nib & 8u) e.Y = sub29<FqP, 4>(F29{}, e.Y);  // -(x, y): Y < 4p
+            acc29(acc, inf, e, false);
+        }
+        if (even) {
+            const F29 ny = sub29<FqP, 1>(F29{}, y);  // y canonical < p
+            madd29_any(acc, inf, x, ny);
         }
     }
     G1Xyzz* dst = tmp + j * TW;
@@ -285,9 +375,9 @@ void scan_exclusive(G1Xyzz* a, uint64_t len, G1Xyzz* tmp, hipStream_t st) {
 
 // one point's scratch, alive until its stream is synchronised
 struct Scratch {
-    DevBuf h_aff, pts, tmp, aff, table_tmp;
+    DevBuf h_aff, pts, tmp, aff, table_tmp, mtab;
     void release() {
-        for (DevBuf* b : {&h_aff, &pts, &tmp, &aff, &table_tmp}) b->release();
+        for (DevBuf* b : {&h_aff, &pts, &tmp, &aff, &table_tmp, &mtab}) b->release();
     }
 };
 
@@ -301,15 +391,19 @@ Status opening_bases_async29(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
     eon_msm_bases* b = nullptr;
     EON_TRY(bases_alloc_table(ctx, n, TC, &b));
     // ~15 dbl (6M+3S) + 257 madd (8M+2S) and ~254 dbl + ~127 madd + 240 dbl per point
-    ctx->prof.begin("k_open_scale29", n * (TW * 64ull + 128ull), st, n * 2705ull);
-    hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(n, 64)), dim3(64), 0, st, bases_table29(srs), n, 0ull, n,
-                       inverse(z), sc.pts.as<G1Xyzz>());
+    EON_HIP(sc.mtab.ensure(n * MTAB * sizeof(G1Raw29)));
+    const G1Affine* tab3 = getenv("EON_OPEN_SCALE_R2") ? nullptr : bases_table3_29(srs, st);
+    // radix 4: 14 dbl (6M+3S) + 129 madd (8M+2S); radix 2: 15 dbl + 257 madd
+    ctx->prof.begin("k_open_scale29", n * (TW * 64ull + 128ull), st, n * (tab3 ? 1416ull : 2705ull));
+    hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(n, 64)), dim3(64), 0, st, bases_table29(srs), tab3, n, 0ull,
+                       n, inverse(z), sc.pts.as<G1Xyzz>());
     ctx->prof.end(st);
     scan_exclusive(sc.pts.as<G1Xyzz>(), n, sc.tmp.as<G1Xyzz>(), st);
     EON_HIP(launch_batch_to_affine(sc.pts.as<G1Xyzz>(), n, sc.aff.as<G1Affine>(), st));
-    ctx->prof.begin("k_open_finish29", n * (64ull + TW * 128ull), st, n * 5716ull);
+    // 256 dbl + 64 add (12M+2S) + 8 multiples, then 240 dbl for the window table
+    ctx->prof.begin("k_open_finish29", n * (64ull + TW * 128ull), st, n * 5300ull);
     hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(n, 64)), dim3(64), 0, st, sc.aff.as<G1Affine>(), n, 0ull, n, z,
-                       sc.table_tmp.as<G1Xyzz>());
+                       sc.mtab.as<G1Raw29>(), sc.table_tmp.as<G1Xyzz>());
     ctx->prof.end(st);
     hipError_t e = launch_batch_to_affine(sc.table_tmp.as<G1Xyzz>(), n * TW, bases_table_mut(b), st);
     Status s = e == hipSuccess ? bases_seal_table(b, st) : Status::err(EON_E_DEVICE, hipGetErrorString(e));
@@ -395,8 +489,10 @@ Status opening_bases_sharded(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
         EON_HIP(sc[t].tmp.ensure(((m + 1) / (SCAN - 1) + 64) * sizeof(G1Xyzz)));
         EON_HIP(sc[t].aff.ensure(m * sizeof(G1Affine)));
         EON_HIP(sc[t].table_tmp.ensure(slice_entries * sizeof(G1Xyzz)));
-        ctx->prof.begin("k_open_scale29", m * (TW * 64ull + 128ull), st, m * 2705ull);
-        hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(m, 64)), dim3(64), 0, st, bases_table29(srs), n, lo, m,
+        EON_HIP(sc[t].mtab.ensure(m * MTAB * sizeof(G1Raw29)));
+        const G1Affine* tab3 = getenv("EON_OPEN_SCALE_R2") ? nullptr : bases_table3_29(srs, st);
+        ctx->prof.begin("k_open_scale29", m * (TW * 64ull + 128ull), st, m * (tab3 ? 1416ull : 2705ull));
+        hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(m, 64)), dim3(64), 0, st, bases_table29(srs), tab3, n, lo, m,
                            inverse(zs[t]), sc[t].pts.as<G1Xyzz>());
         ctx->prof.end(st);
         // one identity past the slice: the exclusive scan leaves the slice total there
@@ -420,9 +516,9 @@ Status opening_bases_sharded(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
             hipLaunchKernelGGL(k_add_rank_offset, dim3(grid_for(m, 64)), dim3(64), 0, st, sc[t].pts.as<G1Xyzz>(), m,
                                all_totals.as<G1Affine>(), np, t, rank);
         EON_HIP(launch_batch_to_affine(sc[t].pts.as<G1Xyzz>(), m, sc[t].aff.as<G1Affine>(), st));
-        ctx->prof.begin("k_open_finish29", m * (64ull + TW * 128ull), st, m * 5716ull);
+        ctx->prof.begin("k_open_finish29", m * (64ull + TW * 128ull), st, m * 5300ull);
         hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(m, 64)), dim3(64), 0, st, sc[t].aff.as<G1Affine>(), n, lo,
-                           m, zs[t], sc[t].table_tmp.as<G1Xyzz>());
+                           m, zs[t], sc[t].mtab.as<G1Raw29>(), sc[t].table_tmp.as<G1Xyzz>());
         ctx->prof.end(st);
         EON_HIP(launch_batch_to_affine(sc[t].table_tmp.as<G1Xyzz>(), slice_entries,
                                        send.as<G1Affine>() + (uint64_t)t * slice_entries, st));

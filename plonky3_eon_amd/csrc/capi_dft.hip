@@ -212,7 +212,9 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         s.has_load_const = 1;
         s.load_const = n_inv;
     }
-    if (op == Op::CosetIdft) {
+    // coset_idft with shift 1 (KzgPcs::commit of the trace, kzg/src/pcs.rs:242) is the idft: no
+    // output scaling by the all-ones powers of 1^-1
+    if (op == Op::CosetIdft && !(shift == Fr::one())) {
         const Fr* table = nullptr;
         EON_TRY(get_power_table(ctx, n, inverse(shift), Fr::one(), false, &table));
         s.store_scale = table;

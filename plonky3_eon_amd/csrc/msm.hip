@@ -7,7 +7,7 @@
 // Pipeline (all on device, one stream):
 //   1. k_msm_digits     scalars (Montgomery) -> canonical -> signed c-bit digits; one
 //                       (bucket key, point reference | sign) pair per nonzero digit.
-//   2. radix sort       hipCUB DeviceRadixSort (stable onesweep) on the low c key bits of the
+//   2. radix sort       rocPRIM radix_sort_pairs (stable onesweep) on the low c key bits of the
 //                       group-major pairs: buckets b' = magnitude * groups + group, zero digits
 //                       last (see k_msm_digits).
 //   3. k_bucket_start   bucket boundaries in the sorted pairs.
@@ -34,6 +34,7 @@
 // stores 2^(c*w) * P_i in affine for every window w, so every window's digits land in ONE bucket
 // set (groups = 1): no per-window bucket reduction and no serial doubling chain at the end.
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -843,6 +844,23 @@ static std::vector<Batch> make_batches(const Fr* scalars, uint32_t width, uint64
     return batches;
 }
 
+// The digit sort: rocPRIM's onesweep radix sort with 8-bit digits, tuned for these 2^28-pair
+// batches (512 threads x 20 items per block: 3.73 vs 3.94 ms for the default config on 2^28 pairs
+// with 16 key bits, profiles/r02/ubench_sort_configs.txt; EON_MSM_SORT_DEFAULT=1 keeps the
+// library default)
+using SortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 20>, rocprim::kernel_config<512, 20>, 8,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
+static hipError_t sort_pairs(void* temp, size_t& bytes, const uint32_t* k_in, uint32_t* k_out, const uint32_t* v_in,
+                             uint32_t* v_out, uint64_t n, uint32_t bits, hipStream_t st) {
+    static const bool dflt = getenv("EON_MSM_SORT_DEFAULT") != nullptr;
+    if (dflt)
+        return rocprim::radix_sort_pairs(temp, bytes, k_in, k_out, v_in, v_out, (size_t)n, 0u, bits, st);
+    return rocprim::radix_sort_pairs<SortCfg>(temp, bytes, k_in, k_out, v_in, v_out, (size_t)n, 0u, bits, st);
+}
+
 // digits + radix sort + bucket starts + piece offsets of one batch into `out`; `wk` supplies the
 // unsorted pairs, the sort / scan scratch and the count read-back slots
 static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t ld, Batch& bt,
@@ -868,9 +886,8 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     EON_HIP(out.start.ensure((nb + 1) * 4ull));
     EON_HIP(out.piece_off.ensure((nb + 1) * 4ull));
     EON_HIP(wk.count.ensure((nb + 1) * 4ull));
-    EON_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bt.sort_bytes, wk.keys.as<uint32_t>(),
-                                               out.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
-                                               out.vals2.as<uint32_t>(), (int)E, 0, bt.key_bits, st));
+    EON_HIP(sort_pairs(nullptr, bt.sort_bytes, wk.keys.as<uint32_t>(), out.keys2.as<uint32_t>(),
+                       wk.vals.as<uint32_t>(), out.vals2.as<uint32_t>(), E, bt.key_bits, st));
     EON_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bt.scan_bytes, wk.count.as<uint32_t>(),
                                              out.piece_off.as<uint32_t>(), (int)(nb + 1), st));
     EON_HIP(wk.temp.ensure(std::max(bt.sort_bytes, bt.scan_bytes)));
@@ -890,9 +907,8 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     prof->end(st);
     EON_HIP(hipGetLastError());
     prof->begin("radix_sort_pairs", E * 16, st);
-    EON_HIP(hipcub::DeviceRadixSort::SortPairs(wk.temp.p, bt.sort_bytes, wk.keys.as<uint32_t>(),
-                                               out.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
-                                               out.vals2.as<uint32_t>(), (int)E, 0, bt.key_bits, st));
+    EON_HIP(sort_pairs(wk.temp.p, bt.sort_bytes, wk.keys.as<uint32_t>(), out.keys2.as<uint32_t>(),
+                       wk.vals.as<uint32_t>(), out.vals2.as<uint32_t>(), E, bt.key_bits, st));
     prof->end(st);
     hipLaunchKernelGGL(k_bucket_start, dim3(blocks_for(E / 4 + 1, 256)), dim3(256), 0, st,
                        out.keys2.as<uint32_t>(), E, bt.c, bt.groups, nb, out.start.as<uint32_t>());

@@ -42,22 +42,33 @@ __device__ __forceinline__ G1X29 dbl29_affine(const F29& x, const F29& y) {
 // acc += (ax, ay) for a non-identity accumulator and a non-identity affine base.  Returns false in
 // the exceptional case x(acc) == x(A) (then acc is left unchanged and the caller resolves it:
 // doubling or the identity).
+//
+// CHECK = false (madd29_unchecked) skips that test: in the exceptional case PP = 0 mod p, so ZZ
+// becomes 0 mod p and stays 0 under every later unchecked addition (ZZ' = ZZ PP), while a genuine
+// sum never has ZZ = 0 (a product of nonzero PPs).  A caller summing a run of bases tests ZZ once
+// at the end of the run and re-sums it with the checked form when it is 0.
+template <bool CHECK = true>
 __device__ __forceinline__ bool madd29(G1X29& acc, const F29& ax, const F29& ay) {
     const F29 U2 = mul29<FqP>(ax, acc.ZZ);            // < 2p
     const F29 P = sub29<FqP, 8>(U2, acc.X);           // < 10p
     const F29 PP = sqr29<FqP>(P);                      // < 2p
-    if (is_zero_mod29<FqP>(PP)) return false;         // P == 0 mod p
+    if (CHECK && is_zero_mod29<FqP>(PP)) return false;  // P == 0 mod p
     const F29 PPP = mul29<FqP>(P, PP);                // < 2p
     const F29 Q = mul29<FqP>(acc.X, PP);              // < 2p
     const F29 S2 = mul29<FqP>(ay, acc.ZZZ);           // < 2p
     const F29 R = sub29<FqP, 4>(S2, acc.Y);           // < 6p
     acc.ZZ = mul29<FqP>(acc.ZZ, PP);                  // < 2p
     acc.ZZZ = mul29<FqP>(acc.ZZZ, PPP);               // < 2p
-    const F29 X3 = sub29<FqP, 4>(sub29<FqP, 2>(sqr29<FqP>(R), PPP), add29_lazy(Q, Q));  // < 8p
+    // X3 = R^2 - (2Q + PPP) + 6p: one normalising subtraction of the lazy sum (limbs < 3 2^29)
+    const F29 X3 = sub29<FqP, 6>(sqr29<FqP>(R), add29_lazy(add29_lazy(Q, Q), PPP));  // < 8p
     // Y3 = R (Q - X3) - Y PPP = R (Q - X3 + 8p) + Y (2p - PPP): one shared reduction, < 2p
     acc.Y = mul29_sum2<FqP>(R, sub29<FqP, 8>(Q, X3), acc.Y, sub29<FqP, 2>(F29{}, PPP));
     acc.X = X3;
     return true;
+}
+
+__device__ __forceinline__ void madd29_unchecked(G1X29& acc, const F29& ax, const F29& ay) {
+    madd29<false>(acc, ax, ay);
 }
 
 // exceptional case of madd29: x(acc) == x(A); returns the sum (doubling when y(acc) == y(A))
@@ -108,7 +119,7 @@ __device__ __forceinline__ int add29(G1X29& p, const G1X29& q) {
     }
     const F29 PPP = mul29<FqP>(P, PP);       // < 2p
     const F29 Q = mul29<FqP>(U1, PP);        // < 2p
-    const F29 X3 = sub29<FqP, 4>(sub29<FqP, 2>(sqr29<FqP>(R), PPP), add29_lazy(Q, Q));  // < 8p
+    const F29 X3 = sub29<FqP, 6>(sqr29<FqP>(R), add29_lazy(add29_lazy(Q, Q), PPP));  // < 8p
     // Y3 = R (Q - X3) - S1 PPP = R (Q - X3 + 8p) + S1 (2p - PPP), < 2p
     p.Y = mul29_sum2<FqP>(R, sub29<FqP, 8>(Q, X3), S1, sub29<FqP, 2>(F29{}, PPP));
     p.ZZ = mul29<FqP>(mul29<FqP>(p.ZZ, q.ZZ), PP);

@@ -150,7 +150,8 @@ EON_HD F29 add29_norm(const F29& a, const F29& b) {
     return r;
 }
 
-// a - b + K p, normalised (requires b < K p; a, b limbs < 2^30)
+// a - b + K p, normalised (requires b < K p; a limbs < 2^30, b limbs < 3 2^29 -- the signed
+// column sums stay inside int32)
 template <class M, uint32_t K>
 EON_HD F29 sub29(const F29& a, const F29& b) {
     constexpr KP29<M, K> kp{};

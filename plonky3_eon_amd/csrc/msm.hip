@@ -242,6 +242,37 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum(const uint
 // 29-bit limbs (lazy bounds, no carry captures in the products) and the bases read in
 // 29-Montgomery form (k_table_to29).  Each bucket run stores its raw accumulator (144 bytes,
 // ZZ = 0 for the identity); k_raw29_to_xyzz converts the pieces for the combine levels.
+//
+// The additions are unchecked (madd29_unchecked): x(acc) == x(A) -- a duplicate base, or a base
+// meeting its negation -- leaves ZZ = 0 mod p for the rest of the run, so the run's ZZ is tested
+// once at its flush and such a run is summed again with the checked additions (piece_run29).
+// An identity base ((0, 0) in the table) is recognised by y = 0 alone: G1 has prime order, so no
+// curve point has y = 0.
+
+// sum of the bases of sorted pairs [e_begin, e_end) with every exceptional case resolved;
+// returns whether the sum is the identity
+__device__ __forceinline__ bool piece_run29(const uint32_t* vals, const G1Affine* pts29, uint32_t e_begin,
+                                            uint32_t e_end, G1X29& acc) {
+    bool inf = true;
+    for (uint32_t e = e_begin; e < e_end; e++) {
+        const uint32_t v = vals[e];
+        G1Affine a = ld_affine(pts29 + (v & 0x7fffffffu));
+        if (a.y.is_zero()) continue;
+        if (v >> 31) a.y = neg(a.y);
+        const F29 ax = unpack29(a.x), ay = unpack29(a.y);
+        if (inf) {
+            acc.X = ax;
+            acc.Y = ay;
+            acc.ZZ = const29<FqP>(R29<FqP>::ONE);
+            acc.ZZZ = acc.ZZ;
+            inf = false;
+        } else if (!madd29(acc, ax, ay)) {
+            inf = madd29_exceptional(acc, ax, ay);
+        }
+    }
+    return inf;
+}
+
 __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
     const uint32_t* keys, const uint32_t* vals, const uint32_t* start, const uint32_t* piece_off,
     uint32_t n_pairs, uint32_t log_chunk, uint32_t c, uint32_t groups, uint32_t nb,
@@ -251,9 +282,11 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
         const uint32_t e0 = t << log_chunk;
         const uint32_t e1 = min(e0 + (1u << log_chunk), n_pairs);
         uint32_t b = keys[e0];
+        uint32_t run = e0;  // first pair of the current bucket run
         G1X29 acc;
         bool inf = true;
-        auto flush = [&]() {
+        auto flush = [&](uint32_t e_end) __attribute__((always_inline)) {
+            if (!inf && is_zero_mod29<FqP>(acc.ZZ)) inf = piece_run29(vals, pts29, run, e_end, acc);
             const uint32_t bb = bucket_of(b, c, groups, nb);
             G1Raw29* dst = piece_raw + piece_off[bb] + t - (start[bb] >> log_chunk);
             if (inf)
@@ -261,12 +294,16 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
             else
                 st_raw29(dst, acc);
         };
-        for (uint32_t e = e0; e < e1; e++) {
-            const uint32_t k = keys[e];
-            if (k != b) {
-                flush();
+        for (uint32_t e = e0;; e++) {
+            // one flush site (the run's end or the chunk's), so the checked re-sum is emitted once
+            const bool last = e == e1;
+            const uint32_t k = last ? b : keys[e];
+            if (last || k != b) {
+                flush(e);
+                if (last) break;
                 inf = true;
                 b = k;
+                run = e;
             }
             const uint32_t v = vals[e];
 #ifdef EON_PIECE_PROBE_MASK
@@ -276,7 +313,7 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
 #else
             G1Affine a = ld_affine(pts29 + (v & 0x7fffffffu));
 #endif
-            if (is_inf(a)) continue;
+            if (a.y.is_zero()) continue;
             if (v >> 31) a.y = neg(a.y);
             const F29 ax = unpack29(a.x), ay = unpack29(a.y);
             if (inf) {
@@ -285,11 +322,10 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
                 acc.ZZ = const29<FqP>(R29<FqP>::ONE);
                 acc.ZZZ = acc.ZZ;
                 inf = false;
-            } else if (!madd29(acc, ax, ay)) {
-                inf = madd29_exceptional(acc, ax, ay);
+            } else {
+                madd29_unchecked(acc, ax, ay);
             }
         }
-        flush();
     }
 }
 

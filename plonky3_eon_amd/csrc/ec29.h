@@ -61,8 +61,9 @@ __device__ __forceinline__ bool madd29(G1X29& acc, const F29& ax, const F29& ay)
     acc.ZZZ = mul29<FqP>(acc.ZZZ, PPP);               // < 2p
     // X3 = R^2 - (2Q + PPP) + 6p: one normalising subtraction of the lazy sum (limbs < 3 2^29)
     const F29 X3 = sub29<FqP, 6>(sqr29<FqP>(R), add29_lazy(add29_lazy(Q, Q), PPP));  // < 8p
-    // Y3 = R (Q - X3) - Y PPP = R (Q - X3 + 8p) + Y (2p - PPP): one shared reduction, < 2p
-    acc.Y = mul29_sum2<FqP>(R, sub29<FqP, 8>(Q, X3), acc.Y, sub29<FqP, 2>(F29{}, PPP));
+    // Y3 = R (Q - X3) - Y PPP = R (Q - X3 + 9p) + Y (2p - PPP): one shared reduction, < 2p
+    // (6p 11p + 4p 2p < p 2^261); Q - X3 + 9p unnormalised (X3 < 8p)
+    acc.Y = mul29_sum2<FqP>(R, sub29_lazy<FqP, 9>(Q, X3), acc.Y, sub29<FqP, 2>(F29{}, PPP));
     acc.X = X3;
     return true;
 }
@@ -94,8 +95,9 @@ __device__ __forceinline__ void dbl29(G1X29& p) {
     const F29 X2 = sqr29<FqP>(p.X);                    // < 2p
     const F29 M = add29_norm(add29_norm(X2, X2), X2);  // < 6p
     const F29 X3 = sub29<FqP, 4>(sqr29<FqP>(M), add29_lazy(S, S));  // < 6p
-    // Y3 = M (S - X3) - W Y = M (S - X3 + 6p) + W (4p - Y), one shared reduction, < 2p
-    const F29 Y3 = mul29_sum2<FqP>(M, sub29<FqP, 6>(S, X3), W, sub29<FqP, 4>(F29{}, p.Y));
+    // Y3 = M (S - X3) - W Y = M (S - X3 + 7p) + W (4p - Y), one shared reduction, < 2p
+    // (6p 9p + 2p 4p < p 2^261); S - X3 + 7p unnormalised (X3 < 6p)
+    const F29 Y3 = mul29_sum2<FqP>(M, sub29_lazy<FqP, 7>(S, X3), W, sub29<FqP, 4>(F29{}, p.Y));
     p.ZZ = mul29<FqP>(V, p.ZZ);
     p.ZZZ = mul29<FqP>(W, p.ZZZ);
     p.X = X3;
@@ -120,8 +122,8 @@ __device__ __forceinline__ int add29(G1X29& p, const G1X29& q) {
     const F29 PPP = mul29<FqP>(P, PP);       // < 2p
     const F29 Q = mul29<FqP>(U1, PP);        // < 2p
     const F29 X3 = sub29<FqP, 6>(sqr29<FqP>(R), add29_lazy(add29_lazy(Q, Q), PPP));  // < 8p
-    // Y3 = R (Q - X3) - S1 PPP = R (Q - X3 + 8p) + S1 (2p - PPP), < 2p
-    p.Y = mul29_sum2<FqP>(R, sub29<FqP, 8>(Q, X3), S1, sub29<FqP, 2>(F29{}, PPP));
+    // Y3 = R (Q - X3) - S1 PPP = R (Q - X3 + 9p) + S1 (2p - PPP), < 2p (4p 11p + 2p 2p < p 2^261)
+    p.Y = mul29_sum2<FqP>(R, sub29_lazy<FqP, 9>(Q, X3), S1, sub29<FqP, 2>(F29{}, PPP));
     p.ZZ = mul29<FqP>(mul29<FqP>(p.ZZ, q.ZZ), PP);
     p.ZZZ = mul29<FqP>(mul29<FqP>(p.ZZZ, q.ZZZ), PPP);
     p.X = X3;

@@ -166,6 +166,31 @@ EON_HD F29 sub29(const F29& a, const F29& b) {
     return r;
 }
 
+// K p in "borrowed" limbs: every limb below the top one in [2^29 - 1, 2^30), the top one
+// (K p)_8 - 1 (same value), so that a - b + K p can be formed limb by limb without carries
+template <class M, uint32_t K>
+struct KPB29 {
+    uint32_t l[9];
+    constexpr KPB29() : l{} {
+        constexpr KP29<M, K> kp{};
+        l[0] = kp.l[0] + (1u << 29);
+        for (int i = 1; i < 8; i++) l[i] = kp.l[i] + (1u << 29) - 1;
+        l[8] = kp.l[8] - 1;
+    }
+};
+
+// a - b + K p WITHOUT carry propagation: limbs in [0, 2^31), for a product input whose partner is
+// normalised (9 terms < 2^60 per column; mul29 / mul29_sum2 stay below 2^64).  Requires a, b
+// normalised and b's top limb < (K p)_8: b < (K - 1) p suffices.
+template <class M, uint32_t K>
+EON_HD F29 sub29_lazy(const F29& a, const F29& b) {
+    constexpr KPB29<M, K> kp{};
+    F29 r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.l[i] = a.l[i] + kp.l[i] - b.l[i];
+    return r;
+}
+
 template <class M>
 EON_HD F29 mulp29(uint32_t k) {
     F29 r;
@@ -293,8 +318,9 @@ EON_HD F29 sqr29(const F29& a) {
     return r;
 }
 
-// (a b + c d) 2^-261 mod p with one reduction: 27 terms per column, so all four inputs must be
-// normalised (limbs < 2^29); a b + c d < p 2^261 gives an output < 2p.
+// (a b + c d) 2^-261 mod p with one reduction: 27 terms per column, so a, c and d must be
+// normalised (limbs < 2^29) and b's limbs < 2^31 (a sub29_lazy output); a b + c d < p 2^261
+// gives an output < 2p.
 template <class M>
 EON_HD F29 mul29_sum2(const F29& a, const F29& b, const F29& c, const F29& d) {
     uint32_t m[9];

@@ -225,9 +225,13 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
     uint4* lo = lds;
     uint4* hi = lds + ne;
     uint32_t* top = reinterpret_cast<uint32_t*>(lds + 2 * ne);
-    // twiddles in 29-form, 9 words each (packing them to 32 B for a fourth resident tile per CU
-    // measured slower: the per-butterfly unpack costs more than the occupancy gains)
-    uint32_t* twl = top + ne;
+    // twiddles in 29-form, three planes like the tile (limbs 0-3, 4-7, 8: one ds_read_b128 pair
+    // and a ds_read_b32 per twiddle); packing them to 32 B for a fourth resident tile per CU
+    // measured slower (the per-butterfly unpack costs more than the occupancy gains)
+    const uint32_t nt = 1u << k;
+    uint4* tlo = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + ((36u * ne + 15u) & ~15u));
+    uint4* thi = tlo + nt;
+    uint32_t* ttop = reinterpret_cast<uint32_t*>(thi + nt);
 
     const uint32_t s0 = a.s0;
     const uint64_t g = blockIdx.x / a.col_tiles;
@@ -243,8 +247,7 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         const uint64_t s = s0 + l;
         const F29 w = mul29<FrP>(unpack29(gload(a.tw + (1ull << s) + low + ((uint64_t)r << s0))),
                                  const29<FrP>(R29<FrP>::TO261));
-#pragma unroll
-        for (int i = 0; i < 9; i++) twl[9 * q + i] = w.l[i];
+        lds_put29(tlo, thi, ttop, q, w);
     }
 
     for (uint32_t e = threadIdx.x; e < ne; e += T) {
@@ -281,9 +284,7 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
     __syncthreads();
 
     auto tw29 = [&](uint32_t q) {
-        F29 w;
-#pragma unroll
-        for (int i = 0; i < 9; i++) w.l[i] = twl[9 * q + i];
+        F29 w = lds_get29(tlo, thi, ttop, q);
         pin29(w);
         return w;
     };
@@ -319,7 +320,10 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
                 idx[t] = ((m0 + t * h) << LOG_CB) | c;
                 x[t] = lds_get29(lo, hi, top, idx[t]);
             }
-            const bool unit = (r0 | low) == 0;
+            // the twiddle-free butterflies are skipped only where a whole stage is twiddle-free
+            // (h = 1 at low = 0: a uniform branch); elsewhere a unit twiddle is multiplied like
+            // any other (its 29-form is 2^261 mod p), as a per-lane choice would run both paths
+            const bool unit = h == 1 && low == 0;
             if (!DIF) {
                 // stage lq (half h): (0,1), (2,3) with w(h + r0); stage lq + 1 (half 2h): (0,2) with
                 // w(2h + r0), (1,3) with w(3h + r0)
@@ -359,14 +363,11 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
             const uint32_t i1 = ((m0 + half) << LOG_CB) | c;
             const F29 x = reduce29<2>(lds_get29(lo, hi, top, i0));  // < 2p
             const F29 y = lds_get29(lo, hi, top, i1);                 // < 4p
-            const bool unit = (r | low) == 0;
+            // twiddle-free only as a whole stage (uniform branch; see the radix-4 rounds)
+            const bool unit = half == 1 && low == 0;
             F29 u, v;
             F29 w;
-            if (!unit) {
-#pragma unroll
-                for (int i = 0; i < 9; i++) w.l[i] = twl[9 * (half + r) + i];
-                pin29(w);
-            }
+            if (!unit) w = tw29(half + r);
             if (!DIF) {
                 // DitButterfly (dft/src/butterflies.rs:177-185): (x + w*y, x - w*y)
                 const F29 t = unit ? reduce29<2>(y) : mul29<FrP>(y, w);  // < 2p
@@ -440,7 +441,7 @@ static hipError_t launch_pass(bool dif, uint32_t log_cb, const PassArgs& a, uint
     if (threads < 64) threads = 64;
     // EON_NTT_R32=1: the radix-2^32 butterflies (k_ntt_pass)
     static const bool r32 = getenv("EON_NTT_R32") != nullptr;
-    const size_t lds = r32 ? (size_t)ne * 32 + ((size_t)1 << a.k) * 32 : (size_t)ne * 36 + ((size_t)1 << a.k) * 36;
+    const size_t lds = r32 ? (size_t)ne * 32 + ((size_t)1 << a.k) * 32 : (((size_t)ne * 36 + 15) & ~(size_t)15) + ((size_t)1 << a.k) * 36;
     dim3 grid((unsigned)(groups * col_tiles));
 #define EON_LAUNCH(D, C)                                                             \
     do {                                                                             \

@@ -252,16 +252,32 @@ EON_HD void mad29_vs(uint64_t& acc, uint32_t a, uint32_t b) {
 #endif
 }
 
+// acc = a b: the first product of a fresh accumulator, with the inline constant 0 as the addend
+// (no v_mov_b64 to clear the accumulator first)
+EON_HD void mul29_vv(uint64_t& acc, uint32_t a, uint32_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    uint64_t c;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(acc), "=s"(c) : "v"(a), "v"(b));
+#else
+    acc = (uint64_t)a * b;
+#endif
+}
+
 // Montgomery product a b 2^-261 mod p (product scanning; see the header comment for the bounds)
 template <class M>
 EON_HD F29 mul29(const F29& a, const F29& b) {
     uint32_t m[9];
     F29 r;
-    uint64_t acc = 0;
+    uint64_t acc;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
 #pragma unroll
-        for (int i = 0; i <= k; i++) mad29_vv(acc, a.l[i], b.l[k - i]);
+        for (int i = 0; i <= k; i++) {
+            if (k == 0)
+                mul29_vv(acc, a.l[0], b.l[0]);
+            else
+                mad29_vv(acc, a.l[i], b.l[k - i]);
+        }
 #pragma unroll
         for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
         m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
@@ -288,14 +304,22 @@ template <class M>
 EON_HD F29 sqr29(const F29& a) {
     uint32_t m[9];
     F29 r;
-    uint64_t acc = 0;
+    uint64_t acc;
+    mul29_vv(acc, a.l[0], a.l[0]);  // column 0: the square term only
 #pragma unroll
     for (int k = 0; k < 9; k++) {
-        uint64_t cross = 0;
+        if (k > 0) {
+            uint64_t cross;
 #pragma unroll
-        for (int i = 0; 2 * i < k; i++) mad29_vv(cross, a.l[i], a.l[k - i]);
-        acc += cross << 1;
-        if ((k & 1) == 0) mad29_vv(acc, a.l[k / 2], a.l[k / 2]);
+            for (int i = 0; 2 * i < k; i++) {
+                if (i == 0)
+                    mul29_vv(cross, a.l[0], a.l[k]);
+                else
+                    mad29_vv(cross, a.l[i], a.l[k - i]);
+            }
+            acc += cross << 1;
+            if ((k & 1) == 0) mad29_vv(acc, a.l[k / 2], a.l[k / 2]);
+        }
 #pragma unroll
         for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
         m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
@@ -306,7 +330,12 @@ EON_HD F29 sqr29(const F29& a) {
     for (int k = 9; k < 17; k++) {
         uint64_t cross = 0;
 #pragma unroll
-        for (int i = k - 8; 2 * i < k; i++) mad29_vv(cross, a.l[i], a.l[k - i]);
+        for (int i = k - 8; 2 * i < k; i++) {
+            if (i == k - 8)
+                mul29_vv(cross, a.l[i], a.l[k - i]);
+            else
+                mad29_vv(cross, a.l[i], a.l[k - i]);
+        }
         acc += cross << 1;
         if ((k & 1) == 0) mad29_vv(acc, a.l[k / 2], a.l[k / 2]);
 #pragma unroll
@@ -325,12 +354,15 @@ template <class M>
 EON_HD F29 mul29_sum2(const F29& a, const F29& b, const F29& c, const F29& d) {
     uint32_t m[9];
     F29 r;
-    uint64_t acc = 0;
+    uint64_t acc;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
 #pragma unroll
         for (int i = 0; i <= k; i++) {
-            mad29_vv(acc, a.l[i], b.l[k - i]);
+            if (k == 0)
+                mul29_vv(acc, a.l[0], b.l[0]);
+            else
+                mad29_vv(acc, a.l[i], b.l[k - i]);
             mad29_vv(acc, c.l[i], d.l[k - i]);
         }
 #pragma unroll

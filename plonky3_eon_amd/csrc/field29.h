@@ -264,7 +264,15 @@ EON_HD void mul29_vv(uint64_t& acc, uint32_t a, uint32_t b) {
 }
 
 // Montgomery product a b 2^-261 mod p (product scanning; see the header comment for the bounds)
-template <class M>
+//
+// U > 0 leaves the first U reduction multipliers m_0..m_(U-1) unmasked (32 bits instead of 29:
+// one v_and fewer each).  m_k only has to be -column * p^-1 modulo 2^29, so the reduction stays
+// exact; the extra multiples of p sit in the low limbs (< 2^(32 + 29 U)), so the output stays
+// < 2p whenever a b < 0.99 p 2^261 (2^261 = 169.3 p: the widest product of the curve formulas,
+// P^2 < 100 p^2, is 0.59 p 2^261).  The column sums
+// then carry U terms < 2^61: with NORMALISED inputs (limbs < 2^29) the widest column is
+// 9 + 8 U + (9 - U) units of 2^58 < 2^64 for U <= 6.  U = 0 is the general product.
+template <class M, int U = 0>
 EON_HD F29 mul29(const F29& a, const F29& b) {
     uint32_t m[9];
     F29 r;
@@ -280,7 +288,7 @@ EON_HD F29 mul29(const F29& a, const F29& b) {
         }
 #pragma unroll
         for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
-        m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
+        m[k] = k < U ? (uint32_t)acc * R29<M>::INV : ((uint32_t)acc * R29<M>::INV) & M29;
         mad29_vs(acc, m[k], R29<M>::P[0]);
         acc >>= 29;
     }
@@ -300,7 +308,7 @@ EON_HD F29 mul29(const F29& a, const F29& b) {
 
 // a^2 2^-261 mod p for a NORMALISED a (limbs < 2^29; value < 13p): each column's cross products
 // once, summed apart and doubled by a shift (45 instead of 81 limb products; sums < 2^63)
-template <class M>
+template <class M, int U = 0>
 EON_HD F29 sqr29(const F29& a) {
     uint32_t m[9];
     F29 r;
@@ -322,7 +330,7 @@ EON_HD F29 sqr29(const F29& a) {
         }
 #pragma unroll
         for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
-        m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
+        m[k] = k < U ? (uint32_t)acc * R29<M>::INV : ((uint32_t)acc * R29<M>::INV) & M29;
         mad29_vs(acc, m[k], R29<M>::P[0]);
         acc >>= 29;
     }

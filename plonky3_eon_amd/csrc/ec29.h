@@ -12,10 +12,6 @@
 
 namespace eon {
 
-// unmasked reduction multipliers in the products of these formulas (field29.h mul29<M, U>): every
-// mul29 / sqr29 below takes normalised operands, and its product is < 100 p^2
-constexpr int UM = 6;
-
 struct G1X29 {
     F29 X, Y, ZZ, ZZZ;
 };
@@ -53,18 +49,18 @@ __device__ __forceinline__ G1X29 dbl29_affine(const F29& x, const F29& y) {
 // at the end of the run and re-sums it with the checked form when it is 0.
 template <bool CHECK = true>
 __device__ __forceinline__ bool madd29(G1X29& acc, const F29& ax, const F29& ay) {
-    const F29 U2 = mul29<FqP, UM>(ax, acc.ZZ);            // < 2p
+    const F29 U2 = mul29<FqP>(ax, acc.ZZ);            // < 2p
     const F29 P = sub29<FqP, 8>(U2, acc.X);           // < 10p
-    const F29 PP = sqr29<FqP, UM>(P);                      // < 2p
+    const F29 PP = sqr29<FqP>(P);                      // < 2p
     if (CHECK && is_zero_mod29<FqP>(PP)) return false;  // P == 0 mod p
-    const F29 PPP = mul29<FqP, UM>(P, PP);                // < 2p
-    const F29 Q = mul29<FqP, UM>(acc.X, PP);              // < 2p
-    const F29 S2 = mul29<FqP, UM>(ay, acc.ZZZ);           // < 2p
+    const F29 PPP = mul29<FqP>(P, PP);                // < 2p
+    const F29 Q = mul29<FqP>(acc.X, PP);              // < 2p
+    const F29 S2 = mul29<FqP>(ay, acc.ZZZ);           // < 2p
     const F29 R = sub29<FqP, 4>(S2, acc.Y);           // < 6p
-    acc.ZZ = mul29<FqP, UM>(acc.ZZ, PP);                  // < 2p
-    acc.ZZZ = mul29<FqP, UM>(acc.ZZZ, PPP);               // < 2p
+    acc.ZZ = mul29<FqP>(acc.ZZ, PP);                  // < 2p
+    acc.ZZZ = mul29<FqP>(acc.ZZZ, PPP);               // < 2p
     // X3 = R^2 - (2Q + PPP) + 6p: one normalising subtraction of the lazy sum (limbs < 3 2^29)
-    const F29 X3 = sub29<FqP, 6>(sqr29<FqP, UM>(R), add29_lazy(add29_lazy(Q, Q), PPP));  // < 8p
+    const F29 X3 = sub29<FqP, 6>(sqr29<FqP>(R), add29_lazy(add29_lazy(Q, Q), PPP));  // < 8p
     // Y3 = R (Q - X3) - Y PPP = R (Q - X3 + 9p) + Y (2p - PPP): one shared reduction, < 2p
     // (6p 11p + 4p 2p < p 2^261); Q - X3 + 9p unnormalised (X3 < 8p)
     acc.Y = mul29_sum2<FqP>(R, sub29_lazy<FqP, 9>(Q, X3), acc.Y, sub29<FqP, 2>(F29{}, PPP));
@@ -93,17 +89,17 @@ __device__ __forceinline__ bool madd29_exceptional(G1X29& acc, const F29& ax, co
 // 2P for an accumulator under the invariant bounds: dbl-2008-s-1 (a = 0), lazy
 __device__ __forceinline__ void dbl29(G1X29& p) {
     const F29 U = add29_norm(p.Y, p.Y);                // < 8p
-    const F29 V = sqr29<FqP, UM>(U);                       // < 2p
-    const F29 W = mul29<FqP, UM>(U, V);                    // < 2p
-    const F29 S = mul29<FqP, UM>(p.X, V);                  // < 2p
-    const F29 X2 = sqr29<FqP, UM>(p.X);                    // < 2p
+    const F29 V = sqr29<FqP>(U);                       // < 2p
+    const F29 W = mul29<FqP>(U, V);                    // < 2p
+    const F29 S = mul29<FqP>(p.X, V);                  // < 2p
+    const F29 X2 = sqr29<FqP>(p.X);                    // < 2p
     const F29 M = add29_norm(add29_norm(X2, X2), X2);  // < 6p
-    const F29 X3 = sub29<FqP, 4>(sqr29<FqP, UM>(M), add29_lazy(S, S));  // < 6p
+    const F29 X3 = sub29<FqP, 4>(sqr29<FqP>(M), add29_lazy(S, S));  // < 6p
     // Y3 = M (S - X3) - W Y = M (S - X3 + 7p) + W (4p - Y), one shared reduction, < 2p
     // (6p 9p + 2p 4p < p 2^261); S - X3 + 7p unnormalised (X3 < 6p)
     const F29 Y3 = mul29_sum2<FqP>(M, sub29_lazy<FqP, 7>(S, X3), W, sub29<FqP, 4>(F29{}, p.Y));
-    p.ZZ = mul29<FqP, UM>(V, p.ZZ);
-    p.ZZZ = mul29<FqP, UM>(W, p.ZZZ);
+    p.ZZ = mul29<FqP>(V, p.ZZ);
+    p.ZZZ = mul29<FqP>(W, p.ZZZ);
     p.X = X3;
     p.Y = Y3;
 }
@@ -112,24 +108,24 @@ __device__ __forceinline__ void dbl29(G1X29& p) {
 // (12M + 2S).  Returns 0, or in the exceptional case x(p) == x(q) (p unchanged) 1 when p == q
 // (the caller doubles) and 2 when p == -q (the sum is the identity).
 __device__ __forceinline__ int add29(G1X29& p, const G1X29& q) {
-    const F29 U1 = mul29<FqP, UM>(p.X, q.ZZ);    // < 2p
-    const F29 U2 = mul29<FqP, UM>(q.X, p.ZZ);    // < 2p
-    const F29 S1 = mul29<FqP, UM>(p.Y, q.ZZZ);   // < 2p
-    const F29 S2 = mul29<FqP, UM>(q.Y, p.ZZZ);   // < 2p
+    const F29 U1 = mul29<FqP>(p.X, q.ZZ);    // < 2p
+    const F29 U2 = mul29<FqP>(q.X, p.ZZ);    // < 2p
+    const F29 S1 = mul29<FqP>(p.Y, q.ZZZ);   // < 2p
+    const F29 S2 = mul29<FqP>(q.Y, p.ZZZ);   // < 2p
     const F29 P = sub29<FqP, 2>(U2, U1);     // < 4p
     const F29 R = sub29<FqP, 2>(S2, S1);     // < 4p
-    const F29 PP = sqr29<FqP, UM>(P);            // < 2p
+    const F29 PP = sqr29<FqP>(P);            // < 2p
     if (is_zero_mod29<FqP>(PP)) {
-        const F29 Rr = mul29<FqP, UM>(R, const29<FqP>(R29<FqP>::ONE));  // R mod p, < 2p
+        const F29 Rr = mul29<FqP>(R, const29<FqP>(R29<FqP>::ONE));  // R mod p, < 2p
         return is_zero_mod29<FqP>(Rr) ? 1 : 2;
     }
-    const F29 PPP = mul29<FqP, UM>(P, PP);       // < 2p
-    const F29 Q = mul29<FqP, UM>(U1, PP);        // < 2p
-    const F29 X3 = sub29<FqP, 6>(sqr29<FqP, UM>(R), add29_lazy(add29_lazy(Q, Q), PPP));  // < 8p
+    const F29 PPP = mul29<FqP>(P, PP);       // < 2p
+    const F29 Q = mul29<FqP>(U1, PP);        // < 2p
+    const F29 X3 = sub29<FqP, 6>(sqr29<FqP>(R), add29_lazy(add29_lazy(Q, Q), PPP));  // < 8p
     // Y3 = R (Q - X3) - S1 PPP = R (Q - X3 + 9p) + S1 (2p - PPP), < 2p (4p 11p + 2p 2p < p 2^261)
     p.Y = mul29_sum2<FqP>(R, sub29_lazy<FqP, 9>(Q, X3), S1, sub29<FqP, 2>(F29{}, PPP));
-    p.ZZ = mul29<FqP, UM>(mul29<FqP, UM>(p.ZZ, q.ZZ), PP);
-    p.ZZZ = mul29<FqP, UM>(mul29<FqP, UM>(p.ZZZ, q.ZZZ), PPP);
+    p.ZZ = mul29<FqP>(mul29<FqP>(p.ZZ, q.ZZ), PP);
+    p.ZZZ = mul29<FqP>(mul29<FqP>(p.ZZZ, q.ZZZ), PPP);
     p.X = X3;
     return 0;
 }

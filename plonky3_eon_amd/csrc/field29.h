@@ -10,7 +10,7 @@
 // Value conventions (p = the modulus, < 2^254):
 //   * an element is 9 limbs l[i] with value sum l[i] 2^(29 i); "normalised" = every limb < 2^29;
 //   * mul29(a, b) returns a b 2^-261 mod p, normalised, value < 2p, for any inputs whose limbs are
-//     < 2^30 and whose values satisfy a b < p 2^261 (e.g. both < 13p);
+//     < 2^30 and whose values satisfy a b < 0.99 p 2^261 (e.g. both < 12p);
 //   * add29_lazy (no carry propagation: limbs < 2^30) feeds a product only; sub29<K> returns
 //     a - b + K p normalised (b < K p) -- no conditional subtraction anywhere on the hot path;
 //   * canon29 brings a value < 2p to [0, p).
@@ -265,14 +265,14 @@ EON_HD void mul29_vv(uint64_t& acc, uint32_t a, uint32_t b) {
 
 // Montgomery product a b 2^-261 mod p (product scanning; see the header comment for the bounds)
 //
-// U > 0 leaves the first U reduction multipliers m_0..m_(U-1) unmasked (32 bits instead of 29:
-// one v_and fewer each).  m_k only has to be -column * p^-1 modulo 2^29, so the reduction stays
-// exact; the extra multiples of p sit in the low limbs (< 2^(32 + 29 U)), so the output stays
-// < 2p whenever a b < 0.99 p 2^261 (2^261 = 169.3 p: the widest product of the curve formulas,
-// P^2 < 100 p^2, is 0.59 p 2^261).  The column sums
-// then carry U terms < 2^61: with NORMALISED inputs (limbs < 2^29) the widest column is
-// 9 + 8 U + (9 - U) units of 2^58 < 2^64 for U <= 6.  U = 0 is the general product.
-template <class M, int U = 0>
+// The reduction multipliers m_0..m_(U-1) are left unmasked (32 bits instead of 29: one v_and
+// fewer each).  m_k only has to be -column * p^-1 modulo 2^29, so the reduction stays exact; the
+// extra multiples of p sit below 2^(32 + 29 (U - 1)), i.e. below 2^235 p for U = 8, so the output
+// stays < 2p whenever a b < 0.99 p 2^261 (2^261 = 169.3 p; e.g. both values < 12p -- the widest
+// product of the curve formulas, P^2 < 100 p^2, is 0.59 p 2^261).  With the actual limbs of p and
+// r the widest column sum is 0.88 (Fq) / 0.93 (Fr) of 2^64 for operands with limbs < 2^30
+// (0.50 / 0.55 for normalised ones); U = 9 would add 8p to the output bound.
+template <class M, int U = 8>
 EON_HD F29 mul29(const F29& a, const F29& b) {
     uint32_t m[9];
     F29 r;
@@ -308,7 +308,7 @@ EON_HD F29 mul29(const F29& a, const F29& b) {
 
 // a^2 2^-261 mod p for a NORMALISED a (limbs < 2^29; value < 13p): each column's cross products
 // once, summed apart and doubled by a shift (45 instead of 81 limb products; sums < 2^63)
-template <class M, int U = 0>
+template <class M, int U = 8>
 EON_HD F29 sqr29(const F29& a) {
     uint32_t m[9];
     F29 r;
@@ -356,8 +356,9 @@ EON_HD F29 sqr29(const F29& a) {
 }
 
 // (a b + c d) 2^-261 mod p with one reduction: 27 terms per column, so a, c and d must be
-// normalised (limbs < 2^29) and b's limbs < 2^31 (a sub29_lazy output); a b + c d < p 2^261
-// gives an output < 2p.
+// normalised (limbs < 2^29) and b's limbs < 2^31 (a sub29_lazy output); a b + c d < 0.99 p 2^261
+// gives an output < 2p.  Six unmasked reduction multipliers (see mul29): widest column 0.91 of
+// 2^64 with such a b.
 template <class M>
 EON_HD F29 mul29_sum2(const F29& a, const F29& b, const F29& c, const F29& d) {
     uint32_t m[9];
@@ -375,7 +376,7 @@ EON_HD F29 mul29_sum2(const F29& a, const F29& b, const F29& c, const F29& d) {
         }
 #pragma unroll
         for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
-        m[k] = ((uint32_t)acc * R29<M>::INV) & M29;
+        m[k] = k < 6 ? (uint32_t)acc * R29<M>::INV : ((uint32_t)acc * R29<M>::INV) & M29;
         mad29_vs(acc, m[k], R29<M>::P[0]);
         acc >>= 29;
     }

@@ -177,7 +177,14 @@ class MsmWorkload:
         ctx.check(ctx.lib.eon_msm_bases_create_dev(ctx.handle, ctypes.c_void_p(self.bases_dev.data_ptr()),
                                                    self.n, L.EON_MSM_PRECOMPUTE, ctypes.byref(h)))
         self.bases = h
-        self.scalars_host = synthetic_fr(self.n, 1, 3 + rank).reshape(self.n, 4)
+        if args.msm_scalars == "small":
+            # all scalars < 2^64, as kzg/benches/kzg_benches.rs:16-22
+            from plonky3_eon_amd.field import ints_to_limbs
+
+            vals = np.random.Generator(np.random.PCG64(3 + rank)).integers(0, 2**63, self.n, dtype=np.uint64)
+            self.scalars_host = np.ascontiguousarray(ints_to_limbs([int(v) for v in vals]), dtype=np.uint64)
+        else:
+            self.scalars_host = synthetic_fr(self.n, 1, 3 + rank).reshape(self.n, 4)
         self.scalars = torch.from_numpy(self.scalars_host.view(np.int64)).to(dev)
         self.out = np.zeros(8, dtype=np.uint64)
 
@@ -190,7 +197,8 @@ class MsmWorkload:
 
     def describe(self, world):
         return (f"configs[2]: KZG commit MSM, 2^{self.args.log_msm} BN254 G1 SRS points (alpha=12345, "
-                f"fixed-base window table built untimed) x uniform Fr scalars (per GPU)",
+                f"fixed-base window table built untimed) x "
+                f"{'scalars < 2^64 (kzg_benches)' if self.args.msm_scalars == 'small' else 'uniform Fr scalars'} (per GPU)",
                 world, self.n, f"msm-shard x{world}")
 
     def throughput(self, world, ms):
@@ -510,6 +518,8 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--added-bits", type=int, default=1)
     ap.add_argument("--order", choices=["natural", "bitrev"], default="natural")
     ap.add_argument("--log-msm", type=int, default=20)
+    ap.add_argument("--msm-scalars", choices=["uniform", "small"], default="uniform",
+                    help="msm: uniform Fr scalars, or all < 2^64 (kzg/benches/kzg_benches.rs:16-22)")
     ap.add_argument("--cpu-sample-cols", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-full", action="store_true",

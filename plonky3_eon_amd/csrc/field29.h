@@ -306,8 +306,8 @@ EON_HD F29 mul29(const F29& a, const F29& b) {
     return r;
 }
 
-// a^2 2^-261 mod p for a NORMALISED a (limbs < 2^29; value < 13p): each column's cross products
-// once, summed apart and doubled by a shift (45 instead of 81 limb products; sums < 2^63)
+// a^2 2^-261 mod p (limbs < 2^30, a^2 < 0.99 p 2^261, as mul29): each column's cross products
+// once, summed apart and doubled by a shift (45 instead of 81 limb products; cross sums < 2^62)
 template <class M, int U = 8>
 EON_HD F29 sqr29(const F29& a) {
     uint32_t m[9];

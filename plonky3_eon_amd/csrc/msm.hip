@@ -180,27 +180,26 @@ __global__ void k_bucket_start(const uint32_t* keys, uint64_t E, uint32_t c, uin
     }
 }
 
-// stat[0] = max over buckets of the pieces a bucket holds (atomicMax; stat[0] zeroed before)
-__global__ void k_max_pieces(const uint32_t* piece_off, uint32_t nb, uint32_t* stat) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t v = b < nb ? piece_off[b + 1] - piece_off[b] : 0u;
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o));
-    // one atomic per wave, and only while it can raise the maximum (~all waves see 2 or 3)
-    if ((threadIdx.x & 63) == 0 && v > 1 && v > __atomic_load_n(stat, __ATOMIC_RELAXED)) atomicMax(stat, v);
-}
-
 __global__ void k_piece_owner(const uint32_t* piece_off, uint32_t nb, uint32_t* owner) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     for (uint32_t p = piece_off[b]; p < piece_off[b + 1]; p++) owner[p] = b;
 }
 
-// count[b] = the chunk-aligned runs bucket b's pairs [start[b], start[b+1]) touch (0 if empty)
-__global__ void k_chunk_count(const uint32_t* start, uint32_t nb, uint32_t log_chunk, uint32_t* count) {
+// count[b] = the chunk-aligned runs bucket b's pairs [start[b], start[b+1]) touch (0 if empty),
+// i.e. the pieces bucket b will hold; stat[0] = their maximum over buckets (atomicMax, one per
+// wave and only while it can raise the maximum; stat[0] zeroed before)
+__global__ void k_chunk_count(const uint32_t* start, uint32_t nb, uint32_t log_chunk, uint32_t* count,
+                              uint32_t* stat) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b > nb) return;
-    const uint32_t s = b == nb ? 0 : start[b], e = b == nb ? 0 : start[b + 1];
-    count[b] = s == e ? 0 : ((e - 1) >> log_chunk) - (s >> log_chunk) + 1;
+    uint32_t v = 0;
+    if (b <= nb) {
+        const uint32_t s = b == nb ? 0 : start[b], e = b == nb ? 0 : start[b + 1];
+        v = s == e ? 0 : ((e - 1) >> log_chunk) - (s >> log_chunk) + 1;
+        count[b] = v;
+    }
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o));
+    if ((threadIdx.x & 63) == 0 && v > 1 && v > __atomic_load_n(stat, __ATOMIC_RELAXED)) atomicMax(stat, v);
 }
 
 // Thread t sums the sorted pairs [t 2^log_chunk, (t+1) 2^log_chunk) (nonzero digits only): one
@@ -948,15 +947,13 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     prof->end(st);
     hipLaunchKernelGGL(k_bucket_start, dim3(blocks_for(E / 4 + 1, 256)), dim3(256), 0, st,
                        out.keys2.as<uint32_t>(), E, bt.c, bt.groups, nb, out.start.as<uint32_t>());
-    hipLaunchKernelGGL(k_chunk_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st,
-                       out.start.as<uint32_t>(), nb, bt.log_chunk, wk.count.as<uint32_t>());
-    EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, bt.scan_bytes, wk.count.as<uint32_t>(),
-                                             out.piece_off.as<uint32_t>(), (int)(nb + 1), st));
     // the most pieces one bucket holds fixes the combine levels (no read-backs in the reduction)
     EON_HIP(wk.stat.ensure(16));
     EON_HIP(hipMemsetAsync(wk.stat.p, 0, 16, st));
-    hipLaunchKernelGGL(k_max_pieces, dim3(blocks_for(nb, 256)), dim3(256), 0, st, out.piece_off.as<uint32_t>(),
-                       nb, wk.stat.as<uint32_t>());
+    hipLaunchKernelGGL(k_chunk_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st,
+                       out.start.as<uint32_t>(), nb, bt.log_chunk, wk.count.as<uint32_t>(), wk.stat.as<uint32_t>());
+    EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, bt.scan_bytes, wk.count.as<uint32_t>(),
+                                             out.piece_off.as<uint32_t>(), (int)(nb + 1), st));
     // launches are sized by the real counts (12-byte read-back: pieces, nonzero digits, max pieces)
     EON_HIP(hipMemcpyAsync(wk.host_counts, out.piece_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
     EON_HIP(hipMemcpyAsync(wk.host_counts + 1, out.start.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));

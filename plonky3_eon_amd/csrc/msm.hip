@@ -101,8 +101,8 @@ constexpr uint32_t DIGIT_COLS = 4;  // widest scalar tile of one 256-thread bloc
 
 __global__ void __launch_bounds__(256) k_msm_digits(const Fr* scalars, uint64_t n, uint64_t ld,
                                                     uint32_t cols, uint32_t c, uint32_t windows,
-                                                    uint32_t precomputed, uint32_t tile_cols,
-                                                    uint32_t* keys, uint32_t* vals) {
+                                                    uint32_t ref_windows, uint32_t precomputed,
+                                                    uint32_t tile_cols, uint32_t* keys, uint32_t* vals) {
     // a block reads 256 / tile_cols row segments of tile_cols adjacent columns (up to 128
     // contiguous bytes), so the group-major writes stay in runs of consecutive rows
     const uint32_t col = blockIdx.y * tile_cols + threadIdx.x % tile_cols;
@@ -132,10 +132,32 @@ __global__ void __launch_bounds__(256) k_msm_digits(const Fr* scalars, uint64_t 
         } else {
             const uint32_t g = precomputed ? col : col * windows + w;
             keys[e] = (g << c) | (mag - 1);
-            const uint32_t ref = precomputed ? (uint32_t)(i * windows + w) : (uint32_t)i;
+            const uint32_t ref = precomputed ? (uint32_t)(i * ref_windows + w) : (uint32_t)i;
             vals[e] = ref | (neg << 31);
         }
     }
+}
+
+// OR of every canonical scalar into or_out[8] (zeroed before): its top set bit bounds the
+// digits a single MSM needs (active windows, msm_run_columns)
+__global__ void __launch_bounds__(256) k_scalar_or(const Fr* scalars, uint64_t n, uint32_t* or_out) {
+    __shared__ uint32_t acc[8];
+    if (threadIdx.x < 8) acc[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const Fr s = to_canonical(ld_pinned(scalars + i));
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] |= s.v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        uint32_t x = v[j];
+        for (int o = 32; o > 0; o >>= 1) x |= (uint32_t)__shfl_xor(x, o);
+        if ((threadIdx.x & 63) == 0 && x) atomicOr(&acc[j], x);
+    }
+    __syncthreads();
+    if (threadIdx.x < 8 && acc[threadIdx.x]) atomicOr(or_out + threadIdx.x, acc[threadIdx.x]);
 }
 
 // bucket index b' of a sorted key (nb for the zero-digit sentinel)
@@ -832,6 +854,7 @@ struct Batch {
     size_t sort_bytes = 0, scan_bytes = 0;
     uint32_t n_pieces = 0, n_pairs = 0;
     uint32_t levels = 0;  // PIECE-way combine levels until every bucket holds <= 1 partial
+    uint32_t w_act = 0;   // windows that can hold a nonzero digit (0: all of the layout's)
 };
 
 struct SortedRef {
@@ -901,7 +924,7 @@ static hipError_t sort_pairs(void* temp, size_t& bytes, const uint32_t* k_in, ui
 static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t ld, Batch& bt,
                          MsmWork& wk, SortedBufs& out, hipStream_t st) {
     bt.c = L.c;
-    bt.W = L.W;
+    bt.W = bt.w_act ? std::min(bt.w_act, L.W) : L.W;
     bt.B = 1u << (bt.c - 1);
     bt.groups = L.precomputed ? bt.cols : bt.cols * bt.W;
     bt.nb = bt.groups * bt.B;
@@ -937,7 +960,7 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     const uint32_t tile_rows = 256 / tile_cols;
     hipLaunchKernelGGL(k_msm_digits, dim3((unsigned)((n + tile_rows - 1) / tile_rows),
                                           (bt.cols + tile_cols - 1) / tile_cols),
-                       dim3(256), 0, st, bt.scalars, n, ld, bt.cols, bt.c, bt.W, (uint32_t)L.precomputed,
+                       dim3(256), 0, st, bt.scalars, n, ld, bt.cols, bt.c, bt.W, L.W, (uint32_t)L.precomputed,
                        tile_cols, wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>());
     prof->end(st);
     EON_HIP(hipGetLastError());
@@ -1607,6 +1630,26 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
     G1Xyzz* res_xyzz = reinterpret_cast<G1Xyzz*>(res + width);
     std::vector<Batch> batches = make_batches(scalars, width, L.cpb);
     for (Batch& bt : batches) bt.out = res_xyzz + bt.col0;
+    // a single MSM digitises only the windows its largest scalar reaches (the signed recoding
+    // carries at most one bit past it): scalars < 2^64, as in kzg/benches, need 5 of 16 windows
+    // of 16 bits.  One OR-reduction over the scalars and a 32-byte read-back.
+    static const bool all_windows = getenv("EON_MSM_ALL_WINDOWS") != nullptr;
+    if (width == 1 && !keep && !all_windows) {
+        EON_HIP(ctx->msm.stat.ensure(64));
+        EON_HIP(hipMemsetAsync(ctx->msm.stat.p, 0, 32, ctx->stream));
+        const unsigned blocks = (unsigned)std::min<uint64_t>(blocks_for(n, 256), 4096);
+        hipLaunchKernelGGL(k_scalar_or, dim3(blocks), dim3(256), 0, ctx->stream, scalars, n,
+                           ctx->msm.stat.as<uint32_t>());
+        EON_HIP(hipGetLastError());
+        if (!ctx->msm.host_counts) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->msm.host_counts), 64));
+        uint32_t* h = ctx->msm.host_counts + 8;
+        EON_HIP(hipMemcpyAsync(h, ctx->msm.stat.p, 32, hipMemcpyDeviceToHost, ctx->stream));
+        EON_HIP(hipStreamSynchronize(ctx->stream));
+        uint32_t bits = 0;
+        for (int j = 7; j >= 0 && !bits; j--)
+            if (h[j]) bits = 32 * j + 32 - __builtin_clz(h[j]);
+        batches[0].w_act = std::max<uint32_t>(1, std::min<uint32_t>(L.W, (bits + 1 + L.c - 1) / L.c));
+    }
     // sorted pairs land in the workspace of batch k % 3, or, when kept, in buffers of their own
     if (keep) {
         keep->sorted.resize(batches.size());

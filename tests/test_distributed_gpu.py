@@ -14,10 +14,12 @@ def test_sharded_prove_matches_single(world, log_n, vl):
     assert all(r["ok"] for r in res), [r["why"] for r in res]
 
 
-@pytest.mark.parametrize("world,log_n,vl", [(2, 5, 4), (4, 3, 8), (2, 17, 2)])
+@pytest.mark.parametrize("world,log_n,vl", [(2, 5, 4), (4, 3, 8), (2, 17, 2), (8, 17, 8)])
 def test_native_sharded_prove_matches_single(world, log_n, vl):
     """The C++ driver's lane-sharded prove (torch.distributed eon_collective) == its unsharded
-    prove == the Python prover."""
+    prove == the Python prover.  (8, 17, 8) is the driver's 8-GPU scaling configuration of the
+    headline proof (one lane per rank of the VECTOR_LEN-8 2^17 trace), here with gloo ranks
+    sharing one GPU."""
     res = run_world("native", world, timeout=900, extra_env={"EON_T_LOG_N": str(log_n), "EON_T_VL": str(vl)})
     assert all(r["ok"] for r in res), [r["why"] for r in res]
 

@@ -550,14 +550,21 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # EON_BENCH_BACKEND=gloo and EON_BENCH_ONE_DEVICE=1 rehearse the N > 1 code path with every
+    # rank on cuda:0 (a one-GPU box); the timings of such a run mean nothing
+    backend = os.environ.get("EON_BENCH_BACKEND", "nccl")
+    local_dev = 0 if os.environ.get("EON_BENCH_ONE_DEVICE") == "1" else local_rank
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from plonky3_eon_amd import Context
 
-    ctx = Context(local_rank)
+    ctx = Context(local_dev)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     wl = {"lde": LdeWorkload, "msm": MsmWorkload, "prove": ProveWorkload, "ntt4": FourStepWorkload,
           "msm-shard": MsmShardWorkload}[args.workload](args, ctx, dev, rank)
@@ -600,7 +607,7 @@ def main() -> int:
         dist.barrier()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

@@ -1,0 +1,35 @@
+"""GPU: bench.py keeps its output contract (the driver parses it): exactly one JSON line with the
+required keys, `roofline` (bound / achieved / peak / unit / frac / traffic, frac = achieved / peak)
+and `cpu_baseline` (value / unit / cores / kind / sample).  Runs the quick configs[2] workload."""
+
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_bench_json_contract():
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--workload", "msm", "--steps", "3", "--warmup", "1"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, lines
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1
+    assert d["value"] > 0 and d["higher_is_better"] is False and d["scaling"] in ("weak", "strong")
+    assert "workload" in d["config"]
+    r = d["roofline"]
+    assert r["bound"] in ("hbm", "mfma") and r["unit"] in ("GB/s", "TFLOP/s")
+    assert r["peak"] == 8000.0 and r["achieved"] > 0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert "traffic" in r
+    c = d["cpu_baseline"]
+    assert c["value"] > 0 and c["cores"] >= 1 and c["kind"] in ("reference", "port") and c["sample"]

@@ -66,3 +66,26 @@ class MixedAir:
         builder.when(loc[2] - 7).assert_zeros([loc[3] * nxt[4], -(nxt[1] - 11)])
         builder.assert_zero(s)  # a constraint that is a shared value
         builder.assert_zero(loc[4])  # a constraint that is a leaf
+
+
+class MulAir:
+    """MulAir of uni-stark/tests/mul_air.rs:37-118 (degree 3, boundary and transition constraints
+    on): REPETITIONS = 20 triples (a, b, c) per row; assert_zero(a^2 b - c); when_first_row
+    assert_eq(a a + 1, b); when_transition assert_eq(a + 20, next a)."""
+
+    REPETITIONS = 20
+
+    def width(self):
+        return 3 * self.REPETITIONS
+
+    def num_public_values(self):
+        return 0
+
+    def eval(self, builder):
+        m = builder.main()
+        loc, nxt = m[0], m[1]
+        for i in range(self.REPETITIONS):
+            a, b, c = loc[3 * i], loc[3 * i + 1], loc[3 * i + 2]
+            builder.assert_zero(a.exp_const_u64(2) * b - c)
+            builder.when_first_row().assert_eq(a * a + 1, b)
+            builder.when_transition().assert_eq(a + self.REPETITIONS, nxt[3 * i])

@@ -5,7 +5,9 @@
 * the Poseidon2-AIR compiled from its symbolic eval equals the fused kernel and the C oracle;
 * the reference's end-to-end Fibonacci tests (fib_air.rs:112-135: n = 1 and n = 8, publics
   (0, 1, F_n), KzgPcs max_degree 1024 with alpha = 12345, Fiat-Shamir) prove on the GPU bit-exact
-  against the CPU restatement and verify; the incorrect-public-value case does not verify.
+  against the CPU restatement and verify; the incorrect-public-value case does not verify;
+* MulAir (uni-stark/tests/mul_air.rs: degree 3, 60 columns, boundary + transition constraints,
+  two quotient chunks) likewise, and its invalid trace (c doubled) does not verify.
 
 Parity note: the challenger's Poseidon2 constants are the in-repo seeded ones (the reference draws
 them from SmallRng, unreproducible offline)."""
@@ -13,7 +15,7 @@ them from SmallRng, unreproducible offline)."""
 import numpy as np
 import pytest
 
-from airs import FibonacciAir, MixedAir
+from airs import FibonacciAir, MixedAir, MulAir
 from oracle import coracle as C
 from oracle import prove_oracle
 from oracle import pyoracle as O
@@ -230,3 +232,63 @@ def test_poseidon2_generic_prove_equals_fused_prove(gpu_ctx):
     for c in range(2):
         np.testing.assert_array_equal(fused.quotient_commit[c], generic.quotient_commit[c])
         np.testing.assert_array_equal(fused.opened[1].witnesses[c][0], generic.opened[1].witnesses[c][0])
+
+
+def mul_constraints(loc, nxt, sels, pub):
+    """MulAir (uni-stark/tests/mul_air.rs:96-118) written out directly, in eval order."""
+    first, _, trans = sels
+    out = []
+    for i in range(MulAir.REPETITIONS):
+        a, b, c = loc[3 * i], loc[3 * i + 1], loc[3 * i + 2]
+        out += [(a * a * b - c) % P, first * (a * a + 1 - b) % P, trans * (a + MulAir.REPETITIONS - nxt[3 * i]) % P]
+    return out
+
+
+def mul_trace(rows: int, valid: bool = True):
+    """random_valid_trace (mul_air.rs:55-81) with degree 3 and both constraint kinds: a = the
+    triple's index, b = a^2 + 1 on the first row and random elsewhere, c = a^2 b (doubled when
+    invalid); randomness from the in-repo PRNG."""
+    rng = O.SplitMix64(7)
+    reps = MulAir.REPETITIONS
+    t = []
+    for i in range(rows * reps):
+        a = i % P
+        b = (a * a + 1) % P if i // reps == 0 else rng.fr_mont() % P
+        c = a * a * b % P
+        t.append([a, b, c * (2 if not valid else 1) % P])
+    return [sum(t[r * reps:(r + 1) * reps], []) for r in range(rows)]
+
+
+@pytest.mark.parametrize("log_n,valid", [(3, True), (5, True), (3, False)])
+def test_mul_air_prove_vs_oracle_and_verify(gpu_ctx, ch_consts, log_n, valid):
+    import torch
+
+    from plonky3_eon_amd.air import AirProgram
+    from plonky3_eon_amd.native import Challenger, NativeKzgPcs, Poseidon2Constants, prove_native
+
+    py, limbs = ch_consts
+    n = 1 << log_n
+    rows = mul_trace(n, valid)
+    trace = np.stack([np.stack([lim(v) for v in r]) for r in rows])
+    prog = AirProgram(MulAir(), gpu_ctx)
+    assert prog.max_constraint_degree == 3 and prog.log_quotient_degree() == 1
+    assert prog.num_constraints == 3 * MulAir.REPETITIONS
+    pcs = NativeKzgPcs(1024, 12345, gpu_ctx)
+    proof = prove_native(prog, pcs, torch.from_numpy(trace.view(np.int64)).to("cuda:0"), None, None,
+                         challenger=Challenger(Poseidon2Constants(*limbs)))
+    pcs.close()
+    res = V.verify_kzg_proof(proof, lambda loc, nxt, sels: mul_constraints(loc, nxt, sels[:3], ()), log_n, 1, 12345,
+                             challenger=O.DuplexChallenger(py), trace=trace)
+    if not valid:
+        assert res["transcript"] and res["kzg"] and not res["ood"], res
+        return
+    assert res == {"transcript": True, "ood": True, "opened_vs_trace": True, "kzg": True}, res
+    srs = C.g1_srs(1025, C.fr_from_u64(12345))
+    want = prove_oracle.prove(trace, srs, None, None, None, None, log_qd=1, challenger=O.DuplexChallenger(py),
+                              constraint_fn=mul_constraints, publics=[])
+    assert (proof.alpha, proof.zeta) == (want["alpha"], want["zeta"])
+    np.testing.assert_array_equal(proof.trace_commit[0], want["trace_commit"])
+    np.testing.assert_array_equal(np.stack([c[0] for c in proof.quotient_commit]), want["quotient_commit"])
+    for p in range(2):
+        np.testing.assert_array_equal(proof.opened[0].values[0][p], want["trace_open"][0][p])
+        np.testing.assert_array_equal(proof.opened[0].witnesses[0][p], want["trace_open"][1][p])

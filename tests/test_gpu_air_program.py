@@ -9,8 +9,10 @@
 * MulAir (uni-stark/tests/mul_air.rs: degree 3, 60 columns, boundary + transition constraints,
   two quotient chunks) likewise, and its invalid trace (c doubled) does not verify.
 
-Parity note: the challenger's Poseidon2 constants are the in-repo seeded ones (the reference draws
-them from SmallRng, unreproducible offline)."""
+Parity note: the Fibonacci tests' challenger permutation is the reference's own
+`Perm::new_from_rng(4, 22, SmallRng::seed_from_u64(1))` (fib_air.rs:113-115) through the restated
+rand 0.9 SmallRng (oracle/smallrng.py, Xoshiro256++ pinned by its published vector); the
+compressed-G1 transcript bytes stay unpinned."""
 
 import numpy as np
 import pytest
@@ -20,6 +22,7 @@ from oracle import coracle as C
 from oracle import prove_oracle
 from oracle import pyoracle as O
 from oracle import verify_oracle as V
+from oracle.smallrng import SmallRng, poseidon2_new_from_rng
 
 pytestmark = pytest.mark.gpu
 P = O.P
@@ -148,7 +151,9 @@ def test_program_rejects_bad_input(gpu_ctx):
 
 @pytest.fixture(scope="module")
 def ch_consts():
-    py = O.p2_constants(77, 4, 22)  # Poseidon2Bn254<3>::new_from_rng(4, 22, ..) shape (fib_air.rs:114)
+    # the reference's own challenger permutation: Perm::new_from_rng(4, 22, SmallRng(1))
+    # (fib_air.rs:113-115), through the restated rand 0.9 SmallRng (oracle/smallrng.py)
+    py = poseidon2_new_from_rng(SmallRng.seed_from_u64(1), 4, 22)
     return py, ([[lim(v) for v in r] for r in py[0]], [lim(v) for v in py[1]], [[lim(v) for v in r] for r in py[2]])
 
 

@@ -11,6 +11,7 @@ from oracle import coracle as C
 from oracle import prove_oracle
 from oracle import pyoracle as O
 from oracle import verify_oracle as V
+from oracle.smallrng import SmallRng, poseidon2_new_from_rng
 
 HF, PR = 4, 56
 
@@ -85,7 +86,7 @@ def test_rejects_tampered(setup, what):
 def test_fibonacci_oracle_prove_verifies(n, x, ok):
     """fib_air.rs:112-155 on the CPU restatement: prove + verify for n = 1 and 8 with publics
     (0, 1, F_n); the incorrect public value yields a proof whose OOD identity fails."""
-    chc = O.p2_constants(77, 4, 22)
+    chc = poseidon2_new_from_rng(SmallRng.seed_from_u64(1), 4, 22)  # fib_air.rs:113-115
     pis = [0, 1, x]
     trace = np.stack([np.stack([lim(v) for v in r]) for r in O.fib_trace(0, 1, n)])
     srs = C.g1_srs(1025, C.fr_from_u64(12345))

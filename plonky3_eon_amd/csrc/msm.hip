@@ -315,10 +315,30 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
             else
                 st_raw29(dst, acc);
         };
+#ifndef EON_PIECE_SCALAR_PAIRS
+        // 16-byte loads of four keys and four references every fourth pair (chunks are aligned to
+        // 2^LOG_CHUNK_MIN pairs; a chunk cut short by n_pairs reads one pair at a time): a quarter
+        // of the pair-stream requests (prove -2.5 % A/B; EON_PIECE_SCALAR_PAIRS restores the
+        // one-pair loads)
+        const bool vec = ((e0 | e1) & 3) == 0;
+        uint4 kq = make_uint4(0, 0, 0, 0), vq = kq;
+#endif
         for (uint32_t e = e0;; e++) {
             // one flush site (the run's end or the chunk's), so the checked re-sum is emitted once
             const bool last = e == e1;
+#ifndef EON_PIECE_SCALAR_PAIRS
+            const uint32_t sub = e & 3;
+            if (vec && !last && sub == 0) {
+                kq = *reinterpret_cast<const uint4*>(keys + e);
+                vq = *reinterpret_cast<const uint4*>(vals + e);
+            }
+            auto pick = [&](const uint4& q, const uint32_t* p) __attribute__((always_inline)) {
+                return vec ? (sub == 0 ? q.x : sub == 1 ? q.y : sub == 2 ? q.z : q.w) : *p;
+            };
+            const uint32_t k = last ? b : pick(kq, keys + e);
+#else
             const uint32_t k = last ? b : keys[e];
+#endif
             if (last || k != b) {
                 flush(e);
                 if (last) break;
@@ -326,7 +346,11 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
                 b = k;
                 run = e;
             }
+#ifndef EON_PIECE_SCALAR_PAIRS
+            const uint32_t v = pick(vq, vals + e);
+#else
             const uint32_t v = vals[e];
+#endif
 #ifdef EON_PIECE_PROBE_MASK
             // memory-sensitivity probe (tuning builds only, wrong results): every gather from a
             // cache-resident slice of the table

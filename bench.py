@@ -3,8 +3,10 @@
 
 Contract (see DESIGN.md "Measurement"): `python bench.py --gpus N --steps K --warmup W` runs W
 untimed steps, then times exactly K steps bracketed by a barrier + device synchronize, takes the
-max over ranks, and rank 0 prints ONE JSON line.  For N > 1 it is launched by
-torch.distributed.run (one process per GPU, RCCL backend).
+max over ranks, and rank 0 prints ONE JSON line.  For N > 1 it runs one process per GPU (RCCL
+backend): under torch.distributed.run as launched by the driver, or, started without a launcher
+(no WORLD_SIZE), it starts torch.distributed.run itself as a child process before touching the
+GPU and relays rank 0's line.  WORLD_SIZE != --gpus is an error.
 
 Workloads (--workload):
   prove (default)  BASELINE.json configs[3] and the headline metric: eon-uni-stark prove of the
@@ -335,6 +337,15 @@ class ProveWorkload:
         l0, l1 = self.shard.lanes if self.shard else (0, self.vl)
         self.consts = p2_constants_limbs(99)
         self.air = Poseidon2Air(*self.consts, l1 - l0, ctx)
+        self.p2air = self.air  # trace generation always runs the Poseidon2 tracegen kernel
+        if args.air == "generic":
+            # the same AIR through the generic quotient path: its symbolic constraints compiled by
+            # eon_air_program_create and run by k_air_quotient (prover.rs:539-709 for any EonAir)
+            if world > 1:
+                raise SystemExit("--air generic is single-GPU (the lane-sharded prove uses the fused AIR)")
+            from plonky3_eon_amd.air import AirProgram
+
+            self.air = AirProgram(self.p2air, ctx)
         from plonky3_eon_amd.native import NativeKzgPcs, RcclCollective, TorchCollective
 
         self.pcs = NativeKzgPcs(n, 12345, ctx)
@@ -348,7 +359,7 @@ class ProveWorkload:
         # (permutation j sits at row j / VECTOR_LEN, lane j % VECTOR_LEN)
         inputs = synthetic_fr(n * self.vl, 3, 5).reshape(n, self.vl, 3, 4)[:, l0:l1]
         inputs = torch.from_numpy(np.ascontiguousarray(inputs).reshape(-1, 3, 4).view(np.int64)).to(dev)
-        self.trace = self.air.generate_trace(inputs)
+        self.trace = self.p2air.generate_trace(inputs)
         del inputs
         self.alpha, self.zeta = 0x1234567890ABCDEF1234567, 0xFEDCBA09876543210FEDCBA
         self.fs = args.transcript == "fs"
@@ -368,7 +379,9 @@ class ProveWorkload:
         w = 164 * self.vl
         return (f"configs[3]: eon-uni-stark prove, Poseidon2-AIR (VECTOR_LEN {self.vl}, width {w}) "
                 f"log-trace-length {self.log_n} (2^{self.log_n + (self.vl.bit_length() - 1)} permutations), "
-                f"KzgPcs over BN254" + (", Fiat-Shamir transcript" if self.fs else ", fixed alpha/zeta"), world, 1 << self.log_n, f"lane-shard x{world}" if world > 1 else "single")
+                f"KzgPcs over BN254" + (", Fiat-Shamir transcript" if self.fs else ", fixed alpha/zeta")
+                + (", generic AIR program quotient (k_air_quotient)" if self.args.air == "generic" else ""),
+                world, 1 << self.log_n, f"lane-shard x{world}" if world > 1 else "single")
 
     def throughput(self, world, ms):
         n = 1 << self.log_n
@@ -384,6 +397,62 @@ class ProveWorkload:
     def cpu_baseline(self):
         return cpu_baseline_prove(self.log_n, self.vl, self.consts, full=self.args.cpu_full)
 
+
+
+class QuotientWorkload:
+    """quotient_values alone at the headline size (configs[3]'s quotient stage): the Poseidon2-AIR
+    (VECTOR_LEN 8, 1280 constraints) over a 2^(log_trace+1) x 1312 LDE, through the fused kernel
+    (--air fused, k_p2_quotient) or the generic compiled program (--air generic, k_air_quotient;
+    prover.rs:539-709 for any EonAir).  Synthetic canonical LDE values resident in HBM."""
+
+    def __init__(self, args, ctx, dev, rank):
+        import torch
+
+        from plonky3_eon_amd.air import AirProgram, Poseidon2Air
+
+        self.args, self.ctx = args, ctx
+        self.log_n, self.vl, self.log_qd = args.log_trace, args.vector_len, 1
+        p2 = Poseidon2Air(*p2_constants_limbs(99), self.vl, ctx)
+        self.air = AirProgram(p2, ctx) if args.air == "generic" else p2
+        self.p2 = p2
+        q = 1 << (self.log_n + self.log_qd)
+        g = torch.Generator(device=dev)
+        g.manual_seed(5 + rank)
+        self.lde = torch.randint(-(1 << 63), (1 << 63) - 1, (q, p2.width, 4), generator=g, device=dev,
+                                 dtype=torch.int64)
+        self.lde[..., 3] &= (1 << 60) - 1  # canonical (< p)
+        self.alpha = 0x1234567890ABCDEF1234567
+        self.alg_bytes_per_step = q * p2.width * 32 + q * 32
+
+    def step(self):
+        self.out = self.air.quotient_values(self.lde, self.log_n, self.log_qd, self.alpha)
+
+    def describe(self, world):
+        kind = "generic AIR program (k_air_quotient)" if self.args.air == "generic" else "fused kernel (k_p2_quotient)"
+        prog = ""
+        if self.args.air == "generic":
+            st = self.air.stats
+            prog = f", {st['num_instructions']} instructions, {st['num_registers']} registers"
+        return (f"configs[3] quotient stage: quotient_values of the Poseidon2-AIR (VECTOR_LEN {self.vl}, "
+                f"{160 * self.vl} constraints) over 2^{self.log_n + self.log_qd} x {self.p2.width} LDE rows, {kind}{prog}",
+                world, 1 << (self.log_n + self.log_qd), "single")
+
+    def throughput(self, world, ms):
+        return {"rows_per_s": round(world * (1 << (self.log_n + self.log_qd)) / (ms * 1e-3), 1)}, None
+
+    def cpu_baseline(self):
+        from oracle import coracle as C
+
+        C.build()
+        k = C.P2Constants(*p2_constants_limbs(99))
+        rows = 4096
+        lde_s = synthetic_fr(rows, 164 * self.vl, 14)
+        t0 = time.perf_counter()
+        C.p2_quotient_values(lde_s, 11, 1, self.vl, k, C.fr_from_u64(12345))
+        dt = time.perf_counter() - t0
+        q = 1 << (self.log_n + self.log_qd)
+        return {"value": round(dt * q / rows * 1e3, 1), "unit": "ms", "cores": C.num_threads(), "kind": "port",
+                "sample": f"C restatement of quotient_values on {rows} of {q} rows ({dt:.2f} s), scaled linearly"}
 
 
 class FourStepWorkload:
@@ -508,7 +577,10 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default: 3 (prove), 10 (lde, msm)")
     ap.add_argument("--warmup", type=int, default=None, help="default: 1 (prove), 3 (lde, msm)")
-    ap.add_argument("--workload", choices=["prove", "lde", "msm", "ntt4", "msm-shard"], default="prove")
+    ap.add_argument("--workload", choices=["prove", "lde", "msm", "ntt4", "msm-shard", "quotient"], default="prove")
+    ap.add_argument("--air", choices=["fused", "generic"], default="fused",
+                    help="prove / quotient: the Poseidon2-AIR's quotient through the fused kernel or the "
+                         "generic compiled constraint program")
     ap.add_argument("--log-ntt", type=int, default=26, help="ntt4: transform size (configs[4] (i))")
     ap.add_argument("--log-shard-msm", type=int, default=24, help="msm-shard: total points (configs[4] (ii))")
     ap.add_argument("--log-trace", type=int, default=17)
@@ -535,21 +607,52 @@ def make_parser() -> argparse.ArgumentParser:
     return ap
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n: int) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: start N ranks through
+    torch.distributed.run as a CHILD process (this process never touches the GPU and never execs),
+    let rank 0's JSON line through on the inherited stdout, and exit with the launcher's status
+    (non-zero if any rank failed)."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py")]
+    cmd += sys.argv[1:]
+    print(f"bench.py: --gpus {n} without WORLD_SIZE: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr,
+          flush=True)
+    return subprocess.call(cmd)
+
+
 def main() -> int:
     args = make_parser().parse_args()
     if args.steps is None:
         args.steps = 3 if args.workload == "prove" else 10
     if args.warmup is None:
         args.warmup = 1 if args.workload == "prove" else 3
+    if args.gpus < 1:
+        print(f"bench.py: --gpus must be >= 1 (got {args.gpus})", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return self_launch(args.gpus)  # before any GPU call: the parent only waits
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        # a run whose rank count differs from --gpus would time the wrong configuration
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     # EON_BENCH_BACKEND=gloo and EON_BENCH_ONE_DEVICE=1 rehearse the N > 1 code path with every
     # rank on cuda:0 (a one-GPU box); the timings of such a run mean nothing
     backend = os.environ.get("EON_BENCH_BACKEND", "nccl")
@@ -567,7 +670,7 @@ def main() -> int:
     ctx = Context(local_dev)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     wl = {"lde": LdeWorkload, "msm": MsmWorkload, "prove": ProveWorkload, "ntt4": FourStepWorkload,
-          "msm-shard": MsmShardWorkload}[args.workload](args, ctx, dev, rank)
+          "msm-shard": MsmShardWorkload, "quotient": QuotientWorkload}[args.workload](args, ctx, dev, rank)
 
     if args.serial:
         ctx.set_serial(True)
@@ -667,6 +770,15 @@ def main() -> int:
             "achieved_mulmod_per_s": round(mulmods / (gpu_total_ms * 1e-3), 1),
             "frac": round(mulmods / (gpu_total_ms * 1e-3) / MULMOD_PEAK_PER_S, 4),
         }
+        if "valu" not in roof:
+            roof["valu"] = dict(roof["valu_whole_step"], binding=True,
+                                peak_mulmod_per_s=MULMOD_PEAK_PER_S)
+    if "valu" in roof:
+        # the binding resource is the VALU issue of the 256-bit Montgomery products (SURVEY.md
+        # 8(d)); achieved / peak / frac stay the HBM figures of section 8(d)'s algorithmic bytes
+        roof["bound"] = "valu"
+        roof["valu"]["unit"] = "mulmod/s"
+        roof["hbm_frac"] = roof["frac"]
     result = {
         "metric": METRIC,
         "value": round(ms_per_step, 3),

@@ -7,7 +7,8 @@
 // Pipeline (all on device, one stream):
 //   1. k_msm_digits     scalars (Montgomery) -> canonical -> signed c-bit digits; one
 //                       (bucket key, point reference | sign) pair per nonzero digit.
-//   2. radix sort       rocPRIM radix_sort_pairs (stable onesweep) on the low c key bits of the
+//   2. radix sort       radix_sort_pairs (sort.hip: stable LSD, 8-bit digits, LDS-ranked tiles
+//                       with a decoupled look-back) on the low c key bits of the
 //                       group-major pairs: buckets b' = magnitude * groups + group, zero digits
 //                       last (see k_msm_digits).
 //   3. k_bucket_start   bucket boundaries in the sorted pairs.
@@ -33,9 +34,6 @@
 // Fixed-base mode (eon_msm_bases_create with EON_MSM_PRECOMPUTE; the KZG SRS): the bases object
 // stores 2^(c*w) * P_i in affine for every window w, so every window's digits land in ONE bucket
 // set (groups = 1): no per-window bucket reduction and no serial doubling chain at the end.
-#include <hipcub/hipcub.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
-
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -45,6 +43,7 @@
 #include "ec.h"
 #include "ec29.h"
 #include "msm.h"
+#include "sort.h"
 
 using namespace eon;
 
@@ -926,21 +925,10 @@ static std::vector<Batch> make_batches(const Fr* scalars, uint32_t width, uint64
     return batches;
 }
 
-// The digit sort: rocPRIM's onesweep radix sort with 8-bit digits, tuned for these 2^28-pair
-// batches (512 threads x 20 items per block: 3.73 vs 3.94 ms for the default config on 2^28 pairs
-// with 16 key bits, profiles/r02/ubench_sort_configs.txt; EON_MSM_SORT_DEFAULT=1 keeps the
-// library default)
-using SortCfg = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 20>, rocprim::kernel_config<512, 20>, 8,
-                                        rocprim::block_radix_rank_algorithm::match>>;
-
-static hipError_t sort_pairs(void* temp, size_t& bytes, const uint32_t* k_in, uint32_t* k_out, const uint32_t* v_in,
+// The digit sort: sort.hip's stable LSD radix sort (two 8-bit passes for c = 16)
+static hipError_t sort_pairs(void* temp, const uint32_t* k_in, uint32_t* k_out, const uint32_t* v_in,
                              uint32_t* v_out, uint64_t n, uint32_t bits, hipStream_t st) {
-    static const bool dflt = getenv("EON_MSM_SORT_DEFAULT") != nullptr;
-    if (dflt)
-        return rocprim::radix_sort_pairs(temp, bytes, k_in, k_out, v_in, v_out, (size_t)n, 0u, bits, st);
-    return rocprim::radix_sort_pairs<SortCfg>(temp, bytes, k_in, k_out, v_in, v_out, (size_t)n, 0u, bits, st);
+    return radix_sort_pairs(temp, k_in, k_out, v_in, v_out, n, bits, st);
 }
 
 // digits + radix sort + bucket starts + piece offsets of one batch into `out`; `wk` supplies the
@@ -968,10 +956,8 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     EON_HIP(out.start.ensure((nb + 1) * 4ull));
     EON_HIP(out.piece_off.ensure((nb + 1) * 4ull));
     EON_HIP(wk.count.ensure((nb + 1) * 4ull));
-    EON_HIP(sort_pairs(nullptr, bt.sort_bytes, wk.keys.as<uint32_t>(), out.keys2.as<uint32_t>(),
-                       wk.vals.as<uint32_t>(), out.vals2.as<uint32_t>(), E, bt.key_bits, st));
-    EON_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bt.scan_bytes, wk.count.as<uint32_t>(),
-                                             out.piece_off.as<uint32_t>(), (int)(nb + 1), st));
+    bt.sort_bytes = radix_sort_temp_bytes(E, bt.key_bits);
+    bt.scan_bytes = exclusive_scan_temp_bytes(nb + 1);
     EON_HIP(wk.temp.ensure(std::max(bt.sort_bytes, bt.scan_bytes)));
     bt.log_chunk = LOG_CHUNK_MIN;
     while (bt.log_chunk < LOG_CHUNK_MAX && (E >> (bt.log_chunk + 1)) >= (1ull << 20)) bt.log_chunk++;
@@ -989,8 +975,8 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     prof->end(st);
     EON_HIP(hipGetLastError());
     prof->begin("radix_sort_pairs", E * 16, st);
-    EON_HIP(sort_pairs(wk.temp.p, bt.sort_bytes, wk.keys.as<uint32_t>(), out.keys2.as<uint32_t>(),
-                       wk.vals.as<uint32_t>(), out.vals2.as<uint32_t>(), E, bt.key_bits, st));
+    EON_HIP(sort_pairs(wk.temp.p, wk.keys.as<uint32_t>(), out.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
+                       out.vals2.as<uint32_t>(), E, bt.key_bits, st));
     prof->end(st);
     hipLaunchKernelGGL(k_bucket_start, dim3(blocks_for(E / 4 + 1, 256)), dim3(256), 0, st,
                        out.keys2.as<uint32_t>(), E, bt.c, bt.groups, nb, out.start.as<uint32_t>());
@@ -999,8 +985,7 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     EON_HIP(hipMemsetAsync(wk.stat.p, 0, 16, st));
     hipLaunchKernelGGL(k_chunk_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st,
                        out.start.as<uint32_t>(), nb, bt.log_chunk, wk.count.as<uint32_t>(), wk.stat.as<uint32_t>());
-    EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, bt.scan_bytes, wk.count.as<uint32_t>(),
-                                             out.piece_off.as<uint32_t>(), (int)(nb + 1), st));
+    EON_HIP(exclusive_scan_u32(wk.temp.p, wk.count.as<uint32_t>(), out.piece_off.as<uint32_t>(), nb + 1, st));
     // launches are sized by the real counts (12-byte read-back: pieces, nonzero digits, max pieces)
     EON_HIP(hipMemcpyAsync(wk.host_counts, out.piece_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
     EON_HIP(hipMemcpyAsync(wk.host_counts + 1, out.start.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
@@ -1200,13 +1185,11 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
     G1Xyzz* part_cur = wk.piece_sums.as<G1Xyzz>();
     G1Xyzz* part_nxt = wk.piece_sums2.as<G1Xyzz>();
     uint64_t bound = bt.n_pieces;  // >= the partials of the current level
-    size_t scan_bytes = bt.scan_bytes;
     for (uint32_t level = 0; level < (fused ? 0u : bt.levels); level++) {
         uint32_t* off_nxt = off_bufs[next_off];
         hipLaunchKernelGGL(k_level_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st, off_cur,
                            nb, wk.count.as<uint32_t>());
-        EON_HIP(hipcub::DeviceScan::ExclusiveSum(wk.temp.p, scan_bytes, wk.count.as<uint32_t>(),
-                                                 off_nxt, (int)(nb + 1), st));
+        EON_HIP(exclusive_scan_u32(wk.temp.p, wk.count.as<uint32_t>(), off_nxt, nb + 1, st));
         hipLaunchKernelGGL(k_piece_owner, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_nxt, nb,
                            wk.owner.as<uint32_t>());
         // sum_b ceil(p_b / PIECE) <= min(bound, nb + bound / PIECE)

@@ -278,6 +278,92 @@ def run_msmshard(rank, world, group):
     return None
 
 
+def _device_fr(n, seed, dev):
+    """n pseudo-random canonical Fr limbs (n, 4) generated on `dev` from a fixed seed, identical on
+    every rank (top limb < 2^60 < p's, so every value is < p)."""
+    import torch
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    x = torch.randint(-(1 << 63), (1 << 63) - 1, (n, 4), generator=g, device=dev, dtype=torch.int64)
+    x[:, 3] &= (1 << 60) - 1
+    return x
+
+
+def run_fourstep_full(rank, world, group):
+    """BASELINE configs[4] (i) at full size: the 2^26 four-step DFT split over `world` ranks, both
+    output layouts, against the world-1 eon_fourstep_dft_dev output and the single-network DFT."""
+    import torch
+
+    from plonky3_eon_amd import Context
+    from plonky3_eon_amd import _lib as L
+    from plonky3_eon_amd import distributed as D
+
+    import ctypes
+
+    ctx = Context(0)
+    dev = torch.device("cuda:0")
+    log_n = int(os.environ.get("EON_T_LOG_N", "26"))
+    n = 1 << log_n
+    log_n1, log_n2 = D.fourstep_split(log_n)
+    n1, n2 = 1 << log_n1, 1 << log_n2
+    x = _device_fr(n, 2026, dev)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    # world-1 references on this rank: the four-step with no collective and the one-network DFT
+    ref4 = torch.empty_like(x)
+    ctx.check(ctx.lib.eon_fourstep_dft_dev(ctx.handle, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(ref4.data_ptr()),
+                                           log_n, L.EON_FOURSTEP_NATURAL, None))
+    ref1 = torch.empty_like(x)
+    ctx.check(ctx.lib.eon_dft_batch_dev(ctx.handle, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(ref1.data_ptr()),
+                                        n, 1, L.EON_ORDER_NATURAL))
+    torch.cuda.synchronize()
+    if not torch.equal(ref4, ref1):
+        return "world-1 four-step != single-network DFT"
+    del ref1
+    cols = n2 // world
+    local = x.view(n1, n2, 4)[:, rank * cols:(rank + 1) * cols].contiguous()
+    del x
+    out = D.fourstep_dft(ctx, local, log_n, rank, world, group)  # one all_to_all
+    per = n1 // world
+    want = ref4.view(n2, n1, 4)[:, rank * per:(rank + 1) * per]
+    if not torch.equal(out, want):
+        return f"2^{log_n} four-step, transposed layout, rank {rank}/{world} != world-1 output"
+    del out
+    out = D.fourstep_dft(ctx, local, log_n, rank, world, group, natural=True)  # two all_to_alls
+    if not torch.equal(out, ref4[rank * (n // world):(rank + 1) * (n // world)]):
+        return f"2^{log_n} four-step, natural layout, rank {rank}/{world} != world-1 output"
+    return None
+
+
+def run_msmshard_full(rank, world, group):
+    """BASELINE configs[4] (ii) at full size: the 2^24-term MSM over the alpha = 12345 SRS split by
+    point range over `world` ranks (eon_msm_sharded_dev) == [f(alpha)] G."""
+    import torch
+
+    from plonky3_eon_amd import Context
+    from plonky3_eon_amd import distributed as D
+    from plonky3_eon_amd.msm import MsmBases, srs_powers
+
+    ctx = Context(0)
+    dev = torch.device("cuda:0")
+    log_n = int(os.environ.get("EON_T_LOG_N", "24"))
+    n = 1 << log_n
+    lo, hi = D.shard_range(n, rank, world)
+    srs = srs_powers(n, 12345, ctx)
+    bases = MsmBases(np.ascontiguousarray(srs[lo:hi]), ctx, precompute=True)
+    del srs
+    s = _device_fr(n, 2424, dev)
+    got = D.msm_sharded(bases, s[lo:hi].contiguous(), "cuda:0", group)
+    bases.close()
+    if rank != 0:
+        return None
+    sh = s.cpu().numpy().view(np.uint64).reshape(n, 1, 4)
+    f_alpha = C.eval_poly_col(sh, 0, C.fr_from_u64(12345))
+    if not np.array_equal(np.asarray(got).reshape(8), C.g1_mul(C.g1_generator(), f_alpha)):
+        return f"2^{log_n} MSM sharded over {world} ranks != [f(alpha)]G"
+    return None
+
+
 def run_openshard(rank, world, group):
     import ctypes
 
@@ -319,7 +405,8 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         fn = {"cpu": run_cpu, "gpu": run_gpu, "a2a": run_a2a, "fourstep": run_fourstep,
-              "msmshard": run_msmshard, "native": run_native, "openshard": run_openshard}[mode]
+              "msmshard": run_msmshard, "native": run_native, "openshard": run_openshard,
+              "fourstep_full": run_fourstep_full, "msmshard_full": run_msmshard_full}[mode]
         why = fn(rank, world, None)
     except Exception:
         why = traceback.format_exc()

@@ -119,6 +119,31 @@ def test_poseidon2_generic_equals_fused(gpu_ctx, vl, log_n):
     np.testing.assert_array_equal(generic.view(np.uint64), want)
 
 
+def test_poseidon2_vl8_generic_equals_fused_2_12(gpu_ctx):
+    """The headline AIR (VECTOR_LEN 8: 1312 columns, 1280 constraints) through the generic program
+    equals the fused kernel on a 2^12-row trace (2^13 quotient rows)."""
+    import torch
+
+    from plonky3_eon_amd.air import AirProgram, Poseidon2Air
+
+    py = O.p2_constants(2024, 4, 56)
+    k = C.P2Constants([[lim(v) for v in r] for r in py[0]], [lim(v) for v in py[1]],
+                      [[lim(v) for v in r] for r in py[2]])
+    air = Poseidon2Air(k.begin, k.partial, k.end, 8, gpu_ctx)
+    prog = AirProgram(air, gpu_ctx)
+    assert prog.num_constraints == 1280 and air.width == 1312
+    log_n, log_qd = 12, 1
+    q = 1 << (log_n + log_qd)
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(1212)
+    lde = torch.randint(-(1 << 63), (1 << 63) - 1, (q, air.width, 4), generator=g, device="cuda:0", dtype=torch.int64)
+    lde[..., 3] &= (1 << 60) - 1
+    alpha = 0x0123456789ABCDEF0123
+    generic = prog.quotient_values(lde, log_n, log_qd, alpha)
+    fused = air.quotient_values(lde, log_n, log_qd, alpha)
+    assert torch.equal(generic, fused)  # the fused kernel is oracle-checked at VECTOR_LEN 1/2/8
+
+
 def test_program_rejects_bad_input(gpu_ctx):
     import ctypes
 

@@ -27,9 +27,29 @@ def test_bench_json_contract():
     assert d["value"] > 0 and d["higher_is_better"] is False and d["scaling"] in ("weak", "strong")
     assert "workload" in d["config"]
     r = d["roofline"]
-    assert r["bound"] in ("hbm", "mfma") and r["unit"] in ("GB/s", "TFLOP/s")
+    assert r["bound"] in ("hbm", "mfma", "valu") and r["unit"] in ("GB/s", "TFLOP/s")
+    if r["bound"] == "valu":  # the binding integer roofline beside the HBM figures
+        v = r["valu"]
+        assert v["unit"] == "mulmod/s" and 0 < v["frac"] <= 1.2 and r["hbm_frac"] == r["frac"]
     assert r["peak"] == 8000.0 and r["achieved"] > 0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert "traffic" in r
     c = d["cpu_baseline"]
     assert c["value"] > 0 and c["cores"] >= 1 and c["kind"] in ("reference", "port") and c["sample"]
+
+
+def test_bench_self_launch_two_ranks():
+    """`bench.py --gpus 2` with no launcher starts its own two ranks (here gloo ranks sharing cuda:0,
+    EON_BENCH_BACKEND=gloo EON_BENCH_ONE_DEVICE=1) and rank 0 prints n_gpus 2."""
+    import os
+
+    env = dict(os.environ, EON_BENCH_BACKEND="gloo", EON_BENCH_ONE_DEVICE="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--workload", "ntt4", "--log-ntt", "16",
+                          "--steps", "2", "--warmup", "1"], cwd=ROOT, capture_output=True, text=True, timeout=240,
+                         env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["cpu_baseline"] is None

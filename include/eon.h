@@ -41,6 +41,19 @@ typedef struct {
     uint64_t y[4];
 } eon_g1_affine;
 
+/* BN254 G2 affine point on the sextic twist over Fq2 = Fq[u]/(u^2 + 1): x = x[0] + x[1] u (Fq
+ * Montgomery [u64;4] LE each), identity = all zero.  Gt / Fq12 element in the tower
+ * Fq12 = Fq6[w]/(w^2 - v), Fq6 = Fq2[v]/(v^3 - (9 + u)): c[2k], c[2k+1] = the Fq2 coefficient k
+ * in the order c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2 (halo2curves' Fq12 layout). */
+typedef struct {
+    uint64_t x[2][4];
+    uint64_t y[2][4];
+} eon_g2_affine;
+
+typedef struct {
+    uint64_t c[12][4];
+} eon_fq12;
+
 typedef struct eon_ctx eon_ctx;
 
 /* Collectives over DEVICE buffers among `world` processes (one per GPU), called with a context's
@@ -383,6 +396,26 @@ int eon_msm_sharded_dev(eon_ctx* ctx, const eon_msm_bases* bases, const eon_fr* 
  * affine, i < n.  `alpha` is a host pointer; `out` host (eon_g1_srs_powers) or device (_dev). */
 int eon_g1_srs_powers(eon_ctx* ctx, const eon_fr* alpha, uint64_t n, eon_g1_affine* out);
 int eon_g1_srs_powers_dev(eon_ctx* ctx, const eon_fr* alpha, uint64_t n, eon_g1_affine* out);
+
+/* ---- verifier pairings (setup / verify, not prove time) --------------------
+ * All host pointers, synchronous.  G1 / G2 inputs must be canonical and on their curves
+ * (EON_E_ARG otherwise).
+ *
+ * eon_g2_mul: out = k * base (base NULL = G2::generator()); init_srs_unsafe's
+ *   g2_alpha = [alpha] G2 (kzg/src/params.rs:123-139), G2::mul_scalar (bn254/src/curve.rs).
+ * eon_multi_pairing: out = prod_i e(p[i], q[i]) (multi_pairing, bn254/src/curve.rs:439-452;
+ *   pairing, :429-436, is n = 1): the optimal-ate Miller loops and one final exponentiation; the
+ *   identity of Gt (Fq12 one) for n = 0.
+ * eon_kzg_verify_batch: *ok = 1 iff prod_i e(C_i - v_i G1, G2) e(-W_i, g2_alpha - z_i G2) is the
+ *   identity -- verify_batch (kzg/src/util.rs:245-292; for n = 1 verify_single, :150-168, whose
+ *   e(C - vG1, G2) == e(W, g2_alpha - zG2) is the same condition).  *ok = 0 is the reference's
+ *   Err(KzgError::ProofShapeMismatch); n = 0 is Ok.  Pairs sharing a G2 argument are merged by
+ *   bilinearity before the Miller loops (one pairing per distinct opening point, plus one). */
+int eon_g2_mul(eon_ctx* ctx, const eon_g2_affine* base, const eon_fr* k, eon_g2_affine* out);
+int eon_multi_pairing(eon_ctx* ctx, const eon_g1_affine* p, const eon_g2_affine* q, uint64_t n, eon_fq12* out);
+int eon_kzg_verify_batch(eon_ctx* ctx, const eon_g1_affine* commitments, const eon_g1_affine* witnesses,
+                         const eon_fr* values, const eon_fr* points, uint64_t n, const eon_g2_affine* g2_alpha,
+                         int* ok);
 
 #ifdef __cplusplus
 }

@@ -115,6 +115,9 @@ SIGNATURES = {
     "eon_kzg_opening_bases_create_many": (_INT, [_P, _P, _U64, _P, _U32, _P]),
     "eon_msm_bases_create_dev": (_INT, [_P, _P, _U64, _U32, ctypes.POINTER(_P)]),
     "eon_g1_srs_powers": (_INT, [_P, _P, _U64, _P]),
+    "eon_g2_mul": (_INT, [_P, _P, _P, _P]),
+    "eon_multi_pairing": (_INT, [_P, _P, _P, _U64, _P]),
+    "eon_kzg_verify_batch": (_INT, [_P, _P, _P, _P, _P, _U64, _P, ctypes.POINTER(ctypes.c_int)]),
     "eon_g1_srs_powers_dev": (_INT, [_P, _P, _U64, _P]),
     "eon_selectors_on_coset_dev": (_INT, [_P, _U32, _U32, _P, _P]),
     "eon_p2air_create": (_INT, [_P, _P, _U32, ctypes.POINTER(_P)]),

@@ -1,0 +1,428 @@
+// KZG verifier pairings on the GPU: G2 scalar multiplication (the SRS's
+// g2_alpha, kzg/src/params.rs:123-139), multi_pairing (bn254/src/curve.rs:439-452) and
+// verify_batch / verify_single (kzg/src/util.rs:150-168, 245-292).  Arithmetic: pairing.h.
+//
+// verify_batch checks prod_i e(C_i - v_i G1, G2) e(-W_i, [alpha]G2 - z_i G2) == 1.  Pairs with
+// the same G2 argument are merged by bilinearity before any Miller loop -- every commitment pair
+// shares G2 itself, and the witness pairs share [alpha - z]G2 per distinct opening point z (the
+// headline proof's 2626 openings have three: zeta, zeta h, and zeta for the quotient chunks) --
+// so the product is the same element of Gt computed from 1 + (#distinct z) pairings:
+//   e(sum_i C_i - (sum_i v_i) G1, G2) * prod_z e(-sum_{i: z_i = z} W_i, [alpha]G2 - z G2).
+// verify_single's e(C - vG1, G2) == e(W, [alpha]G2 - zG2) is the same product being 1.
+//
+//   k_vb_sums     one block per distinct point: -sum W_i over its openings; one more block for
+//                 sum C_i and sum v_i (XYZZ partial sums per thread, LDS tree)
+//   k_vb_pairs    the merged pairs: P_0 = sum C - (sum v) G1 with Q_0 = G2, P_z = -sum W with
+//                 Q_z = [alpha]G2 - z G2 (Jacobian double-and-add over Fq2, then affine)
+//   k_miller      one thread per pair: f_{6x+2,Q}(P) and the two Frobenius-twisted lines
+//   k_final_exp   product of the Miller values, easy part f^((q^6-1)(q^2+1)), hard part
+//                 f^((q^4-q^2+1)/r) by square-and-multiply, and the test against 1
+#include <algorithm>
+#include <map>
+#include <vector>
+
+#include "context.h"
+#include "pairing.h"
+
+using namespace eon;
+
+namespace {
+
+struct HardExp {
+    uint32_t w[pc::HARD_EXP_WORDS];
+};
+
+// ---- Miller loop --------------------------------------------------------------------------------
+
+// The line through T and A (tangent when equal, vertical when A = -T) on the twist, untwisted
+// and evaluated at P = (xp, yp): with lambda the twist slope,
+//   l = -yp + (lambda xp) w + (y_T - lambda x_T) w^3,   vertical: l = xp - x_T w^2.
+// Also returns T + A (affine; the Miller loop never meets the identity before its last line).
+__device__ __noinline__ Fq12 line_and_step(G2Affine& T, const G2Affine& A, const Fq& xp, const Fq& yp) {
+    Fq12 l = {f6_zero(), f6_zero()};
+    Fq2 lam;
+    if (!f2_eq(T.x, A.x)) {
+        lam = f2_mul(f2_sub(A.y, T.y), f2_inv(f2_sub(A.x, T.x)));
+    } else if (f2_eq(T.y, A.y)) {
+        const Fq2 x2 = f2_sqr(T.x);
+        lam = f2_mul(f2_add(f2_dbl(x2), x2), f2_inv(f2_dbl(T.y)));
+    } else {
+        l.c0.c0 = {xp, Fq::zero()};
+        l.c0.c1 = f2_neg(T.x);
+        T = {f2_zero(), f2_zero()};
+        return l;
+    }
+    l.c0.c0 = {neg(yp), Fq::zero()};
+    l.c1.c0 = f2_mul_fq(lam, xp);
+    l.c1.c1 = f2_sub(T.y, f2_mul(lam, T.x));
+    const Fq2 x3 = f2_sub(f2_sub(f2_sqr(lam), T.x), A.x);
+    const Fq2 y3 = f2_sub(f2_mul(lam, f2_sub(T.x, x3)), T.y);
+    T = {x3, y3};
+    return l;
+}
+
+__device__ __noinline__ Fq12 miller_loop(const G1Affine& p, const G2Affine& q) {
+    if (is_inf(p) || g2_is_inf(q)) return f12_one();
+    Fq12 f = f12_one();
+    G2Affine T = q;
+    for (int b = 63; b >= 0; b--) {  // 6x + 2 below its top bit, MSB first
+        f = f12_mul(f12_sqr(f), line_and_step(T, T, p.x, p.y));
+        if ((pc::ATE_LOOP_LOW >> b) & 1) f = f12_mul(f, line_and_step(T, q, p.x, p.y));
+    }
+    // Q1 = pi(Q), -Q2 = -pi^2(Q) on the twist: pi(x, y) = (conj(x) g_x, conj(y) g_y),
+    // pi^2(x, y) = (x g2_x, -y)
+    const G2Affine q1 = {f2_mul(f2_conj(q.x), f2_c(pc::TWIST_FROB_X)), f2_mul(f2_conj(q.y), f2_c(pc::TWIST_FROB_Y))};
+    const G2Affine nq2 = {f2_mul_fq(q.x, fq_c(pc::TWIST_FROB2_X)), q.y};
+    f = f12_mul(f, line_and_step(T, q1, p.x, p.y));
+    f = f12_mul(f, line_and_step(T, nq2, p.x, p.y));
+    return f;
+}
+
+__global__ void __launch_bounds__(64) k_miller(const G1Affine* __restrict__ P, const G2Affine* __restrict__ Q, uint32_t m,
+                                               Fq12* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    out[i] = miller_loop(P[i], Q[i]);
+}
+
+__device__ __noinline__ Fq12 final_exponentiation(const Fq12& f, const HardExp& e) {
+    // easy part: f^((q^6 - 1)(q^2 + 1))
+    Fq12 t = f12_mul(f12_conj(f), f12_inv(f));
+    t = f12_mul(f12_frob<2>(t), t);
+    // hard part: t^((q^4 - q^2 + 1) / r), MSB first
+    Fq12 r = f12_one();
+    bool started = false;
+    for (int w = (int)pc::HARD_EXP_WORDS - 1; w >= 0; w--)
+        for (int b = 31; b >= 0; b--) {
+            if (started) r = f12_sqr(r);
+            if ((e.w[w] >> b) & 1) {
+                r = started ? f12_mul(r, t) : t;
+                started = true;
+            }
+        }
+    return r;
+}
+
+__global__ void k_final_exp(const Fq12* __restrict__ f, uint32_t m, HardExp e, Fq12* __restrict__ out,
+                            uint32_t* __restrict__ is_one) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    Fq12 acc = f12_one();
+    for (uint32_t i = 0; i < m; i++) acc = f12_mul(acc, f[i]);
+    const Fq12 r = final_exponentiation(acc, e);
+    *out = r;
+    *is_one = f12_is_one(r) ? 1u : 0u;
+}
+
+// ---- verify_batch: merged pairs -----------------------------------------------------------------
+
+constexpr uint32_t VB_THREADS = 128;
+
+// block g < G: -sum of the witnesses of openings ord[gs[g] .. gs[g+1]); block G: sum of every
+// commitment and sum of every value
+__global__ void __launch_bounds__(VB_THREADS) k_vb_sums(const G1Affine* __restrict__ com, const G1Affine* __restrict__ wit,
+                                                        const Fr* __restrict__ val, const uint32_t* __restrict__ ord,
+                                                        const uint32_t* __restrict__ gs, uint32_t G, uint32_t n,
+                                                        G1Xyzz* __restrict__ sums, Fr* __restrict__ vsum) {
+    __shared__ G1Xyzz part[VB_THREADS];
+    __shared__ Fr vpart[VB_THREADS];
+    const uint32_t g = blockIdx.x, t = threadIdx.x;
+    G1Xyzz acc = xyzz_inf();
+    Fr vacc = Fr::zero();
+    if (g < G) {
+        for (uint32_t i = gs[g] + t; i < gs[g + 1]; i += VB_THREADS) acc = xyzz_add_affine(acc, wit[ord[i]]);
+    } else {
+        for (uint32_t i = t; i < n; i += VB_THREADS) {
+            acc = xyzz_add_affine(acc, com[i]);
+            vacc = add(vacc, val[i]);
+        }
+    }
+    part[t] = acc;
+    vpart[t] = vacc;
+    __syncthreads();
+    for (uint32_t s = VB_THREADS / 2; s > 0; s >>= 1) {
+        if (t < s) {
+            part[t] = xyzz_add(part[t], part[t + s]);
+            vpart[t] = add(vpart[t], vpart[t + s]);
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        G1Xyzz r = part[0];
+        if (g < G && !is_inf(r)) r.Y = neg(r.Y);  // -sum W
+        sums[g] = r;
+        if (g == G) *vsum = vpart[0];
+    }
+}
+
+__device__ __noinline__ G1Xyzz g1_mul_words(const G1Affine& p, const uint32_t (&k)[8]) {
+    G1Xyzz acc = xyzz_inf();
+    for (int w = 7; w >= 0; w--)
+        for (int b = 31; b >= 0; b--) {
+            acc = xyzz_dbl(acc);
+            if ((k[w] >> b) & 1) acc = xyzz_add_affine(acc, p);
+        }
+    return acc;
+}
+
+__global__ void __launch_bounds__(64) k_vb_pairs(const G1Xyzz* __restrict__ sums, const Fr* __restrict__ vsum,
+                                                 const Fr* __restrict__ zs, uint32_t G, G2Affine g2_alpha,
+                                                 G1Affine* __restrict__ P, G2Affine* __restrict__ Q) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > G) return;
+    if (t == 0) {
+        // P_0 = sum C - (sum v) G1, Q_0 = G2
+        G1Affine g1;
+        g1.x = from_u64<FqP>(1);
+        g1.y = from_u64<FqP>(2);
+        const Fr v = to_canonical(*vsum);
+        uint32_t k[8];
+        for (int i = 0; i < 8; i++) k[i] = v.v[i];
+        G1Affine vg = xyzz_to_affine(g1_mul_words(g1, k));
+        P[0] = xyzz_to_affine(xyzz_add_affine(sums[G], affine_neg(vg)));
+        Q[0] = g2_generator();
+    } else {
+        // P_z = -sum W, Q_z = [alpha]G2 - z G2
+        const Fr z = to_canonical(zs[t - 1]);
+        uint32_t k[8];
+        for (int i = 0; i < 8; i++) k[i] = z.v[i];
+        G2Jac zg = g2_mul_words(g2_generator(), k);
+        if (!f2_is_zero(zg.Z)) zg.Y = f2_neg(zg.Y);
+        P[t] = xyzz_to_affine(sums[t - 1]);
+        Q[t] = g2j_to_affine(g2j_add_affine(zg, g2_alpha));
+    }
+}
+
+__global__ void k_g2_mul(G2Affine base, Fr k_mont, G2Affine* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const Fr kc = to_canonical(k_mont);
+    uint32_t k[8];
+    for (int i = 0; i < 8; i++) k[i] = kc.v[i];
+    *out = g2j_to_affine(g2_mul_words(base, k));
+}
+
+// ---- ABI conversions ----------------------------------------------------------------------------
+
+Fq fq_from_u64x4(const uint64_t (&l)[4]) {
+    Fq r;
+    for (int i = 0; i < 4; i++) {
+        r.v[2 * i] = (uint32_t)l[i];
+        r.v[2 * i + 1] = (uint32_t)(l[i] >> 32);
+    }
+    return r;
+}
+
+void fq_to_u64x4(const Fq& a, uint64_t (&l)[4]) {
+    for (int i = 0; i < 4; i++) l[i] = (uint64_t)a.v[2 * i] | (uint64_t)a.v[2 * i + 1] << 32;
+}
+
+bool fq_is_canonical(const Fq& x) {
+    for (int i = 7; i >= 0; i--) {
+        if (x.v[i] < FqP::P[i]) return true;
+        if (x.v[i] > FqP::P[i]) return false;
+    }
+    return false;
+}
+
+Status g2_from_abi(const eon_g2_affine& a, G2Affine& out) {
+    out.x = {fq_from_u64x4(a.x[0]), fq_from_u64x4(a.x[1])};
+    out.y = {fq_from_u64x4(a.y[0]), fq_from_u64x4(a.y[1])};
+    for (const Fq* c : {&out.x.c0, &out.x.c1, &out.y.c0, &out.y.c1})
+        if (!fq_is_canonical(*c)) return Status::err(EON_E_ARG, "G2 coordinate is not a canonical Fq");
+    if (!g2_on_curve(out)) return Status::err(EON_E_ARG, "G2 point is not on the twist curve");
+    return Status::ok();
+}
+
+void g2_to_abi(const G2Affine& a, eon_g2_affine& out) {
+    fq_to_u64x4(a.x.c0, out.x[0]);
+    fq_to_u64x4(a.x.c1, out.x[1]);
+    fq_to_u64x4(a.y.c0, out.y[0]);
+    fq_to_u64x4(a.y.c1, out.y[1]);
+}
+
+Status g1_from_abi(const eon_g1_affine& a, G1Affine& out) {
+    out.x = fq_from_u64x4(a.x);
+    out.y = fq_from_u64x4(a.y);
+    if (!fq_is_canonical(out.x) || !fq_is_canonical(out.y))
+        return Status::err(EON_E_ARG, "G1 coordinate is not a canonical Fq");
+    if (!is_inf(out)) {
+        // y^2 = x^3 + 3
+        const Fq lhs = mul(out.y, out.y);
+        const Fq rhs = add(mul(mul(out.x, out.x), out.x), from_u64<FqP>(3));
+        if (lhs != rhs) return Status::err(EON_E_ARG, "G1 point is not on the curve");
+    }
+    return Status::ok();
+}
+
+void fq12_to_abi(const Fq12& a, eon_fq12& out) {
+    const Fq2* x = &a.c0.c0;
+    for (int i = 0; i < 6; i++) {
+        fq_to_u64x4(x[i].c0, out.c[2 * i]);
+        fq_to_u64x4(x[i].c1, out.c[2 * i + 1]);
+    }
+}
+
+HardExp hard_exp() {
+    HardExp e;
+    for (uint32_t i = 0; i < pc::HARD_EXP_WORDS; i++) e.w[i] = pc::HARD_EXP[i];
+    return e;
+}
+
+// product of the pairings of m device pairs -> Gt element and the is-one flag (host)
+Status pair_product(eon_ctx* ctx, const G1Affine* P, const G2Affine* Q, uint32_t m, Fq12* gt, bool* one) {
+    DevBuf f, res;
+    EON_HIP(f.ensure((size_t)std::max<uint32_t>(m, 1) * sizeof(Fq12)));
+    EON_HIP(res.ensure(sizeof(Fq12) + 16));
+    if (m) hipLaunchKernelGGL(k_miller, dim3((m + 63) / 64), dim3(64), 0, ctx->stream, P, Q, m, f.as<Fq12>());
+    hipLaunchKernelGGL(k_final_exp, dim3(1), dim3(64), 0, ctx->stream, f.as<Fq12>(), m, hard_exp(), res.as<Fq12>(),
+                       reinterpret_cast<uint32_t*>(res.as<char>() + sizeof(Fq12)));
+    EON_HIP(hipGetLastError());
+    struct {
+        Fq12 v;
+        uint32_t flag;
+    } host;
+    EON_HIP(hipMemcpyAsync(&host.v, res.p, sizeof(Fq12), hipMemcpyDeviceToHost, ctx->stream));
+    EON_HIP(hipMemcpyAsync(&host.flag, res.as<char>() + sizeof(Fq12), 4, hipMemcpyDeviceToHost, ctx->stream));
+    EON_HIP(hipStreamSynchronize(ctx->stream));
+    if (gt) *gt = host.v;
+    if (one) *one = host.flag != 0;
+    return Status::ok();
+}
+
+int finish(eon_ctx* ctx, const Status& s) {
+    if (s.bad()) ctx->last_error = s.msg;
+    return s.code;
+}
+
+}  // namespace
+
+extern "C" {
+
+int eon_g2_mul(eon_ctx* ctx, const eon_g2_affine* base, const eon_fr* k, eon_g2_affine* out) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    Status s = [&]() -> Status {
+        if (!k || !out) return Status::err(EON_E_ARG, "null argument");
+        G2Affine b = g2_generator();
+        if (base) EON_TRY(g2_from_abi(*base, b));
+        const Fr kk = fr_from_abi(k);
+        if (!fr_is_canonical(kk)) return Status::err(EON_E_ARG, "scalar is not a canonical Fr");
+        DevBuf d;
+        EON_HIP(d.ensure(sizeof(G2Affine)));
+        hipLaunchKernelGGL(k_g2_mul, dim3(1), dim3(64), 0, ctx->stream, b, kk, d.as<G2Affine>());
+        EON_HIP(hipGetLastError());
+        G2Affine r;
+        EON_HIP(hipMemcpyAsync(&r, d.p, sizeof(r), hipMemcpyDeviceToHost, ctx->stream));
+        EON_HIP(hipStreamSynchronize(ctx->stream));
+        g2_to_abi(r, *out);
+        return Status::ok();
+    }();
+    return finish(ctx, s);
+}
+
+int eon_multi_pairing(eon_ctx* ctx, const eon_g1_affine* p, const eon_g2_affine* q, uint64_t n, eon_fq12* out) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    Status s = [&]() -> Status {
+        if (!out || (n && (!p || !q))) return Status::err(EON_E_ARG, "null argument");
+        if (n > (1u << 24)) return Status::err(EON_E_SHAPE, "at most 2^24 pairs");
+        std::vector<G1Affine> hp(n);
+        std::vector<G2Affine> hq(n);
+        for (uint64_t i = 0; i < n; i++) {
+            EON_TRY(g1_from_abi(p[i], hp[i]));
+            EON_TRY(g2_from_abi(q[i], hq[i]));
+        }
+        DevBuf dp, dq;
+        EON_HIP(dp.ensure(std::max<uint64_t>(n, 1) * sizeof(G1Affine)));
+        EON_HIP(dq.ensure(std::max<uint64_t>(n, 1) * sizeof(G2Affine)));
+        if (n) {
+            EON_HIP(hipMemcpyAsync(dp.p, hp.data(), n * sizeof(G1Affine), hipMemcpyHostToDevice, ctx->stream));
+            EON_HIP(hipMemcpyAsync(dq.p, hq.data(), n * sizeof(G2Affine), hipMemcpyHostToDevice, ctx->stream));
+        }
+        Fq12 gt;
+        EON_TRY(pair_product(ctx, dp.as<G1Affine>(), dq.as<G2Affine>(), (uint32_t)n, &gt, nullptr));
+        fq12_to_abi(gt, *out);
+        return Status::ok();
+    }();
+    return finish(ctx, s);
+}
+
+int eon_kzg_verify_batch(eon_ctx* ctx, const eon_g1_affine* commitments, const eon_g1_affine* witnesses,
+                         const eon_fr* values, const eon_fr* points, uint64_t n, const eon_g2_affine* g2_alpha,
+                         int* ok) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    Status s = [&]() -> Status {
+        if (!ok || !g2_alpha || (n && (!commitments || !witnesses || !values || !points)))
+            return Status::err(EON_E_ARG, "null argument");
+        if (n > (1u << 26)) return Status::err(EON_E_SHAPE, "at most 2^26 openings");
+        *ok = 0;
+        if (n == 0) {  // verify_batch: no openings is Ok(())
+            *ok = 1;
+            return Status::ok();
+        }
+        G2Affine ga;
+        EON_TRY(g2_from_abi(*g2_alpha, ga));
+        std::vector<G1Affine> hc(n), hw(n);
+        std::vector<Fr> hv(n);
+        // group the openings by point (host: the points are few and small)
+        std::map<std::vector<uint32_t>, uint32_t> gid;
+        std::vector<Fr> zs;
+        std::vector<uint32_t> grp(n);
+        for (uint64_t i = 0; i < n; i++) {
+            EON_TRY(g1_from_abi(commitments[i], hc[i]));
+            EON_TRY(g1_from_abi(witnesses[i], hw[i]));
+            hv[i] = fr_from_abi(&values[i]);
+            const Fr z = fr_from_abi(&points[i]);
+            if (!fr_is_canonical(hv[i]) || !fr_is_canonical(z)) return Status::err(EON_E_ARG, "value or point is not a canonical Fr");
+            std::vector<uint32_t> key(z.v, z.v + 8);
+            auto it = gid.find(key);
+            if (it == gid.end()) {
+                it = gid.emplace(key, (uint32_t)zs.size()).first;
+                zs.push_back(z);
+            }
+            grp[i] = it->second;
+        }
+        const uint32_t G = (uint32_t)zs.size();
+        std::vector<uint32_t> gs(G + 1, 0), ord(n);
+        for (uint64_t i = 0; i < n; i++) gs[grp[i] + 1]++;
+        for (uint32_t g = 0; g < G; g++) gs[g + 1] += gs[g];
+        {
+            std::vector<uint32_t> fill(gs.begin(), gs.end() - 1);
+            for (uint64_t i = 0; i < n; i++) ord[fill[grp[i]]++] = (uint32_t)i;
+        }
+        DevBuf dc, dw, dv, dord, dgs, dz, dsums, dvsum, dP, dQ;
+        EON_HIP(dc.ensure(n * sizeof(G1Affine)));
+        EON_HIP(dw.ensure(n * sizeof(G1Affine)));
+        EON_HIP(dv.ensure(n * sizeof(Fr)));
+        EON_HIP(dord.ensure(n * 4));
+        EON_HIP(dgs.ensure((G + 1) * 4));
+        EON_HIP(dz.ensure(G * sizeof(Fr)));
+        EON_HIP(dsums.ensure((G + 1) * sizeof(G1Xyzz)));
+        EON_HIP(dvsum.ensure(sizeof(Fr)));
+        EON_HIP(dP.ensure((G + 1) * sizeof(G1Affine)));
+        EON_HIP(dQ.ensure((G + 1) * sizeof(G2Affine)));
+        hipStream_t st = ctx->stream;
+        EON_HIP(hipMemcpyAsync(dc.p, hc.data(), n * sizeof(G1Affine), hipMemcpyHostToDevice, st));
+        EON_HIP(hipMemcpyAsync(dw.p, hw.data(), n * sizeof(G1Affine), hipMemcpyHostToDevice, st));
+        EON_HIP(hipMemcpyAsync(dv.p, hv.data(), n * sizeof(Fr), hipMemcpyHostToDevice, st));
+        EON_HIP(hipMemcpyAsync(dord.p, ord.data(), n * 4, hipMemcpyHostToDevice, st));
+        EON_HIP(hipMemcpyAsync(dgs.p, gs.data(), (G + 1) * 4, hipMemcpyHostToDevice, st));
+        EON_HIP(hipMemcpyAsync(dz.p, zs.data(), G * sizeof(Fr), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_vb_sums, dim3(G + 1), dim3(VB_THREADS), 0, st, dc.as<G1Affine>(), dw.as<G1Affine>(),
+                           dv.as<Fr>(), dord.as<uint32_t>(), dgs.as<uint32_t>(), G, (uint32_t)n, dsums.as<G1Xyzz>(),
+                           dvsum.as<Fr>());
+        hipLaunchKernelGGL(k_vb_pairs, dim3((G + 1 + 63) / 64), dim3(64), 0, st, dsums.as<G1Xyzz>(), dvsum.as<Fr>(),
+                           dz.as<Fr>(), G, ga, dP.as<G1Affine>(), dQ.as<G2Affine>());
+        EON_HIP(hipGetLastError());
+        bool one = false;
+        EON_TRY(pair_product(ctx, dP.as<G1Affine>(), dQ.as<G2Affine>(), G + 1, nullptr, &one));
+        *ok = one ? 1 : 0;
+        return Status::ok();
+    }();
+    return finish(ctx, s);
+}
+
+}  // extern "C"

@@ -82,3 +82,27 @@ def test_headline_proof_valid(gpu_ctx, log_n, vl):
     bad = list(openings)
     bad[0] = (bad[0][0], bad[0][1], (bad[0][2] + 1) % O.P, bad[0][3])
     assert not E.verify_batch(bad, g2a)
+    # ALL 2626 openings (2 x 1312 trace + 2 quotient chunks) through the GPU verify_batch
+    # (eon_kzg_verify_batch: the same multi-pairing, merged per opening point), and a tampered one
+    from plonky3_eon_amd import verify as GV
+
+    def fr_l(x):
+        return np.array(O.int_to_limbs(O.to_mont(x % O.P)), dtype=np.uint64)
+
+    com, wit, val, pts = [], [], [], []
+    for p, z in enumerate((proof.zeta, zn)):
+        com.append(tc)
+        wit.append(np.asarray(tr.witnesses[0][p]).reshape(-1, 8))
+        val.append(np.asarray(tr.values[0][p]).reshape(-1, 4))
+        pts.append(np.tile(fr_l(z), (tc.shape[0], 1)))
+    for c, qc in enumerate(proof.quotient_commit):
+        com.append(np.asarray(qc).reshape(1, 8))
+        wit.append(np.asarray(qo.witnesses[c][0]).reshape(1, 8))
+        val.append(np.asarray(qo.values[c][0]).reshape(1, 4))
+        pts.append(fr_l(proof.zeta)[None])
+    com, wit, val, pts = (np.ascontiguousarray(np.concatenate(a), dtype=np.uint64) for a in (com, wit, val, pts))
+    assert com.shape[0] == 2 * tc.shape[0] + len(proof.quotient_commit)
+    g2a_gpu = GV.g2_mul(12345, ctx=gpu_ctx)
+    assert GV.verify_batch(com, wit, val, pts, g2a_gpu, ctx=gpu_ctx) is True
+    val[tc.shape[0] + 5] = fr_l(V.fr_int(val[tc.shape[0] + 5]) + 1)
+    assert GV.verify_batch(com, wit, val, pts, g2a_gpu, ctx=gpu_ctx) is False

@@ -1,0 +1,92 @@
+"""Generate the constant tables of csrc/pairing.h (BN254 optimal-ate pairing) from their
+definitions, with Python integers (run once, output pasted into pairing.h; the GPU tests compare
+the kernels with oracle/pairing.py, which derives the same values independently).
+
+Tower: Fq2 = Fq[u]/(u^2+1), Fq6 = Fq2[v]/(v^3 - xi), Fq12 = Fq6[w]/(w^2 - v), xi = 9 + u, so
+w^6 = xi.  Frobenius: (a w^k)^(q^j) = frob_j(a) w^k xi^(k (q^j - 1) / 6).
+"""
+
+Q = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+X_BN = 4965661367192848881
+
+
+def f2_mul(a, b):
+    return ((a[0] * b[0] - a[1] * b[1]) % Q, (a[0] * b[1] + a[1] * b[0]) % Q)
+
+
+def f2_pow(a, e):
+    r = (1, 0)
+    while e:
+        if e & 1:
+            r = f2_mul(r, a)
+        a = f2_mul(a, a)
+        e >>= 1
+    return r
+
+
+def mont_limbs32(x):
+    m = x * (1 << 256) % Q
+    return [(m >> (32 * i)) & 0xFFFFFFFF for i in range(8)]
+
+
+def fq_lit(x):
+    return "{" + ", ".join(f"0x{v:08x}u" for v in mont_limbs32(x)) + "}"
+
+
+def f2_lit(a):
+    return "{" + fq_lit(a[0]) + ", " + fq_lit(a[1]) + "}"
+
+
+XI = (9, 1)
+
+
+def main():
+    assert (Q - 1) % 6 == 0
+    out = []
+    for j in (1, 2, 3):
+        ks = []
+        for k in range(6):
+            g = f2_pow(XI, k * (Q ** j - 1) // 6)
+            ks.append(f2_lit(g))
+        out.append(f"// xi^(k (q^{j} - 1) / 6), k = 0..5\nconstexpr uint32_t FROB{j}[6][2][8] = {{\n    " + ",\n    ".join(ks) + "};")
+    # twist Frobenius: pi(x, y) = (conj(x) xi^((q-1)/3), conj(y) xi^((q-1)/2))
+    g13 = f2_pow(XI, (Q - 1) // 3)
+    g12 = f2_pow(XI, (Q - 1) // 2)
+    g23 = f2_pow(XI, (Q * Q - 1) // 3)
+    g22 = f2_pow(XI, (Q * Q - 1) // 2)
+    assert g23[1] == 0 and g22 == (Q - 1, 0)
+    out.append(f"constexpr uint32_t TWIST_FROB_X[2][8] = {f2_lit(g13)};")
+    out.append(f"constexpr uint32_t TWIST_FROB_Y[2][8] = {f2_lit(g12)};")
+    out.append(f"constexpr uint32_t TWIST_FROB2_X[8] = {fq_lit(g23[0])};  // xi^((q^2-1)/3) (in Fq); xi^((q^2-1)/2) = -1")
+    inv_xi = f2_pow(XI, Q * Q - 2)
+    b2 = f2_mul((3, 0), inv_xi)
+    out.append(f"constexpr uint32_t TWIST_B[2][8] = {f2_lit(b2)};  // 3 / xi")
+    hard = (Q ** 4 - Q ** 2 + 1)
+    assert hard % R == 0
+    e = hard // R
+    words = []
+    while e:
+        words.append(e & 0xFFFFFFFF)
+        e >>= 32
+    out.append(f"// (q^4 - q^2 + 1) / r, {len(words)} little-endian 32-bit words\nconstexpr uint32_t HARD_EXP_WORDS = {len(words)};\n"
+               f"constexpr uint32_t HARD_EXP[{len(words)}] = {{" + ", ".join(f"0x{w:08x}u" for w in words) + "};")
+    # the standard BN254 G2 generator (EIP-197; halo2curves' G2::generator)
+    gx = (10857046999023057135944570762232829481370756359578518086990519993285655852781,
+          11559732032986387107991004021392285783925812861821192530917403151452391805634)
+    gy = (8495653923123431417604973247489272438418190587263600148770280649306958101930,
+          4082367875863433681332203403145435568316851327593401208105741076214120093531)
+    lhs = f2_mul(gy, gy)
+    rhs = f2_mul(f2_mul(gx, gx), gx)
+    rhs = ((rhs[0] + b2[0]) % Q, (rhs[1] + b2[1]) % Q)
+    assert lhs == rhs
+    out.append(f"constexpr uint32_t G2_GEN_X[2][8] = {f2_lit(gx)};")
+    out.append(f"constexpr uint32_t G2_GEN_Y[2][8] = {f2_lit(gy)};")
+    ate = 6 * X_BN + 2
+    assert ate.bit_length() == 65
+    out.append(f"constexpr uint64_t ATE_LOOP_LOW = 0x{ate & ((1 << 64) - 1):x}ull;  // 6x + 2 below its top bit (bit 64)")
+    print("\n".join(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -183,7 +183,8 @@ class MsmWorkload:
             # all scalars < 2^64, as kzg/benches/kzg_benches.rs:16-22
             from plonky3_eon_amd.field import ints_to_limbs
 
-            vals = np.random.Generator(np.random.PCG64(3 + rank)).integers(0, 2**63, self.n, dtype=np.uint64)
+            # the full u64 range, as Fr::new(rng.random::<u64>()) (kzg_benches.rs:19)
+            vals = np.random.Generator(np.random.PCG64(3 + rank)).integers(0, 2**64, self.n, dtype=np.uint64)
             self.scalars_host = np.ascontiguousarray(ints_to_limbs([int(v) for v in vals]), dtype=np.uint64)
         else:
             self.scalars_host = synthetic_fr(self.n, 1, 3 + rank).reshape(self.n, 4)

@@ -128,7 +128,9 @@ int eon_ctx_profile_report(eon_ctx* ctx, char* buf, uint64_t len);
  * the prove is slower (no overlap of digit sorts with piece sums). */
 int eon_ctx_set_serial(eon_ctx* ctx, int serial);
 int eon_ctx_serial(const eon_ctx* ctx);
-/* ABI version; bumped on any signature change */
+/* ABI version; bumped on any signature or struct-layout change (4: the verifier pairings and their
+ * eon_g2_affine / eon_fq12 types; 3: eon_collective's all_to_all field).  Bindings must check it
+ * at load time: a binding built against an older layout would pass a shorter eon_collective. */
 uint32_t eon_abi_version(void);
 
 /* ---- TwoAdicSubgroupDft<Fr> (dft/src/traits.rs:27-249) -----------------------------------

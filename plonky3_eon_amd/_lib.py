@@ -23,6 +23,7 @@ EON_ORDER_BITREV = 1
 EON_FOURSTEP_NATURAL = 0
 EON_FOURSTEP_TRANSPOSED = 1
 EON_MSM_PRECOMPUTE = 1
+ABI_VERSION = 4  # include/eon.h eon_abi_version(): the layouts below (eon_collective, eon_g2_affine, ...)
 
 _ERRNAMES = {
     EON_E_SHAPE: "EON_E_SHAPE",
@@ -154,5 +155,8 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.eon_abi_version() != ABI_VERSION:
+        raise ImportError(f"{path} has ABI version {lib.eon_abi_version()}, this binding expects {ABI_VERSION} "
+                          f"(struct layouts differ): rebuild the library")
     _lib = lib
     return lib

@@ -470,12 +470,10 @@ int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const e
         const uint64_t mulmods = q * (uint64_t)(prog->code.size() + 1);
         ctx->prof.begin("k_air_quotient", q * (uint64_t)prog->width * 32 + q * 32, ctx->stream, mulmods);
         if (lds) {
-            static bool attr = false;
-            if (!attr) {
-                EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_air_quotient<true>),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-                attr = true;
-            }
+            // per launch: the attribute is per device, and this context's device may differ from
+            // the one another context set it on
+            EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_air_quotient<true>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
             hipLaunchKernelGGL(k_air_quotient<true>, dim3(grid), dim3(block), shmem, ctx->stream,
                                prog->d_code.as<Instr>(), (uint32_t)prog->code.size(), reinterpret_cast<const Fr*>(lde),
                                prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(),

@@ -271,7 +271,7 @@ Status dft_natural_dev(eon_ctx* ctx, const Fr* in, Fr* out, uint64_t height, uin
 
 extern "C" {
 
-uint32_t eon_abi_version(void) { return 3; }
+uint32_t eon_abi_version(void) { return 4; }
 
 int eon_ctx_create(int device_ordinal, eon_ctx** out) {
     if (!out) return EON_E_ARG;
@@ -294,30 +294,9 @@ int eon_ctx_create(int device_ordinal, eon_ctx** out) {
     (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
     bool ok = hipStreamCreateWithFlags(&c->msm_side, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->msm_side2, hipStreamNonBlocking) == hipSuccess;
-    if (const char* e = getenv("EON_MSM_SORT_CUS")) c->msm_sort_cus = (uint32_t)atoi(e);
-    hipDeviceProp_t prop{};
-    int ncu = 0;
-    if (hipGetDeviceProperties(&prop, device_ordinal) == hipSuccess) ncu = prop.multiProcessorCount;
-    if (const char* e = getenv("EON_PIECE_WAVES"))
-        if (ncu > 0) c->piece_block_cap = (uint32_t)atoi(e) * 4u * (uint32_t)ncu;
-    if (c->msm_sort_cus && ncu > 0 && c->msm_sort_cus < (uint32_t)ncu) {
-        // the sort CUs spread evenly over the CU index space (every (ncu / k)-th CU)
-        const uint32_t words = ((uint32_t)ncu + 31) / 32, stride = (uint32_t)ncu / c->msm_sort_cus;
-        std::vector<uint32_t> sort_mask(words, 0), comp_mask(words, 0);
-        for (uint32_t i = 0; i < (uint32_t)ncu; i++) {
-            const bool srt = (i % stride) == 0 && i / stride < c->msm_sort_cus;
-            (srt ? sort_mask : comp_mask)[i / 32] |= 1u << (i % 32);
-        }
-        ok = ok && hipExtStreamCreateWithCUMask(&c->msm_sort, words, sort_mask.data()) == hipSuccess &&
-             hipExtStreamCreateWithCUMask(&c->msm_comp[0], words, comp_mask.data()) == hipSuccess &&
-             hipExtStreamCreateWithCUMask(&c->msm_comp[1], words, comp_mask.data()) == hipSuccess;
-    } else {
-        c->msm_sort_cus = 0;
-        ok = ok && hipStreamCreateWithPriority(&c->msm_sort, hipStreamNonBlocking, prio_greatest) == hipSuccess;
-    }
+    ok = ok && hipStreamCreateWithPriority(&c->msm_sort, hipStreamNonBlocking, prio_greatest) == hipSuccess;
     for (hipEvent_t* e : {&c->msm_ev[0], &c->msm_ev[1], &c->msm_ev[2], &c->msm_sorted[0], &c->msm_sorted[1],
-                          &c->msm_sorted[2], &c->msm_reduced[0], &c->msm_reduced[1], &c->msm_reduced[2],
-                          &c->msm_pdone[0], &c->msm_pdone[1], &c->msm_pdone[2], &c->msm_pdone[3]})
+                          &c->msm_sorted[2], &c->msm_reduced[0], &c->msm_reduced[1], &c->msm_reduced[2]})
         ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         (void)hipStreamDestroy(c->own_stream);
@@ -326,9 +305,12 @@ int eon_ctx_create(int device_ordinal, eon_ctx** out) {
     }
     if (const char* e = getenv("EON_SERIAL")) c->serial = e[0] == '1';
     if (const char* e = getenv("EON_NTT_MAX_STAGES")) c->ntt_max_stages = (uint32_t)atoi(e);
+#ifdef EON_TUNING_KNOBS
+    // NTT plan overrides for tuning builds only (_build.build_variant(..., ["EON_TUNING_KNOBS"]))
     if (const char* e = getenv("EON_NTT_TPB")) c->ntt_tpb = (uint32_t)atoi(e);
     if (const char* e = getenv("EON_NTT_TILE")) c->ntt_log_tile = (uint32_t)atoi(e);
     if (const char* e = getenv("EON_NTT_LOG_CB")) c->ntt_log_cb = atoi(e) > 3 ? 3 : atoi(e);
+#endif
     *out = c;
     return EON_OK;
 }
@@ -340,8 +322,6 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->msm_side);
     (void)hipStreamSynchronize(ctx->msm_side2);
     (void)hipStreamSynchronize(ctx->msm_sort);
-    for (hipStream_t st : ctx->msm_comp)
-        if (st) (void)hipStreamSynchronize(st);
     ctx->tw_fwd.release();
     ctx->tw_inv.release();
     for (auto& kv : ctx->tables) kv.second.release();
@@ -353,7 +333,6 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     ctx->msm.release();
     ctx->msm_b.release();
     ctx->msm_c.release();
-    ctx->msm_d.release();
     for (auto& sb : ctx->sorted_cache) sb.release();
     ctx->sorted_cache.clear();
     ctx->sel_tab.release();
@@ -369,11 +348,8 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     (void)hipStreamDestroy(ctx->msm_side);
     (void)hipStreamDestroy(ctx->msm_side2);
     (void)hipStreamDestroy(ctx->msm_sort);
-    for (hipStream_t st : ctx->msm_comp)
-        if (st) (void)hipStreamDestroy(st);
     for (hipEvent_t e : {ctx->msm_ev[0], ctx->msm_ev[1], ctx->msm_ev[2], ctx->msm_sorted[0], ctx->msm_sorted[1],
-                         ctx->msm_sorted[2], ctx->msm_reduced[0], ctx->msm_reduced[1], ctx->msm_reduced[2],
-                         ctx->msm_pdone[0], ctx->msm_pdone[1], ctx->msm_pdone[2], ctx->msm_pdone[3]})
+                         ctx->msm_sorted[2], ctx->msm_reduced[0], ctx->msm_reduced[1], ctx->msm_reduced[2]})
         (void)hipEventDestroy(e);
     delete ctx;
 }

@@ -63,14 +63,14 @@ struct SortedBufs {
 
 struct MsmWork {
     DevBuf keys, vals, count, off2, off3, owner, piece_sums, piece_sums2, bucket_sums, red_a, red_b,
-        temp, results, levels, piece_raw, stat;
+        temp, results, piece_raw, stat;
     SortedBufs sorted;
     uint32_t* host_counts = nullptr;  // pinned read-back slots
     void release() {
         if (host_counts) (void)hipHostFree(host_counts);
         host_counts = nullptr;
         for (DevBuf* b : {&keys, &vals, &count, &off2, &off3, &owner, &piece_sums, &piece_sums2,
-                          &bucket_sums, &red_a, &red_b, &temp, &levels, &results, &piece_raw, &stat})
+                          &bucket_sums, &red_a, &red_b, &temp, &results, &piece_raw, &stat})
             b->release();
         sorted.release();
     }
@@ -126,21 +126,12 @@ struct eon_ctx {
 
     // MSM pipeline: workspaces msm / msm_b / msm_c for batches k % 3; piece sums + reductions on
     // `stream` / msm_side, digit sorts on the high-priority msm_sort (msm.hip: msm_run_columns)
-    eon::MsmWork msm, msm_b, msm_c, msm_d;
+    eon::MsmWork msm, msm_b, msm_c;
     hipStream_t msm_side = nullptr, msm_sort = nullptr;
     // third compute stream of the prepared path (jobs round-robin over stream / msm_side / msm_side2)
     hipStream_t msm_side2 = nullptr;
-    // EON_MSM_SORT_CUS > 0: piece sums on msm_comp[2] (CU-masked to all but those CUs), sorts
-    // on msm_sort masked to them -- a full piece-sum launch leaves no room for a sort workgroup
-    uint32_t msm_sort_cus = 0;
-    // EON_PIECE_WAVES (1..4): cap k_piece_sum's grid at that many one-wave blocks per SIMD
-    // (0 = one thread per chunk, no cap)
-    uint32_t piece_block_cap = 0;
-    hipStream_t msm_comp[2] = {nullptr, nullptr};
     hipEvent_t msm_ev[3] = {nullptr, nullptr, nullptr};
     hipEvent_t msm_sorted[3] = {nullptr, nullptr, nullptr}, msm_reduced[3] = {nullptr, nullptr, nullptr};
-    // prepared path: "piece sums of job j done" (jobs chained through them, round-robin)
-    hipEvent_t msm_pdone[4] = {nullptr, nullptr, nullptr, nullptr};
 
     // sorted-digit buffers of destroyed eon_msm_scalars, reused by the next prepared MSM (the
     // prover commits matrices of the same shape every proof: keeping ~22 GB resident beats a

@@ -395,6 +395,36 @@ EON_HD F29 mul29_sum2(const F29& a, const F29& b, const F29& c, const F29& d) {
     return r;
 }
 
+// ---- compile-time overflow guard for the unmasked Montgomery multipliers --------------------------
+// Worst case of every 64-bit column accumulator of mul29 / sqr29 / mul29_sum2: every operand limb
+// at its contract maximum (`prod_max` = the operand products one column position can add), every
+// unmasked multiplier m_k at 2^32 - 1 (masked ones at 2^29 - 1), the actual limbs of the modulus,
+// and the carry in from the previous column at its own worst case.
+template <class M>
+constexpr bool columns_fit_u64(unsigned __int128 prod_max, int unmasked) {
+    unsigned __int128 carry = 0;
+    for (int k = 0; k < 17; k++) {
+        unsigned __int128 col = carry;
+        for (int i = 0; i < 9; i++) {
+            const int j = k - i;
+            if (j < 0 || j > 8) continue;
+            col += prod_max;
+            const unsigned __int128 m_max = i < unmasked ? 0xffffffffu : M29;
+            col += m_max * R29<M>::P[j];  // reduction products m_i p_j
+        }
+        if (col >= ((unsigned __int128)1 << 64)) return false;
+        carry = col >> 29;
+    }
+    return true;
+}
+constexpr unsigned __int128 L29 = M29, L30 = (1u << 30) - 1, L31 = (1u << 31) - 1;
+// mul29 / sqr29 (U = 8 unmasked multipliers), operand limbs < 2^30 (add29_lazy outputs):
+// 0.876 (Fq) / 0.93 (Fr) of 2^64
+static_assert(columns_fit_u64<FqP>(L30 * L30, 8), "mul29<Fq> column overflow");
+static_assert(columns_fit_u64<FrP>(L30 * L30, 8), "mul29<Fr> column overflow");
+// mul29_sum2: a, c, d normalised, b < 2^31 (a sub29_lazy output), 6 unmasked multipliers
+static_assert(columns_fit_u64<FqP>(L29 * L31 + L29 * L29, 6), "mul29_sum2<Fq> column overflow");
+
 // Same with the product and reduction terms of a column in two accumulators (shorter dependency
 // chains), merged once per column.
 template <class M>

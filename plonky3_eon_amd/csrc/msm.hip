@@ -14,17 +14,17 @@
 //   3. k_bucket_start   bucket boundaries in the sorted pairs.
 //   4. pieces           a piece is the part of a bucket inside one chunk (2^log_chunk aligned
 //                       sorted pairs); exclusive scan of the per-bucket piece counts.
-//   5. k_piece_sum      one thread per chunk of sorted pairs (every lane does the same number of
-//                       XYZZ mixed additions of affine bases), flushing a partial per piece.
+//   5. k_piece_sum29    one thread per chunk of sorted pairs (every lane does the same number of
+//                       XYZZ mixed additions of affine bases, radix 2^29), flushing a partial per
+//                       piece.
 //   6. k_partial_combine levels of <= PIECE-way sums until each bucket holds one partial
 //                       (log-depth under any skew, e.g. all-equal scalars), k_bucket_final.
-//   7. k_seg_level /    sum_d d * B_d per group as a recursive weighted sum: with T_j / U_j the
-//      k_tree_sum /     plain / locally weighted sums of segment j (SEG buckets, by running sums),
-//      k_seg_final      W(S) = SEG * W(T) + sum_j U_j; the U sums by LDS trees, the SEG powers by
-//                       doublings in a per-group Horner step (~2 additions per bucket).  Batches
-//                       with < 64 groups (a single MSM) use the shorter-chain k_segment_sum
-//                       (running sums + lo * run) + one tree instead: there latency, not
-//                       additions, sets the time.
+//   7. k_bucket_reduce29 sum_d d * B_d per group: T_j / U_j the plain / locally weighted sums of
+//      (k_seg_level) /  segment j (SEG buckets, by running sums), then
+//      k_group_finish   sum_j U_j + SEG sum_j j T_j + sum_j T_j per group (deferred to one launch
+//                       per call).  Batches with < 64 groups (a single MSM) use the shorter-chain
+//                       k_segment_sum (running sums + lo * run) + k_tree_sum instead: there
+//                       latency, not additions, sets the time.
 //   8. k_window_horner  (per-window buckets only) sum_w 2^(c*w) G_w per MSM; batched affine.
 //
 // Batched mode (eon_msm_g1_columns*): one pipeline run handles many MSMs at once -- the columns
@@ -54,17 +54,14 @@ struct eon_msm_bases {
     bool precomputed = false;
     uint32_t c = 0, windows = 0;
     DevBuf table;  // precomputed: n * windows affine points, entry i * windows + w = 2^(c*w) P_i
-    // radix-2^29 piece sums (EON_MSM_R32=1 keeps radix-2^32 bases and k_piece_sum): the piece
-    // sums read 29-Montgomery coordinates from `table` (precomputed) or `points29`; `points` stays
-    // in the ABI form (the KZG opening bases are derived from it)
-    bool r29 = false;
+    // the piece sums read 29-Montgomery coordinates from `table` (precomputed) or `points29`;
+    // `points` stays in the ABI form (the KZG opening bases are derived from it)
     DevBuf points29;
     // 3 * table (29-form affine, same layout), built on first use by the KZG opening bases'
     // radix-4 fixed-base multiplications (bases_table3_29)
     DevBuf table3;
     const G1Affine* piece_source() const {
-        if (precomputed) return table.as<G1Affine>();
-        return r29 ? points29.as<G1Affine>() : points.as<G1Affine>();
+        return precomputed ? table.as<G1Affine>() : points29.as<G1Affine>();
     }
 };
 
@@ -76,6 +73,7 @@ constexpr uint32_t LOG_CHUNK_MIN = 4, LOG_CHUNK_MAX = 7;
 constexpr uint32_t PIECE = 32;   // partials per combine step
 constexpr uint32_t SEG = 8;     // buckets per reduction segment
 constexpr uint32_t TREE = 256;  // points per tree-reduction block
+constexpr uint32_t FINISH_THREADS = 256;  // threads per group of k_group_finish / k_group_finish29
 
 __device__ __forceinline__ uint32_t window_bits(const uint32_t* s, uint32_t pos, uint32_t c) {
     // bits [pos, pos + c) of the 256-bit canonical scalar s (little-endian u32 limbs), c <= 24
@@ -223,44 +221,14 @@ __global__ void k_chunk_count(const uint32_t* start, uint32_t nb, uint32_t log_c
     if ((threadIdx.x & 63) == 0 && v > 1 && v > __atomic_load_n(stat, __ATOMIC_RELAXED)) atomicMax(stat, v);
 }
 
-// Thread t sums the sorted pairs [t 2^log_chunk, (t+1) 2^log_chunk) (nonzero digits only): one
-// partial per bucket run, stored at piece_off[b] + t - (start[b] >> log_chunk).
 #ifndef EON_PIECE_MINWAVES
 #define EON_PIECE_MINWAVES 4
 #endif
-__global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum(const uint32_t* keys, const uint32_t* vals, const uint32_t* start,
-                            const uint32_t* piece_off, uint32_t n_pairs, uint32_t log_chunk,
-                            uint32_t c, uint32_t groups, uint32_t nb, const G1Affine* pts,
-                            G1Xyzz* piece_sums) {
-    // grid-stride over chunks: a capped grid (EON_PIECE_WAVES) leaves wave slots for the
-    // concurrent digit sort of the next batch
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; ((uint64_t)t << log_chunk) < n_pairs;
-         t += gridDim.x * blockDim.x) {
-    const uint32_t e0 = t << log_chunk;
-    const uint32_t e1 = min(e0 + (1u << log_chunk), n_pairs);
-    uint32_t b = keys[e0];
-    G1Xyzz acc = xyzz_inf();
-    for (uint32_t e = e0; e < e1; e++) {
-        const uint32_t k = keys[e];
-        if (k != b) {
-            const uint32_t bb = bucket_of(b, c, groups, nb);
-            st_xyzz(piece_sums + piece_off[bb] + t - (start[bb] >> log_chunk), acc);
-            acc = xyzz_inf();
-            b = k;
-        }
-        const uint32_t v = vals[e];
-        G1Affine a = ld_affine(pts + (v & 0x7fffffffu));
-        if (v >> 31) a = affine_neg(a);
-        acc = xyzz_add_affine(acc, a);
-    }
-    const uint32_t bb = bucket_of(b, c, groups, nb);
-    st_xyzz(piece_sums + piece_off[bb] + t - (start[bb] >> log_chunk), acc);
-    }
-}
 
-// Radix-2^29 form of k_piece_sum (ec29.h): the same chunk walk, with the XYZZ accumulator in
-// 29-bit limbs (lazy bounds, no carry captures in the products) and the bases read in
-// 29-Montgomery form (k_table_to29).  Each bucket run stores its raw accumulator (144 bytes,
+// Thread t sums the sorted pairs [t 2^log_chunk, (t+1) 2^log_chunk) (nonzero digits only): one
+// partial per bucket run, stored at piece_off[b] + t - (start[b] >> log_chunk).  The XYZZ
+// accumulator is in 29-bit limbs (ec29.h: lazy bounds, no carry captures in the products) and the
+// bases are read in 29-Montgomery form (k_table_to29).  Each bucket run stores its raw accumulator (144 bytes,
 // ZZ = 0 for the identity); k_raw29_to_xyzz converts the pieces for the combine levels.
 //
 // The additions are unchecked (madd29_unchecked): x(acc) == x(A) -- a duplicate base, or a base
@@ -635,25 +603,6 @@ __global__ void __launch_bounds__(64) k_segment_reduce29(const G1Raw29* pieces, 
     st_xyzz(seg_out + t, x29_to_xyzz(acc, acc_inf));
 }
 
-constexpr uint32_t MAX_SEG_LEVELS = 24;
-struct SegLogs {
-    uint8_t v[MAX_SEG_LEVELS];
-};
-
-// out[g] = usum[0] + s_0 (usum[1] + s_1 (... + s_{m-2} usum[m-1])) + t_final[g], s_l = 2^logs[l]
-// (usum[l] = sum of level l's U over group g, stored at usum[l * groups + g])
-__global__ void k_seg_final(const G1Xyzz* usum, uint32_t m, SegLogs logs, uint32_t groups,
-                            const G1Xyzz* t_final, G1Xyzz* out) {
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= groups) return;
-    G1Xyzz acc = ld_xyzz(usum + (uint64_t)(m - 1) * groups + g);
-    for (int l = (int)m - 2; l >= 0; l--) {
-        for (uint32_t d = 0; d < logs.v[l]; d++) acc = xyzz_dbl(acc);
-        acc = xyzz_add(acc, ld_xyzz(usum + (uint64_t)l * groups + g));
-    }
-    st_xyzz(out + g, xyzz_add(acc, ld_xyzz(t_final + g)));
-}
-
 // out[g * gridDim.x + blk] = sum of in[g * n + blk * TREE .. + TREE)
 __global__ void __launch_bounds__(TREE) k_tree_sum(const G1Xyzz* in, uint32_t n, G1Xyzz* out) {
     __shared__ G1Xyzz sh[TREE];
@@ -763,20 +712,11 @@ static inline unsigned blocks_for(uint64_t n, unsigned bs) { return (unsigned)((
 
 hipError_t launch_batch_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out, hipStream_t st) {
     if (m == 0) return hipSuccess;
-    // one inversion (~380 dependent products) per CHUNK points: a small chunk spends more
-    // products, a large one leaves the SIMDs idle behind the latency of too few waves
-    static const uint32_t chunk = [] {
-        const char* e = getenv("EON_B2A_CHUNK");
-        const int v = e ? atoi(e) : (int)BATCH;
-        return (uint32_t)(v == 8 || v == 16 || v == 64 ? v : 32);
-    }();
+    // one inversion (~380 dependent products) per BATCH points: a smaller chunk spends more
+    // products, a larger one leaves the SIMDs idle behind the latency of too few waves
     const unsigned threads = 128;
-    switch (chunk) {
-        case 8: hipLaunchKernelGGL(k_batch_to_affine<8>, dim3(blocks_for((m + 7) / 8, threads)), dim3(threads), 0, st, in, m, out); break;
-        case 16: hipLaunchKernelGGL(k_batch_to_affine<16>, dim3(blocks_for((m + 15) / 16, threads)), dim3(threads), 0, st, in, m, out); break;
-        case 64: hipLaunchKernelGGL(k_batch_to_affine<64>, dim3(blocks_for((m + 63) / 64, threads)), dim3(threads), 0, st, in, m, out); break;
-        default: hipLaunchKernelGGL(k_batch_to_affine<32>, dim3(blocks_for((m + 31) / 32, threads)), dim3(threads), 0, st, in, m, out); break;
-    }
+    hipLaunchKernelGGL(k_batch_to_affine<BATCH>, dim3(blocks_for((m + BATCH - 1) / BATCH, threads)), dim3(threads), 0,
+                       st, in, m, out);
     return hipGetLastError();
 }
 
@@ -814,13 +754,7 @@ Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32
         if (e != hipSuccess) return fail(Status::err(EON_E_DEVICE, hipGetErrorString(e)));
     }
     b->precomputed = (flags & EON_MSM_PRECOMPUTE) != 0 && n > 0;
-    // EON_MSM_C (A/B knob): the window of precomputed (fixed-base) tables
-    static const uint32_t env_c = [] {
-        const char* e = getenv("EON_MSM_C");
-        const int v = e ? atoi(e) : 0;
-        return (uint32_t)(v >= 8 && v <= 20 ? v : 0);
-    }();
-    b->c = force_c ? force_c : (env_c && b->precomputed ? env_c : choose_c(n ? n : 1, b->precomputed));
+    b->c = force_c ? force_c : choose_c(n ? n : 1, b->precomputed);
     b->windows = (255 + b->c - 1) / b->c;
     if (b->precomputed) {
         const uint64_t m = n * b->windows;
@@ -840,8 +774,7 @@ Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32
         }
         if (e != hipSuccess) return fail(Status::err(EON_E_DEVICE, hipGetErrorString(e)));
     }
-    b->r29 = getenv("EON_MSM_R32") == nullptr;
-    if (b->r29 && n) {
+    if (n) {
         const uint64_t m = b->precomputed ? n * b->windows : n;
         if (!b->precomputed) {
             e = b->points29.ensure(n * sizeof(G1Affine));
@@ -1012,9 +945,8 @@ static SortedRef sorted_ref(const SortedBufs& s) {
 // pieces per bucket -- with few groups and several pieces per bucket (a single 2^20 MSM: ~4.5)
 // the one-thread-per-segment chain is longer than combine + bucket-final + k_segment_sum
 // (3.23 vs 3.00 ms for the 2^20 MSM)
-static bool fused_reduce(const eon_msm_bases* b, const Batch& bt) {
-    static const bool off = getenv("EON_MSM_UNFUSED") != nullptr;
-    return !off && b->r29 && bt.levels <= 1 && bt.B >= SEG &&
+static bool fused_reduce(const Batch& bt) {
+    return bt.levels <= 1 && bt.B >= SEG &&
            (bt.groups >= 64 || (uint64_t)bt.n_pieces <= 2ull * bt.nb);
 }
 
@@ -1029,7 +961,7 @@ static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt
     EON_HIP(wk.off3.ensure((bt.nb + 1) * 4ull));
     EON_HIP(wk.count.ensure((bt.nb + 1) * 4ull));
     EON_HIP(wk.temp.ensure(bt.scan_bytes));
-    if (b->r29) EON_HIP(wk.piece_raw.ensure(bt.max_pieces * sizeof(G1Raw29)));
+    EON_HIP(wk.piece_raw.ensure(bt.max_pieces * sizeof(G1Raw29)));
     if (!wk.host_counts) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&wk.host_counts), 64));
     const G1Affine* pts = b->piece_source();
     // algorithmic bytes: n (64 + 32) B per MSM of n terms -- each
@@ -1040,16 +972,12 @@ static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt
     const uint64_t msm_n = bt.E / ((uint64_t)bt.W * bt.cols);
     ctx->prof.begin("k_piece_sum", (uint64_t)bt.cols * msm_n * 96, st, (uint64_t)bt.n_pairs * 10,
                     (uint64_t)bt.n_pairs * 72 + (uint64_t)bt.n_pieces * 144);
-    uint32_t blocks = blocks_for(((uint64_t)bt.n_pairs + (1u << bt.log_chunk) - 1) >> bt.log_chunk, 64);
-    if (ctx->piece_block_cap) blocks = std::min(blocks, ctx->piece_block_cap);
-    if (bt.n_pairs && b->r29)
+    const uint32_t blocks = blocks_for(((uint64_t)bt.n_pairs + (1u << bt.log_chunk) - 1) >> bt.log_chunk, 64);
+    if (bt.n_pairs)
         hipLaunchKernelGGL(k_piece_sum29, dim3(blocks), dim3(64), 0, st, sr.keys, sr.vals, sr.start, sr.piece_off,
                            bt.n_pairs, bt.log_chunk, bt.c, bt.groups, bt.nb, pts, wk.piece_raw.as<G1Raw29>());
-    else if (bt.n_pairs)
-        hipLaunchKernelGGL(k_piece_sum, dim3(blocks), dim3(64), 0, st, sr.keys, sr.vals, sr.start, sr.piece_off,
-                           bt.n_pairs, bt.log_chunk, bt.c, bt.groups, bt.nb, pts, wk.piece_sums.as<G1Xyzz>());
     ctx->prof.end(st);
-    if (bt.n_pieces && b->r29 && !fused_reduce(b, bt))
+    if (bt.n_pieces && !fused_reduce(bt))
         hipLaunchKernelGGL(k_raw29_to_xyzz, dim3(blocks_for(bt.n_pieces, 128)), dim3(128), 0, st,
                            wk.piece_raw.as<G1Raw29>(), bt.n_pieces, wk.piece_sums.as<G1Xyzz>());
     EON_HIP(hipGetLastError());
@@ -1112,11 +1040,6 @@ struct DeferredFinish {
     std::vector<std::pair<uint64_t, uint64_t>> rows;  // deferred [row0, row0 + n)
 };
 
-static bool defer_finish_enabled() {
-    static const bool off = getenv("EON_MSM_FINISH_PER_BATCH") != nullptr;
-    return !off;
-}
-
 // k_group_finish over the deferred rows (merged into maximal runs) on `st`
 static hipError_t launch_group_finish29(const G1Raw29* T, const G1Raw29* U, uint32_t nseg, uint32_t lsg,
                                         G1Xyzz* out, uint32_t groups, hipStream_t st);
@@ -1144,7 +1067,7 @@ static Status run_deferred_finish(eon_ctx* ctx, DeferredFinish& df, hipStream_t 
 static Status prepare_deferred(eon_ctx* ctx, const MsmLayout& L, uint64_t rows, G1Xyzz* out_base,
                                DeferredFinish& df) {
     df = DeferredFinish{};
-    if (!defer_finish_enabled() || !L.precomputed) return Status::ok();
+    if (!L.precomputed) return Status::ok();
     const uint32_t B = 1u << (L.c - 1);
     if (B < SEG) return Status::ok();
     df.nseg = B / SEG;
@@ -1164,8 +1087,7 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
                            MsmWork& wk, hipStream_t st, bool fused, DeferredFinish* df = nullptr) {
     Profiler* prof = &ctx->prof;
     const uint32_t nb = bt.nb, groups = bt.groups, B = bt.B;
-    if (df && df->T && fused && groups >= 64 && B >= SEG && L.precomputed &&
-        getenv("EON_MSM_SEG_LEVELS") == nullptr) {
+    if (df && df->T && fused && groups >= 64 && B >= SEG && L.precomputed) {
         // first level only; the finish runs once per call (run_deferred_finish)
         const uint64_t row0 = (uint64_t)(bt.out - df->out_base);
         prof->begin("bucket_reduce", (uint64_t)nb * 128 + (uint64_t)nb / SEG * 256, st);
@@ -1207,84 +1129,23 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
         hipLaunchKernelGGL(k_bucket_final, dim3(blocks_for(nb, 256)), dim3(256), 0, st, off_cur, B, groups,
                            part_cur, wk.bucket_sums.as<G1Xyzz>());
     if (groups < 64) return reduce_segments(ctx, L, bt, sr, wk, st, fused);
-    // sum_d d * B_d = W(S) + T(S) per group (bucket b holds digit b + 1), level by level
-    G1Xyzz* t_buf[2] = {wk.piece_sums.as<G1Xyzz>(), wk.piece_sums.as<G1Xyzz>() + (uint64_t)groups * (B / 2)};
+    // sum_d d * B_d per group (bucket b holds digit b + 1): segment sums T, U of SEG buckets
+    // (k_bucket_reduce29 from the raw pieces, or k_seg_level from bucket sums), then k_group_finish
+    G1Xyzz* T = wk.piece_sums.as<G1Xyzz>();
     G1Xyzz* u_buf = wk.piece_sums2.as<G1Xyzz>();
-    const uint32_t tree_max = (uint32_t)((uint64_t)groups * ((B / 2 + TREE - 1) / TREE));
-    EON_HIP(wk.red_a.ensure((uint64_t)tree_max * sizeof(G1Xyzz)));
-    EON_HIP(wk.red_b.ensure((uint64_t)tree_max * sizeof(G1Xyzz)));
-    EON_HIP(wk.levels.ensure((uint64_t)MAX_SEG_LEVELS * groups * sizeof(G1Xyzz)));
-    G1Xyzz* usum = wk.levels.as<G1Xyzz>();
-    SegLogs logs{};
-    const G1Xyzz* X = wk.bucket_sums.as<G1Xyzz>();
-    uint32_t Lb = B, m = 0;
-    // profiled as one span: the weighted bucket sum (k_bucket_reduce29 or k_seg_level, then
-    // k_group_finish, or the level chain)
+    EON_HIP(wk.red_a.ensure((uint64_t)groups * sizeof(G1Xyzz)));
     prof->begin("bucket_reduce", (uint64_t)nb * 128 + (uint64_t)nb / SEG * 256, st);
-    // EON_MSM_SEG_LEVELS=1: the level-by-level chain below instead of k_group_finish
-    static const bool seg_levels = getenv("EON_MSM_SEG_LEVELS") != nullptr;
-    if (!seg_levels) {
-        const uint32_t seg = B < SEG ? B : SEG;
-        const uint32_t nseg = B / seg;
-        G1Xyzz* T = t_buf[0];
-        if (fused)
-            hipLaunchKernelGGL(k_bucket_reduce29<G1Xyzz>, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0,
-                               st, wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, seg, groups, T, u_buf);
-        else
-            hipLaunchKernelGGL(k_seg_level, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st, X, B,
-                               seg, groups, T, u_buf);
-        G1Xyzz* per_group = wk.red_a.as<G1Xyzz>();
-        // EON_MSM_GF_THREADS (256 / 512 / 1024): threads per group of the latency-bound finish
-        static const uint32_t gf = [] {
-            const char* e = getenv("EON_MSM_GF_THREADS");
-            const int v = e ? atoi(e) : 256;
-            return (uint32_t)(v == 512 || v == 1024 ? v : 256);
-        }();
-        const uint32_t lsg = 31 - __builtin_clz(seg);
-        if (gf == 1024)
-            hipLaunchKernelGGL(k_group_finish<1024>, dim3(groups), dim3(1024), 0, st, T, u_buf, nseg, lsg, per_group);
-        else if (gf == 512)
-            hipLaunchKernelGGL(k_group_finish<512>, dim3(groups), dim3(512), 0, st, T, u_buf, nseg, lsg, per_group);
-        else
-            hipLaunchKernelGGL(k_group_finish<256>, dim3(groups), dim3(256), 0, st, T, u_buf, nseg, lsg, per_group);
-        prof->end(st);
-        EON_HIP(hipGetLastError());
-        return write_columns(L, bt, per_group, st);
-    }
-    while (Lb > 1) {
-        const uint32_t seg = Lb < SEG ? Lb : SEG;
-        const uint32_t nseg = Lb / seg;
-        G1Xyzz* T = t_buf[m & 1];
-        if (fused && m == 0)
-            hipLaunchKernelGGL(k_bucket_reduce29<G1Xyzz>, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0,
-                               st, wk.piece_raw.as<G1Raw29>(), sr.piece_off, Lb, seg, groups, T, u_buf);
-        else
-            hipLaunchKernelGGL(k_seg_level, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
-                               X, Lb, seg, groups, T, u_buf);
-        // usum[m] = sum over the group's nseg U values
-        const G1Xyzz* cur = u_buf;
-        uint32_t len = nseg;
-        G1Xyzz* bufs[2] = {wk.red_a.as<G1Xyzz>(), wk.red_b.as<G1Xyzz>()};
-        int which = 0;
-        while (len > 1) {
-            const uint32_t blk = (len + TREE - 1) / TREE;
-            G1Xyzz* dst = blk == 1 ? usum + (uint64_t)m * groups : bufs[which];
-            hipLaunchKernelGGL(k_tree_sum, dim3(blk, groups), dim3(TREE), 0, st, cur, len, dst);
-            cur = dst;
-            which ^= 1;
-            len = blk;
-        }
-        if (nseg == 1)
-            EON_HIP(hipMemcpyAsync(usum + (uint64_t)m * groups, u_buf, groups * sizeof(G1Xyzz),
-                                   hipMemcpyDeviceToDevice, st));
-        logs.v[m] = (uint8_t)(31 - __builtin_clz(seg));
-        X = T;
-        Lb = nseg;
-        m++;
-    }
+    const uint32_t seg = B < SEG ? B : SEG;
+    const uint32_t nseg = B / seg;
+    if (fused)
+        hipLaunchKernelGGL(k_bucket_reduce29<G1Xyzz>, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
+                           wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, seg, groups, T, u_buf);
+    else
+        hipLaunchKernelGGL(k_seg_level, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
+                           wk.bucket_sums.as<G1Xyzz>(), B, seg, groups, T, u_buf);
     G1Xyzz* per_group = wk.red_a.as<G1Xyzz>();
-    hipLaunchKernelGGL(k_seg_final, dim3(blocks_for(groups, 64)), dim3(64), 0, st, usum, m, logs, groups,
-                       X, per_group);
+    hipLaunchKernelGGL(k_group_finish<FINISH_THREADS>, dim3(groups), dim3(FINISH_THREADS), 0, st, T, u_buf, nseg,
+                       31 - __builtin_clz(seg), per_group);
     prof->end(st);
     EON_HIP(hipGetLastError());
     return write_columns(L, bt, per_group, st);
@@ -1292,16 +1153,8 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
 
 static hipError_t launch_group_finish29(const G1Raw29* T, const G1Raw29* U, uint32_t nseg, uint32_t lsg,
                                         G1Xyzz* out, uint32_t groups, hipStream_t st) {
-    // EON_MSM_GF29_THREADS (128 / 256): threads per column of the call-wide finish
-    static const uint32_t gf = [] {
-        const char* e = getenv("EON_MSM_GF29_THREADS");
-        const int v = e ? atoi(e) : 256;
-        return (uint32_t)(v == 128 ? v : 256);
-    }();
-    if (gf == 128)
-        hipLaunchKernelGGL(k_group_finish29<128>, dim3(groups), dim3(128), 0, st, T, U, nseg, lsg, out);
-    else
-        hipLaunchKernelGGL(k_group_finish29<256>, dim3(groups), dim3(256), 0, st, T, U, nseg, lsg, out);
+    hipLaunchKernelGGL(k_group_finish29<FINISH_THREADS>, dim3(groups), dim3(FINISH_THREADS), 0, st, T, U, nseg, lsg,
+                       out);
     return hipGetLastError();
 }
 
@@ -1359,7 +1212,7 @@ __global__ void k_triple29(const G1Affine* tab, uint64_t m, G1Xyzz* out) {
 
 const G1Affine* bases_table3_29(const eon_msm_bases* cb, hipStream_t st) {
     eon_msm_bases* b = const_cast<eon_msm_bases*>(cb);  // a cache filled once
-    if (!b->precomputed || !b->r29 || b->n == 0) return nullptr;
+    if (!b->precomputed || b->n == 0) return nullptr;
     if (b->table3.p) return b->table3.as<G1Affine>();
     const uint64_t m = b->n * b->windows;
     DevBuf tmp;
@@ -1384,7 +1237,7 @@ const G1Affine* bases_table3_29(const eon_msm_bases* cb, hipStream_t st) {
 }
 
 const G1Affine* bases_table29(const eon_msm_bases* b) {
-    return b->precomputed && b->r29 ? b->table.as<G1Affine>() : nullptr;
+    return b->precomputed ? b->table.as<G1Affine>() : nullptr;
 }
 
 uint32_t bases_windows(const eon_msm_bases* b) { return b->windows; }
@@ -1397,7 +1250,6 @@ Status bases_alloc_table(eon_ctx* ctx, uint64_t n, uint32_t c, eon_msm_bases** o
     b->precomputed = true;
     b->c = c;
     b->windows = (255 + c - 1) / c;
-    b->r29 = getenv("EON_MSM_R32") == nullptr;
     if (b->points.ensure(n * sizeof(G1Affine)) != hipSuccess ||
         b->table.ensure(n * b->windows * sizeof(G1Affine)) != hipSuccess) {
         bases_free(b);
@@ -1413,11 +1265,9 @@ Status bases_seal_table(eon_msm_bases* b, hipStream_t st) {
     // points = the w = 0 entries (radix-2^32 ABI form), then the table to 29-Montgomery
     EON_HIP(hipMemcpy2DAsync(b->points.p, sizeof(G1Affine), b->table.p, sizeof(G1Affine) * b->windows,
                              sizeof(G1Affine), b->n, hipMemcpyDeviceToDevice, st));
-    if (b->r29) {
-        const uint64_t m = b->n * b->windows;
-        hipLaunchKernelGGL(k_table_to29, dim3(blocks_for(m, 256)), dim3(256), 0, st, b->table.as<G1Affine>(), m);
-        EON_HIP(hipGetLastError());
-    }
+    const uint64_t m = b->n * b->windows;
+    hipLaunchKernelGGL(k_table_to29, dim3(blocks_for(m, 256)), dim3(256), 0, st, b->table.as<G1Affine>(), m);
+    EON_HIP(hipGetLastError());
     return Status::ok();
 }
 
@@ -1609,27 +1459,6 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
     if (width == 0) return Status::ok();
     if (n == 0) return out_host ? identity_columns(width, out_host) : Status::ok();
     const MsmLayout L = msm_layout(b, n, width);
-    // EON_MSM_SORT_FIRST=1 with kept digits: every batch sorted first (each sort alone on the
-    // device), then the prepared pipeline -- measured ~5 ms slower per trace commit than the
-    // streaming pipeline below, which keeps the sorted buffers as it goes.
-    static const bool sort_first = getenv("EON_MSM_SORT_FIRST") != nullptr;
-    if (keep && sort_first) {
-        keep->batches = make_batches(scalars, width, L.cpb);
-        keep->sorted.resize(keep->batches.size());
-        for (auto& sb : keep->sorted) {
-            if (ctx->sorted_cache.empty()) break;
-            sb = std::move(ctx->sorted_cache.back());
-            ctx->sorted_cache.back() = SortedBufs{};
-            ctx->sorted_cache.pop_back();
-        }
-        for (size_t k = 0; k < keep->batches.size(); k++) {
-            EON_TRY(batch_sort(ctx, L, n, width, keep->batches[k], ctx->msm, keep->sorted[k], ctx->stream));
-            keep->batches[k].scalars = nullptr;
-        }
-        std::vector<G1Affine> tmp(out_host ? 0 : width);
-        const eon_msm_bases* bl[1] = {b};
-        return msm_run_prepared(ctx, bl, 1, keep, out_host ? out_host : tmp.data());
-    }
     // every batch leaves XYZZ results; one batched XYZZ -> affine conversion at the end (the
     // conversion is an inversion-latency-bound launch, so it is paid once per call)
     EON_HIP(ctx->msm.results.ensure(width * (sizeof(G1Affine) + sizeof(G1Xyzz))));
@@ -1672,9 +1501,7 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
     // alternating between the context stream and the side stream.  Three workspaces (batch k uses
     // k % 3): sort(k+1) only waits for reduce(k-2).  Events order sort(k) after reduce(k - 3)
     // and pieces(k) after sort(k).
-    const bool masked = ctx->msm_sort_cus > 0;
-    hipStream_t comp[2] = {ctx->side(masked ? ctx->msm_comp[0] : ctx->stream),
-                           ctx->side(masked ? ctx->msm_comp[1] : ctx->msm_side)};
+    hipStream_t comp[2] = {ctx->stream, ctx->side(ctx->msm_side)};
     hipStream_t sort_st = ctx->side(ctx->msm_sort);
     MsmWork* wks[3] = {&ctx->msm, &ctx->msm_b, &ctx->msm_c};
     EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));  // scalars and earlier work are ready
@@ -1693,12 +1520,6 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
         EON_HIP(hipStreamWaitEvent(comp[i], ctx->msm_sorted[w], 0));
         return batch_pieces(ctx, b, batches[k], sorted_ref(sorted_of(k)), *wks[w], comp[i]);
     };
-    // EON_MSM_SORT_AHEAD=1: sort(k + 1) enqueued before pieces(k), so that its kernels take CU
-    // slots before the piece sum fills them (otherwise it is starved and runs after it)
-    static const bool sort_ahead = [] {
-        const char* e = getenv("EON_MSM_SORT_AHEAD");
-        return e && e[0] == '1';
-    }();
     DeferredFinish df;
     EON_TRY(prepare_deferred(ctx, L, width, res_xyzz, df));
     EON_TRY(sort_batch(0));
@@ -1706,11 +1527,10 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
         const int i = (int)(k & 1), w = (int)(k % 3);
         // pieces(k + 1) is enqueued only after reduce(k)'s read-backs: launched earlier it starves
         // the latency-bound reduction (measured +20 ms per prove)
-        if (sort_ahead && k + 1 < batches.size()) EON_TRY(sort_batch(k + 1));
         EON_TRY(pieces(k));
-        if (!sort_ahead && k + 1 < batches.size()) EON_TRY(sort_batch(k + 1));
+        if (k + 1 < batches.size()) EON_TRY(sort_batch(k + 1));
         EON_TRY(batch_reduce(ctx, L, batches[k], sorted_ref(sorted_of(k)), *wks[w], comp[i],
-                             fused_reduce(b, batches[k]), &df));
+                             fused_reduce(batches[k]), &df));
         EON_HIP(hipEventRecord(ctx->msm_reduced[w], comp[i]));
     }
     // the context stream resumes after both compute streams' last reductions
@@ -1751,22 +1571,12 @@ Status msm_run_prepared(eon_ctx* ctx, const eon_msm_bases* const* bases, uint32_
     EON_HIP(ctx->msm.results.ensure(total * (sizeof(G1Affine) + sizeof(G1Xyzz))));
     G1Affine* res = ctx->msm.results.as<G1Affine>();
     G1Xyzz* res_xyzz = reinterpret_cast<G1Xyzz*>(res + total);
-    // Jobs (batch k, bases t) round-robin over NS streams and workspaces (NS = 3, or
-    // EON_MSM_PREP_STREAMS = 2..4), enqueued without a host wait (the reductions have no
-    // read-backs); a workspace is reused only by its own stream, NS jobs later.
-    // EON_MSM_PIECE_CHAIN=1 chains the piece sums (job j's start when job j-1's end, so each
-    // reduction runs beside the next job's piece sums): measured equal to unchained.
-    static const uint32_t NS = [] {
-        const char* e = getenv("EON_MSM_PREP_STREAMS");
-        const int v = e ? atoi(e) : 3;
-        return (uint32_t)(v < 2 ? 2 : (v > 4 ? 4 : v));
-    }();
-    static const bool chain = [] {
-        const char* e = getenv("EON_MSM_PIECE_CHAIN");
-        return e && e[0] == '1';
-    }();
-    hipStream_t comp[4] = {ctx->stream, ctx->side(ctx->msm_side), ctx->side(ctx->msm_side2), ctx->side(ctx->msm_sort)};
-    MsmWork* wks[4] = {&ctx->msm, &ctx->msm_b, &ctx->msm_c, &ctx->msm_d};
+    // Jobs (batch k, bases t) round-robin over NS = 3 streams and workspaces, enqueued without a
+    // host wait (the reductions have no read-backs); a workspace is reused only by its own
+    // stream, NS jobs later.
+    constexpr uint32_t NS = 3;
+    hipStream_t comp[NS] = {ctx->stream, ctx->side(ctx->msm_side), ctx->side(ctx->msm_side2)};
+    MsmWork* wks[NS] = {&ctx->msm, &ctx->msm_b, &ctx->msm_c};
     DeferredFinish df;
     EON_TRY(prepare_deferred(ctx, s->layout, total, res_xyzz, df));
     EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));
@@ -1778,10 +1588,8 @@ Status msm_run_prepared(eon_ctx* ctx, const eon_msm_bases* const* bases, uint32_
             Batch bt = s->batches[k];
             bt.out = res_xyzz + (uint64_t)t * width + bt.col0;
             const SortedRef sr = sorted_ref(s->sorted[k]);
-            if (chain && j > 0) EON_HIP(hipStreamWaitEvent(st, ctx->msm_pdone[(j - 1) % 4], 0));
             EON_TRY(batch_pieces(ctx, bases[t], bt, sr, *wks[j % NS], st));
-            if (chain) EON_HIP(hipEventRecord(ctx->msm_pdone[j % 4], st));
-            EON_TRY(batch_reduce(ctx, s->layout, bt, sr, *wks[j % NS], st, fused_reduce(bases[t], bt), &df));
+            EON_TRY(batch_reduce(ctx, s->layout, bt, sr, *wks[j % NS], st, fused_reduce(bt), &df));
         }
     for (uint32_t i = 1; i < NS; i++) {
         EON_HIP(hipEventRecord(ctx->msm_ev[1], comp[i]));

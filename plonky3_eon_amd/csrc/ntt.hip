@@ -36,21 +36,8 @@ struct PassArgs {
     uint32_t load_param;
     uint32_t has_load_const;
     uint32_t col_tiles;
-    uint32_t radix4;  // k_ntt_pass29: two stages per LDS round trip (EON_NTT_R4)
+    uint32_t last;  // the network's last pass: canonical output (earlier passes store values < 2p)
 };
-
-__device__ __forceinline__ void lds_put(uint4* lo, uint4* hi, uint32_t i, const Fr& x) {
-    lo[i] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
-    hi[i] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
-}
-
-__device__ __forceinline__ Fr lds_get(const uint4* lo, const uint4* hi, uint32_t i) {
-    const uint4 a = lo[i], b = hi[i];
-    Fr x;
-    x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
-    x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
-    return x;
-}
 
 __device__ __forceinline__ Fr gload(const Fr* p) {
     const uint4* q = reinterpret_cast<const uint4*>(p);
@@ -67,119 +54,8 @@ __device__ __forceinline__ void gstore(Fr* p, const Fr& x) {
     q[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
 }
 
-template <bool DIF, int LOG_CB>
-__global__ void __launch_bounds__(1024) k_ntt_pass(PassArgs a) {
-    constexpr uint32_t CB = 1u << LOG_CB;
-    extern __shared__ __attribute__((aligned(16))) uint4 lds[];
-    const uint32_t k = a.k;
-    const uint32_t ne = CB << k;
-    uint4* lo = lds;
-    uint4* hi = lds + ne;
-    Fr* twl = reinterpret_cast<Fr*>(lds + 2 * ne);
-
-    const uint32_t s0 = a.s0;
-    // one-dimensional grid, column tile fastest: the tiles sharing a row segment's cache lines
-    // run together
-    const uint64_t g = blockIdx.x / a.col_tiles;
-    const uint64_t low = g & ((1ull << s0) - 1);
-    const uint64_t base_row = low + ((g >> s0) << (s0 + k));
-    const uint64_t col0 = (uint64_t)(blockIdx.x % a.col_tiles) * CB;
-    const uint64_t width = a.width;
-    const uint32_t T = blockDim.x;
-
-    // Stage the pass's twiddles: LDS slot 2^l + r holds the stage-(s0+l) twiddle for r.
-    for (uint32_t q = threadIdx.x + 1; q < (1u << k); q += T) {
-        const uint32_t l = 31 - __builtin_clz(q);
-        const uint32_t r = q - (1u << l);
-        const uint64_t s = s0 + l;
-        twl[q] = gload(a.tw + (1ull << s) + low + ((uint64_t)r << s0));
-    }
-
-    // Load the tile (row segments of CB columns), applying the input transform.
-    for (uint32_t e = threadIdx.x; e < ne; e += T) {
-        const uint32_t c = e & (CB - 1);
-        const uint32_t m = e >> LOG_CB;
-        const uint64_t p = base_row + ((uint64_t)m << s0);
-        const uint64_t col = col0 + c;
-        Fr x = Fr::zero();
-        if (col < width) {
-            uint64_t r = p;
-            bool present = true;
-            switch (a.load_mode) {
-                case LOAD_BITREV:
-                    r = a.load_param ? (__builtin_bitreverse64(p) >> (64 - a.load_param)) : 0;
-                    break;
-                case LOAD_SPREAD: r = p >> a.load_param; break;
-                case LOAD_ZEROPAD: present = p < a.load_param; break;
-                case LOAD_BITREV_SPREAD: {
-                    const uint32_t nb = a.load_param >> 8;
-                    const uint64_t q = p >> (a.load_param & 0xff);
-                    r = nb ? (__builtin_bitreverse64(q) >> (64 - nb)) : 0;
-                    break;
-                }
-                default: break;
-            }
-            if (present) {
-                x = gload(a.src + r * width + col);
-                if (a.load_scale) x = mul(x, ld_pinned(a.load_scale + r));
-                if (a.has_load_const) x = mul(x, a.load_const);
-            }
-        }
-        lds_put(lo, hi, e, x);
-    }
-    __syncthreads();
-
-    for (uint32_t it = 0; it < k; it++) {
-        const uint32_t l = DIF ? (k - 1 - it) : it;
-        const uint32_t half = 1u << l;
-        for (uint32_t b = threadIdx.x; b < (ne >> 1); b += T) {
-            const uint32_t c = b & (CB - 1);
-            const uint32_t j = b >> LOG_CB;
-            const uint32_t r = j & (half - 1);
-            const uint32_t m0 = ((j >> l) << (l + 1)) | r;
-            const uint32_t i0 = (m0 << LOG_CB) | c;
-            const uint32_t i1 = ((m0 + half) << LOG_CB) | c;
-            const Fr x = lds_get(lo, hi, i0);
-            const Fr y = lds_get(lo, hi, i1);
-            // the twiddle is 1 only for the first butterfly of a block in the group at low = 0
-            const bool unit = (r | low) == 0;
-            Fr u, v;
-            if (!DIF) {
-                // DitButterfly (dft/src/butterflies.rs:177-185): (x + w*y, x - w*y)
-                Fr w = twl[half + r];
-                pin(w);
-                const Fr t = unit ? y : mul(y, w);
-                u = add(x, t);
-                v = sub(x, t);
-            } else {
-                // DIF butterfly: (x + y, (x - y) * w)
-                u = add(x, y);
-                const Fr d = sub(x, y);
-                Fr w = twl[half + r];
-                pin(w);
-                v = unit ? d : mul(d, w);
-            }
-            lds_put(lo, hi, i0, u);
-            lds_put(lo, hi, i1, v);
-        }
-        __syncthreads();
-    }
-
-    for (uint32_t e = threadIdx.x; e < ne; e += T) {
-        const uint32_t c = e & (CB - 1);
-        const uint32_t m = e >> LOG_CB;
-        const uint64_t p = base_row + ((uint64_t)m << s0);
-        const uint64_t col = col0 + c;
-        if (col < width) {
-            Fr x = lds_get(lo, hi, e);
-            if (a.store_scale) x = mul(x, ld_pinned(a.store_scale + p));
-            gstore(a.dst + p * width + col, x);
-        }
-    }
-}
-
-// ---- radix-2^29 butterflies ---------------------------------------------------------------------
-// The same pass with the tile held in LDS as 9 x 29-bit limbs (three planes: limbs 0-3, 4-7, 8)
+// ---- the pass kernel ----------------------------------------------------------------------------
+// The tile is held in LDS as 9 x 29-bit limbs (three planes: limbs 0-3, 4-7, 8)
 // and lazy values < 4p: the product is mul29 (162 carry-free multiply-adds, no carry captures)
 // against twiddles converted to 29-Montgomery form (w 2^261) at staging, so y w 2^256 comes out
 // directly in the radix-2^32 Montgomery form of the product; a butterfly input is brought below
@@ -201,19 +77,20 @@ __device__ __forceinline__ F29 lds_get29(const uint4* lo, const uint4* hi, const
     return x;
 }
 
-// a - K p if a >= K p (a normalised)
-template <uint32_t K>
-__device__ __forceinline__ F29 reduce29(const F29& a) {
-    constexpr KP29<FrP, K> kp{};
-    F29 d;
-    int32_t c = 0;
+// a - q p with q = floor(a_8 / (p_8 + 1)) (a normalised, any value < 2^261): q p <= a_8 2^232 <= a,
+// and a - q p < p + (q + 1) 2^232 < 2p (q <= 169, 2^232 < p / 3.1e6) -- one small-quotient step
+// instead of a chain of conditional subtractions, so the butterflies can let values grow
+__device__ __forceinline__ F29 reduce_top29(const F29& a) {
+    const uint32_t q = a.l[8] / (R29<FrP>::P[8] + 1);
+    F29 r;
+    int64_t c = 0;
 #pragma unroll
     for (int i = 0; i < 9; i++) {
-        const int32_t t = (int32_t)a.l[i] - (int32_t)kp.l[i] + c;
-        d.l[i] = (uint32_t)t & M29;
-        c = t >> 29;
+        const int64_t t = (int64_t)a.l[i] - (int64_t)q * R29<FrP>::P[i] + c;
+        r.l[i] = (uint32_t)t & M29;
+        c = t >> 29;  // arithmetic
     }
-    return c < 0 ? a : d;
+    return r;
 }
 
 template <bool DIF, int LOG_CB>
@@ -288,70 +165,7 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         pin29(w);
         return w;
     };
-    // DitButterfly (dft/src/butterflies.rs:177-185): (x + w y, x - w y); inputs < 4p, outputs < 4p
-    auto bfly_dit = [](F29& x, F29& y, const F29& w, bool unit) {
-        const F29 xr = reduce29<2>(x);
-        const F29 t = unit ? reduce29<2>(y) : mul29<FrP>(y, w);
-        x = add29_norm(xr, t);
-        y = sub29<FrP, 2>(xr, t);
-    };
-    // DIF butterfly: (x + y, (x - y) w)
-    auto bfly_dif = [](F29& x, F29& y, const F29& w, bool unit) {
-        const F29 xr = reduce29<2>(x), yr = reduce29<2>(y);
-        const F29 d = sub29<FrP, 2>(xr, yr);
-        x = add29_norm(xr, yr);
-        y = unit ? d : mul29<FrP>(d, w);
-    };
-    uint32_t it = 0;
-    // radix-4 rounds: the four elements m0 + t h (t < 4) close under two consecutive stages, so a
-    // thread carries them through both in registers -- half the LDS traffic and barriers
-    while (a.radix4 && it + 2 <= k) {
-        const uint32_t lq = DIF ? (k - 2 - it) : it;  // log2 of the quarter distance h
-        const uint32_t h = 1u << lq;
-        for (uint32_t b = threadIdx.x; b < (ne >> 2); b += T) {
-            const uint32_t c = b & (CB - 1);
-            const uint32_t j = b >> LOG_CB;
-            const uint32_t r0 = j & (h - 1);
-            const uint32_t m0 = ((j >> lq) << (lq + 2)) | r0;
-            uint32_t idx[4];
-            F29 x[4];
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                idx[t] = ((m0 + t * h) << LOG_CB) | c;
-                x[t] = lds_get29(lo, hi, top, idx[t]);
-            }
-            // the twiddle-free butterflies are skipped only where a whole stage is twiddle-free
-            // (h = 1 at low = 0: a uniform branch); elsewhere a unit twiddle is multiplied like
-            // any other (its 29-form is 2^261 mod p), as a per-lane choice would run both paths
-            const bool unit = h == 1 && low == 0;
-            if (!DIF) {
-                // stage lq (half h): (0,1), (2,3) with w(h + r0); stage lq + 1 (half 2h): (0,2) with
-                // w(2h + r0), (1,3) with w(3h + r0)
-                const F29 w = unit ? F29{} : tw29(h + r0);
-                bfly_dit(x[0], x[1], w, unit);
-                bfly_dit(x[2], x[3], w, unit);
-                const F29 w0 = unit ? F29{} : tw29(2 * h + r0);
-                bfly_dit(x[0], x[2], w0, unit);
-                const F29 w1 = tw29(3 * h + r0);
-                bfly_dit(x[1], x[3], w1, false);
-            } else {
-                // stage lq + 1 (half 2h): (0,2) with w(2h + r0), (1,3) with w(3h + r0); stage lq
-                // (half h): (0,1), (2,3) with w(h + r0)
-                const F29 w0 = unit ? F29{} : tw29(2 * h + r0);
-                bfly_dif(x[0], x[2], w0, unit);
-                const F29 w1 = tw29(3 * h + r0);
-                bfly_dif(x[1], x[3], w1, false);
-                const F29 w = unit ? F29{} : tw29(h + r0);
-                bfly_dif(x[0], x[1], w, unit);
-                bfly_dif(x[2], x[3], w, unit);
-            }
-#pragma unroll
-            for (int t = 0; t < 4; t++) lds_put29(lo, hi, top, idx[t], x[t]);
-        }
-        __syncthreads();
-        it += 2;
-    }
-    for (; it < k; it++) {
+    for (uint32_t it = 0; it < k; it++) {
         const uint32_t l = DIF ? (k - 1 - it) : it;
         const uint32_t half = 1u << l;
         for (uint32_t b = threadIdx.x; b < (ne >> 1); b += T) {
@@ -361,23 +175,30 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
             const uint32_t m0 = ((j >> l) << (l + 1)) | r;
             const uint32_t i0 = (m0 << LOG_CB) | c;
             const uint32_t i1 = ((m0 + half) << LOG_CB) | c;
-            const F29 x = reduce29<2>(lds_get29(lo, hi, top, i0));  // < 2p
-            const F29 y = lds_get29(lo, hi, top, i1);                 // < 4p
-            // twiddle-free only as a whole stage (uniform branch; see the radix-4 rounds)
+            const F29 x = lds_get29(lo, hi, top, i0);
+            const F29 y = lds_get29(lo, hi, top, i1);
+            // the twiddle-free butterflies are skipped only where a whole stage is twiddle-free
+            // (half = 1 at low = 0: a uniform branch); elsewhere a unit twiddle is multiplied like
+            // any other (its 29-form is 2^261 mod p), as a per-lane choice would run both paths
             const bool unit = half == 1 && low == 0;
             F29 u, v;
             F29 w;
             if (!unit) w = tw29(half + r);
             if (!DIF) {
-                // DitButterfly (dft/src/butterflies.rs:177-185): (x + w*y, x - w*y)
-                const F29 t = unit ? reduce29<2>(y) : mul29<FrP>(y, w);  // < 2p
+                // DitButterfly (dft/src/butterflies.rs:177-185): (x + w*y, x - w*y).  Lazy: t < 2p
+                // (the product, or y itself at the unit stage, which is the pass's first and sees
+                // loaded values < 2p), so both outputs are below x + 2p -- a pass of k <= 10
+                // stages ends below 22p, far inside mul29's input bound (84p against a twiddle
+                // < 2p); the store brings it back below 2p (reduce_top29)
+                const F29 t = unit ? y : mul29<FrP>(y, w);
                 u = add29_norm(x, t);
                 v = sub29<FrP, 2>(x, t);
             } else {
-                // DIF butterfly: (x + y, (x - y) * w)
-                const F29 y2 = reduce29<2>(y);
-                u = add29_norm(x, y2);
-                const F29 d = sub29<FrP, 2>(x, y2);  // < 4p
+                // DIF butterfly: (x + y, (x - y) * w) with inputs < 2p: the sum brought back below
+                // 2p by reduce_top29, the difference < 4p into the product (< 2p) -- or kept below
+                // 4p at the unit stage, which is the pass's last (reduce_top29 at the store)
+                u = reduce_top29(add29_norm(x, y));
+                const F29 d = sub29<FrP, 2>(x, y);
                 v = unit ? d : mul29<FrP>(d, w);
             }
             lds_put29(lo, hi, top, i0, u);
@@ -392,7 +213,9 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         const uint64_t p = base_row + ((uint64_t)m << s0);
         const uint64_t col = col0 + c;
         if (col < width) {
-            Fr x = pack29<FrP>(canon29<FrP>(reduce29<2>(lds_get29(lo, hi, top, e))));
+            // below 2p (fits 256 bits) between passes, canonical after the last one
+            const F29 r = reduce_top29(lds_get29(lo, hi, top, e));
+            Fr x = pack29<FrP>(a.last ? canon29<FrP>(r) : r);
             if (a.store_scale) x = mul(x, ld_pinned(a.store_scale + p));
             gstore(a.dst + p * width + col, x);
         }
@@ -439,17 +262,9 @@ static hipError_t launch_pass(bool dif, uint32_t log_cb, const PassArgs& a, uint
     uint32_t threads = ne / 2;
     if (threads > max_threads) threads = max_threads;
     if (threads < 64) threads = 64;
-    // EON_NTT_R32=1: the radix-2^32 butterflies (k_ntt_pass)
-    static const bool r32 = getenv("EON_NTT_R32") != nullptr;
-    const size_t lds = r32 ? (size_t)ne * 32 + ((size_t)1 << a.k) * 32 : (((size_t)ne * 36 + 15) & ~(size_t)15) + ((size_t)1 << a.k) * 36;
+    const size_t lds = (((size_t)ne * 36 + 15) & ~(size_t)15) + ((size_t)1 << a.k) * 36;
     dim3 grid((unsigned)(groups * col_tiles));
-#define EON_LAUNCH(D, C)                                                             \
-    do {                                                                             \
-        if (r32)                                                                     \
-            hipLaunchKernelGGL((k_ntt_pass<D, C>), grid, dim3(threads), lds, st, a); \
-        else                                                                         \
-            hipLaunchKernelGGL((k_ntt_pass29<D, C>), grid, dim3(threads), lds, st, a); \
-    } while (0)
+#define EON_LAUNCH(D, C) hipLaunchKernelGGL((k_ntt_pass29<D, C>), grid, dim3(threads), lds, st, a)
     switch ((dif ? 4 : 0) + log_cb) {
         case 0: EON_LAUNCH(false, 0); break;
         case 1: EON_LAUNCH(false, 1); break;
@@ -531,27 +346,18 @@ hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
             a.load_mode = LOAD_DIRECT;
         }
         a.store_scale = last ? s.store_scale : nullptr;
+        a.last = last ? 1u : 0u;
         const uint64_t groups = (1ull << s.log_m) >> a.k;
-        static const char* names32[8] = {"k_ntt_pass<false, 0>", "k_ntt_pass<false, 1>",
-                                         "k_ntt_pass<false, 2>", "k_ntt_pass<false, 3>",
-                                         "k_ntt_pass<true, 0>",  "k_ntt_pass<true, 1>",
-                                         "k_ntt_pass<true, 2>",  "k_ntt_pass<true, 3>"};
-        static const char* names29[8] = {"k_ntt_pass29<false, 0>", "k_ntt_pass29<false, 1>",
+        static const char* names[8] = {"k_ntt_pass29<false, 0>", "k_ntt_pass29<false, 1>",
                                          "k_ntt_pass29<false, 2>", "k_ntt_pass29<false, 3>",
                                          "k_ntt_pass29<true, 0>",  "k_ntt_pass29<true, 1>",
                                          "k_ntt_pass29<true, 2>",  "k_ntt_pass29<true, 3>"};
-        static const char* const* names = getenv("EON_NTT_R32") ? names32 : names29;
         // mulmods: one per butterfly (the BASELINE.md count), plus the fused input/output scalings
         const uint64_t elems = (1ull << s.log_m) * s.width;
         const uint64_t mm = elems / 2 * a.k + (a.load_scale ? elems : 0) + (a.has_load_const ? elems : 0) +
                             (a.store_scale ? elems : 0);
         if (prof) prof->begin(names[(s.dif ? 4 : 0) + log_cb], 64ull * elems, st, mm);
         a.col_tiles = (uint32_t)col_tiles;
-        static const bool r4 = [] {
-            const char* e = getenv("EON_NTT_R4");
-            return e && e[0] == '1';
-        }();
-        a.radix4 = r4 ? 1u : 0u;
         const uint32_t tpb = s.max_threads ? s.max_threads : (log_tile > 10 ? 1024 : 512);
         hipError_t e = launch_pass(s.dif, log_cb, a, groups, col_tiles, tpb, st);
         if (prof) prof->end(st);

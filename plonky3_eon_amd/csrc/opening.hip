@@ -392,7 +392,7 @@ Status opening_bases_async29(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
     EON_TRY(bases_alloc_table(ctx, n, TC, &b));
     // ~15 dbl (6M+3S) + 257 madd (8M+2S) and ~254 dbl + ~127 madd + 240 dbl per point
     EON_HIP(sc.mtab.ensure(n * MTAB * sizeof(G1Raw29)));
-    const G1Affine* tab3 = getenv("EON_OPEN_SCALE_R2") ? nullptr : bases_table3_29(srs, st);
+    const G1Affine* tab3 = bases_table3_29(srs, st);  // null (radix 2) if it cannot be built
     // radix 4: 14 dbl (6M+3S) + 129 madd (8M+2S); radix 2: 15 dbl + 257 madd
     ctx->prof.begin("k_open_scale29", n * (TW * 64ull + 128ull), st, n * (tab3 ? 1416ull : 2705ull));
     hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(n, 64)), dim3(64), 0, st, bases_table29(srs), tab3, n, 0ull,
@@ -419,8 +419,7 @@ Status opening_bases_async29(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
 // enqueue the bases of point z on st (no host sync)
 Status opening_bases_async(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, const Fr& z, hipStream_t st,
                            Scratch& sc, eon_msm_bases** out) {
-    static const bool slow = getenv("EON_OPEN_BASES_R32") != nullptr;
-    if (!slow && !z.is_zero() && bases_table29(srs) && bases_window(srs) == TC && bases_windows(srs) == TW &&
+    if (!z.is_zero() && bases_table29(srs) && bases_window(srs) == TC && bases_windows(srs) == TW &&
         n >= 2)
         return opening_bases_async29(ctx, srs, n, z, st, sc, out);
     const G1Affine* g = bases_points(srs);
@@ -490,7 +489,7 @@ Status opening_bases_sharded(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
         EON_HIP(sc[t].aff.ensure(m * sizeof(G1Affine)));
         EON_HIP(sc[t].table_tmp.ensure(slice_entries * sizeof(G1Xyzz)));
         EON_HIP(sc[t].mtab.ensure(m * MTAB * sizeof(G1Raw29)));
-        const G1Affine* tab3 = getenv("EON_OPEN_SCALE_R2") ? nullptr : bases_table3_29(srs, st);
+        const G1Affine* tab3 = bases_table3_29(srs, st);  // null (radix 2) if it cannot be built
         ctx->prof.begin("k_open_scale29", m * (TW * 64ull + 128ull), st, m * (tab3 ? 1416ull : 2705ull));
         hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(m, 64)), dim3(64), 0, st, bases_table29(srs), tab3, n, lo, m,
                            inverse(zs[t]), sc[t].pts.as<G1Xyzz>());
@@ -569,11 +568,9 @@ Status opening_bases_many(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, co
     }
     // sharded when the context is bound to a process group and every point takes the radix-2^29
     // path (a uniform decision: every rank has the same points and SRS)
-    static const bool slow = getenv("EON_OPEN_BASES_R32") != nullptr;
-    static const bool no_shard = getenv("EON_OPEN_BASES_NO_SHARD") != nullptr;
-    bool fast = !slow && bases_table29(srs) && bases_window(srs) == TC && bases_windows(srs) == TW && n >= 2;
+    bool fast = bases_table29(srs) && bases_window(srs) == TC && bases_windows(srs) == TW && n >= 2;
     for (const Fr& z : zs) fast = fast && !z.is_zero();
-    if (fast && !no_shard && ctx->coll.world > 1 && npoints) return opening_bases_sharded(ctx, srs, n, zs, outs);
+    if (fast && ctx->coll.world > 1 && npoints) return opening_bases_sharded(ctx, srs, n, zs, outs);
     hipStream_t streams[3] = {ctx->stream, ctx->side(ctx->msm_side), ctx->side(ctx->msm_side2)};
     EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));
     EON_HIP(hipStreamWaitEvent(ctx->msm_side, ctx->msm_ev[0], 0));

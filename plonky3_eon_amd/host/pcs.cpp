@@ -146,8 +146,6 @@ KzgPcs::KzgPcs(eon_ctx* ctx, uint64_t max_degree, const Fr& srs_alpha) : ctx_(ct
     check(ctx_, eon_msm_bases_create_dev(ctx_, pts.as<eon_g1_affine>(), n, EON_MSM_PRECOMPUTE, &bases_),
           "eon_msm_bases_create_dev");
     check(ctx_, eon_ctx_synchronize(ctx_), "eon_ctx_synchronize");
-    const char* mode = getenv("EON_KZG_OPEN");
-    keep_digits_ = !(mode && std::strcmp(mode, "quotient") == 0);
     // the auxiliary context: its own non-blocking stream, so that its work overlaps this
     // context's even when that one runs on the legacy null stream
     const int dev = eon_ctx_device(ctx_);
@@ -203,14 +201,11 @@ void KzgPcs::commit_columns(std::vector<MatrixProverData>& data, size_t first,
         const uint64_t h = d.coeffs.height;
         const uint32_t w = d.coeffs.width;
         std::vector<eon_g1_affine> cm(w);
-        if (keep_digits_) {
-            eon_msm_scalars* prep = nullptr;
-            check(ctx_, eon_msm_g1_columns_prepare_dev(ctx_, bases_, d.coeffs.data(), h, w, cm.data(), &prep),
-                  "commit_column");
-            d.prepared.reset(prep);
-        } else {
-            check(ctx_, eon_msm_g1_columns_dev(ctx_, bases_, d.coeffs.data(), h, w, cm.data()), "commit_column");
-        }
+        // the column MSMs keep their sorted digits for the openings (KzgPcs::open)
+        eon_msm_scalars* prep = nullptr;
+        check(ctx_, eon_msm_g1_columns_prepare_dev(ctx_, bases_, d.coeffs.data(), h, w, cm.data(), &prep),
+              "commit_column");
+        d.prepared.reset(prep);
         commitments.push_back(std::move(cm));
     }
 }
@@ -265,7 +260,7 @@ std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
     for (const OpenRound& r : rounds) {
         if (r.data->size() != r.points.size()) throw Error(EON_E_SHAPE, "one point list per matrix");
         for (const MatrixProverData& m : *r.data)
-            if (!m.prepared) return open_quotients(rounds);
+            if (!m.prepared) throw Error(EON_E_ARG, "open: matrix committed without its prepared digits");
     }
     using Key = std::pair<uint64_t, std::array<uint64_t, 4>>;
     auto key_of = [](uint64_t n, const Fr& z) {
@@ -374,124 +369,9 @@ std::vector<Opened> KzgPcs::open(const std::vector<OpenRound>& rounds) {
                 }
             }
     };
-    // EON_OPEN_OVERLAP=1: the first point's bases, then the others built on the auxiliary context
-    // while the main one runs the first point's witness MSMs.  Measured equal to building all
-    // bases first (the MSM already saturates the VALUs the bases' kernels need), so off.
-    static const bool overlap = [] {
-        const char* e = getenv("EON_OPEN_OVERLAP");
-        return e && e[0] == '1';
-    }();
-    if (!overlap || !aux_live() || keys.size() < 2) {
-        build(ctx_, keys);
-        run_ready();
-        collect_values();
-        return out;
-    }
-    build(ctx_, {keys[0]});
-    const std::vector<Key> rest(keys.begin() + 1, keys.end());
-    // the thread fills its own map; merged after the join (bases_at is read by run_ready meanwhile)
-    std::map<Key, eon_msm_bases*> made;
-    std::exception_ptr err;
-    const int dev = eon_ctx_device(ctx_);
-    std::thread th([&] {
-        try {
-            hip_check(hipSetDevice(dev), "hipSetDevice");
-            std::map<uint64_t, std::vector<eon_fr>> by_height;
-            for (const Key& k : rest)
-                by_height[k.first].push_back(eon_fr{{k.second[0], k.second[1], k.second[2], k.second[3]}});
-            for (auto& [n, zs] : by_height) {
-                std::vector<eon_msm_bases*> bs(zs.size(), nullptr);
-                check(aux_, eon_kzg_opening_bases_create_many(aux_, bases_, n, zs.data(), (uint32_t)zs.size(), bs.data()),
-                      "opening bases");
-                for (size_t t = 0; t < zs.size(); t++)
-                    made[Key(n, std::array<uint64_t, 4>{zs[t].l[0], zs[t].l[1], zs[t].l[2], zs[t].l[3]})] = bs[t];
-            }
-        } catch (...) {
-            err = std::current_exception();
-        }
-    });
-    try {
-        run_ready();
-    } catch (...) {
-        th.join();
-        for (auto& kv : made) bases_at[kv.first] = kv.second;
-        throw;
-    }
-    th.join();
-    for (auto& kv : made) bases_at[kv.first] = kv.second;
-    if (err) std::rethrow_exception(err);
+    build(ctx_, keys);
     run_ready();
     collect_values();
-    return out;
-}
-
-std::vector<Opened> KzgPcs::open_quotients(const std::vector<OpenRound>& rounds) {
-    struct Job {
-        size_t round, matrix, point;
-        uint64_t n;
-        uint32_t w;
-        uint32_t col0 = 0;
-    };
-    std::vector<Job> jobs;
-    std::vector<Opened> out(rounds.size());
-    for (size_t r = 0; r < rounds.size(); r++) {
-        const auto& data = *rounds[r].data;
-        if (data.size() != rounds[r].points.size()) throw Error(EON_E_SHAPE, "one point list per matrix");
-        out[r].values.resize(data.size());
-        out[r].witnesses.resize(data.size());
-        for (size_t m = 0; m < data.size(); m++) {
-            const size_t np = rounds[r].points[m].size();
-            out[r].values[m].resize(np);
-            out[r].witnesses[m].resize(np);
-            for (size_t p = 0; p < np; p++) jobs.push_back(Job{r, m, p, data[m].coeffs.height, data[m].coeffs.width});
-        }
-    }
-    // one witness matrix per quotient height n - 1, columns in job order
-    std::map<uint64_t, uint32_t> group_width;
-    for (Job& j : jobs) {
-        j.col0 = group_width[j.n];
-        group_width[j.n] += j.w;
-    }
-    std::map<uint64_t, DeviceMatrix> mats;
-    uint64_t tmp_elems = 1;
-    for (const auto& [n, w] : group_width) {
-        mats.emplace(n, DeviceMatrix::alloc(std::max<uint64_t>(n, 2) - 1, w));
-        (void)w;
-    }
-    for (const Job& j : jobs) tmp_elems = std::max<uint64_t>(tmp_elems, (std::max<uint64_t>(j.n, 2) - 1) * j.w);
-    uint32_t max_w = 1;
-    for (const Job& j : jobs) max_w = std::max(max_w, j.w);
-    DeviceBuffer quo(tmp_elems * sizeof(eon_fr));
-    DeviceBuffer vals(max_w * sizeof(eon_fr));
-    hipStream_t st = static_cast<hipStream_t>(eon_ctx_stream(ctx_));
-    for (const Job& j : jobs) {
-        const MatrixProverData& m = (*rounds[j.round].data)[j.matrix];
-        const eon_fr z = rounds[j.round].points[j.matrix][j.point].abi();
-        // quotient_and_eval (util.rs:100-111) for every column of the matrix
-        check(ctx_,
-              eon_quotient_and_eval_columns_dev(ctx_, m.coeffs.data(), j.n, j.w, &z, quo.as<eon_fr>(),
-                                                vals.as<eon_fr>()),
-              "quotient_and_eval");
-        DeviceMatrix& dst = mats.at(j.n);
-        if (j.n > 1)
-            hip_check(hipMemcpy2DAsync(dst.mutable_data() + j.col0, sizeof(eon_fr) * dst.width, quo.get(),
-                                       sizeof(eon_fr) * j.w, sizeof(eon_fr) * j.w, j.n - 1, hipMemcpyDeviceToDevice,
-                                       st),
-                      "witness matrix");
-        std::vector<eon_fr>& v = out[j.round].values[j.matrix][j.point];
-        v.resize(j.w);
-        hip_check(hipMemcpyAsync(v.data(), vals.get(), sizeof(eon_fr) * j.w, hipMemcpyDeviceToHost, st),
-                  "opened values");
-        hip_check(hipStreamSynchronize(st), "opened values");
-    }
-    for (auto& [n, mat] : mats) {
-        std::vector<eon_g1_affine> wits(mat.width);
-        check(ctx_, eon_msm_g1_columns_dev(ctx_, bases_, mat.data(), n - 1, mat.width, wits.data()), "witnesses");
-        for (const Job& j : jobs) {
-            if (j.n != n) continue;
-            out[j.round].witnesses[j.matrix][j.point].assign(wits.begin() + j.col0, wits.begin() + j.col0 + j.w);
-        }
-    }
     return out;
 }
 

@@ -125,7 +125,6 @@ class KzgPcs {
     DeviceMatrix get_evaluations_on_domain(const std::vector<MatrixProverData>& data, size_t idx,
                                            const Domain& domain, bool aux = false);
     // a second context on the same device for work concurrent with this one's (null if none)
-    eon_ctx* aux_ctx() const { return aux_live(); }
     // the auxiliary context, unless the main one is in serial mode (eon_ctx_set_serial: every
     // kernel alone on the device, for isolated profiles)
     eon_ctx* aux_live() const { return aux_ && !eon_ctx_serial(ctx_) ? aux_ : nullptr; }
@@ -140,8 +139,6 @@ class KzgPcs {
     std::vector<Opened> open(const std::vector<OpenRound>& rounds);
 
   private:
-    std::vector<Opened> open_quotients(const std::vector<OpenRound>& rounds);
-    bool keep_digits_ = true;
     eon_ctx* ctx_;
     uint64_t max_degree_;
     eon_msm_bases* bases_ = nullptr;

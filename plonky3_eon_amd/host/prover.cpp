@@ -93,15 +93,6 @@ Proof prove(KzgPcs& pcs, const AirRef& air, const eon_fr* trace, uint64_t height
     std::vector<MatrixProverData> trace_data;
     const Domain quotient_domain = trace_domain.create_disjoint_domain(1ull << (log_n + log_qd));
     const uint64_t q_rows = quotient_domain.size();
-    // The trace LDE (prover.rs:315) needs only the committed coefficients, not alpha: it runs on
-    // the PCS's auxiliary context while the column MSMs of the commitment (prover.rs:186-187)
-    // run on the main one, and filling the MSM's memory- and latency-bound phases (digit sorts,
-    // bucket reductions) with NTT passes.  Opt-in (EON_PROVE_OVERLAP=1): measured equal to the
-    // reference's order so far -- the NTT saturates the VALUs the piece sums need.
-    static const bool overlap = [] {
-        const char* e = getenv("EON_PROVE_OVERLAP");
-        return e && e[0] == '1';
-    }();
     DeviceMatrix lde;
     clock::time_point t1, t2;
     {
@@ -109,30 +100,8 @@ Proof prove(KzgPcs& pcs, const AirRef& air, const eon_fr* trace, uint64_t height
         ev.emplace_back(trace_domain, DeviceMatrix::borrow(trace, height, width));
         pcs.commit_coeffs(std::move(ev), trace_data);
     }
-    if (overlap && pcs.aux_ctx()) {
-        std::exception_ptr lde_err;
-        const int dev = eon_ctx_device(ctx);
-        std::thread lde_thread([&] {
-            try {
-                hip_ok(hipSetDevice(dev), "hipSetDevice");
-                lde = pcs.get_evaluations_on_domain(trace_data, 0, quotient_domain, true);
-            } catch (...) {
-                lde_err = std::current_exception();
-            }
-        });
-        try {
-            pcs.commit_columns(trace_data, 0, trace_commit);
-        } catch (...) {
-            lde_thread.join();
-            throw;
-        }
-        t1 = tick();
-        lde_thread.join();
-        if (lde_err) std::rethrow_exception(lde_err);
-    } else {
-        pcs.commit_columns(trace_data, 0, trace_commit);
-        t1 = tick();
-    }
+    pcs.commit_columns(trace_data, 0, trace_commit);
+    t1 = tick();
     // Fiat-Shamir up to alpha (prover.rs:196-208, 300) on a host thread while the device extends
     // the trace: sharded, every rank observes the full commitment (all-gathered in rank = lane
     // order first)
@@ -161,13 +130,12 @@ Proof prove(KzgPcs& pcs, const AirRef& air, const eon_fr* trace, uint64_t height
             alpha = challenger->sample();  // no lookups
         });
     }
-    if (!(overlap && pcs.aux_ctx())) {
-        try {
-            lde = pcs.get_evaluations_on_domain(trace_data, 0, quotient_domain);
-        } catch (...) {
-            if (fs_thread.joinable()) fs_thread.join();
-            throw;
-        }
+    // the trace LDE (prover.rs:315) while the host thread runs the transcript up to alpha
+    try {
+        lde = pcs.get_evaluations_on_domain(trace_data, 0, quotient_domain);
+    } catch (...) {
+        if (fs_thread.joinable()) fs_thread.join();
+        throw;
     }
     if (fs_thread.joinable()) fs_thread.join();
     DeviceMatrix qv = DeviceMatrix::alloc(q_rows, 1);

@@ -88,6 +88,29 @@ def test_structured_scalars(gpu_ctx):
             np.testing.assert_array_equal(MsmBases(pts, gpu_ctx, precompute=pre).msm(s), C.g1_msm(pts, s))
 
 
+@pytest.mark.parametrize("bits", [8, 12, 16, 24, 48, 64])
+def test_active_window_truncation_edges(gpu_ctx, bits):
+    """A single MSM digitises only the windows its largest scalar reaches (k_scalar_or); the signed
+    recoding can carry one window past that scalar's top bit.  Largest scalar exactly 2^b - 1, 2^b
+    and 2^b + 2^(b-1) for b on and off the window boundaries of both layouts (c = 12 fixed-base,
+    c = 8 plain at n = 4096), the rest below 2^(b-1); plus scalars over the full u64 range
+    (kzg/benches/kzg_benches.rs:19, Fr::new(rng.random::<u64>()))."""
+    n = 4096
+    pts = C.g1_srs(n, C.fr_from_u64(12345))
+    rng = np.random.default_rng(bits)
+    base = [int(x) for x in rng.integers(0, 2 ** (bits - 1), n, dtype=np.uint64)]
+    for top in ((1 << bits) - 1, 1 << bits, (1 << bits) + (1 << (bits - 1))):
+        vals = list(base)
+        vals[rng.integers(0, n)] = top
+        s = np.array([O.int_to_limbs(O.to_mont(v)) for v in vals], dtype=np.uint64)
+        want = C.g1_msm(pts, s)
+        for pre in (True, False):
+            np.testing.assert_array_equal(MsmBases(pts, gpu_ctx, precompute=pre).msm(s), want, err_msg=f"top={top:#x}")
+    full = np.stack([C.fr_from_u64(int(v)) for v in rng.integers(0, 2**64, n, dtype=np.uint64)])
+    for pre in (True, False):
+        np.testing.assert_array_equal(MsmBases(pts, gpu_ctx, precompute=pre).msm(full), C.g1_msm(pts, full))
+
+
 def test_all_equal_scalars_multi_level(gpu_ctx):
     """2^16 equal scalars: every window's digit hits one bucket, 2^16 entries -> 3 combine
     levels; the value is [s * sum(alpha^i)] G."""

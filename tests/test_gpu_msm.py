@@ -211,3 +211,47 @@ def test_columns_fused_reduce_edge_cases(gpu_ctx):
     for j in range(width):
         k = sum(cols[j]) % O.P
         assert as_py(got2[j]) == (O.g1_mul(P, k) if k else O.INF), j
+
+
+def test_all_windows_knob_same_result():
+    """EON_MSM_ALL_WINDOWS=1 (digitise every window, not only those the largest scalar reaches)
+    gives the same MSMs: window-boundary scalars and full-range ones, in a fresh process (the knob
+    is read once)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[2])
+from oracle import coracle as C
+from oracle import pyoracle as O
+from plonky3_eon_amd import Context
+from plonky3_eon_amd.msm import MsmBases
+ctx = Context(0)
+n = 2048
+pts = C.g1_srs(n, C.fr_from_u64(777))
+out = []
+for top in (1 << 16, (1 << 24) - 1, (1 << 32) + (1 << 31), O.P - 1):
+    vals = [int(x) for x in np.random.default_rng(top % 1000).integers(0, 2**15, n)]
+    vals[5] = top
+    s = np.array([O.int_to_limbs(O.to_mont(v)) for v in vals], dtype=np.uint64)
+    for pre in (True, False):
+        out.append(MsmBases(pts, ctx, precompute=pre).msm(s))
+np.save(sys.argv[1], np.stack(out))
+'''
+    import os
+    import tempfile
+
+    root = str(Path(__file__).resolve().parents[1])
+    res = []
+    with tempfile.TemporaryDirectory() as d:
+        for knob in (None, "1"):
+            env = dict(os.environ)
+            env.pop("EON_MSM_ALL_WINDOWS", None)
+            if knob:
+                env["EON_MSM_ALL_WINDOWS"] = knob
+            f = os.path.join(d, f"r{knob}.npy")
+            subprocess.run([sys.executable, "-c", code, f, root], check=True, env=env, timeout=240)
+            res.append(np.load(f))
+    np.testing.assert_array_equal(res[0], res[1])

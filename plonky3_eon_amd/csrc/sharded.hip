@@ -85,17 +85,6 @@ Status fourstep_dft(eon_ctx* ctx, const Fr* in, Fr* out, uint32_t log_n, int lay
     return Status::ok();
 }
 
-G1Affine from_abi(const eon_g1_affine& p) {
-    G1Affine r;
-    for (int i = 0; i < 4; i++) {
-        r.x.v[2 * i] = (uint32_t)p.x[i];
-        r.x.v[2 * i + 1] = (uint32_t)(p.x[i] >> 32);
-        r.y.v[2 * i] = (uint32_t)p.y[i];
-        r.y.v[2 * i + 1] = (uint32_t)(p.y[i] >> 32);
-    }
-    return r;
-}
-
 eon_g1_affine to_abi(const G1Affine& a) {
     eon_g1_affine r;
     for (int i = 0; i < 4; i++) {
@@ -103,6 +92,14 @@ eon_g1_affine to_abi(const G1Affine& a) {
         r.y[i] = (uint64_t)a.y.v[2 * i] | (uint64_t)a.y.v[2 * i + 1] << 32;
     }
     return r;
+}
+
+// out = sum of the n affine partials (ABI layout = G1Affine), in index order
+__global__ void k_sum_partials(const G1Affine* parts, uint32_t n, G1Affine* out) {
+    if (threadIdx.x != 0) return;
+    G1Xyzz acc = xyzz_inf();
+    for (uint32_t g = 0; g < n; g++) acc = xyzz_add_affine(acc, ld_affine(parts + g));
+    st_affine(out, xyzz_to_affine(acc));
 }
 
 Status msm_sharded(eon_ctx* ctx, const eon_msm_bases* bases, const Fr* scalars, uint64_t n_local,
@@ -128,14 +125,14 @@ Status msm_sharded(eon_ctx* ctx, const eon_msm_bases* bases, const Fr* scalars, 
     EON_HIP(hipMemcpyAsync(send.p, &pa, sizeof pa, hipMemcpyHostToDevice, ctx->stream));
     if (coll->all_gather(coll->user, send.p, recv.p, sizeof(eon_g1_affine), ctx->stream) != 0)
         return Status::err(EON_E_DEVICE, "collective all_gather failed (MSM partials)");
-    std::vector<eon_g1_affine> parts(world);
-    EON_HIP(hipMemcpyAsync(parts.data(), recv.p, world * sizeof(eon_g1_affine), hipMemcpyDeviceToHost, ctx->stream));
-    EON_HIP(hipStreamSynchronize(ctx->stream));
-    // rank order, the same on every rank: every rank ends with identical bytes
-    G1Xyzz acc = xyzz_inf();
-    for (uint32_t g = 0; g < world; g++) acc = xyzz_add_affine(acc, from_abi(parts[g]));
+    // the partials summed on device in rank order (EC additions: not an RCCL reduction op), the
+    // same on every rank, so every rank ends with identical bytes
+    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, ctx->stream, recv.as<G1Affine>(), world,
+                       send.as<G1Affine>());
+    EON_HIP(hipGetLastError());
     G1Affine r;
-    host_xyzz_to_affine(&acc, 1, &r);
+    EON_HIP(hipMemcpyAsync(&r, send.p, sizeof r, hipMemcpyDeviceToHost, ctx->stream));
+    EON_HIP(hipStreamSynchronize(ctx->stream));
     *out = to_abi(r);
     return Status::ok();
 }

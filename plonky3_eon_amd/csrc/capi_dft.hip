@@ -129,7 +129,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         const Fr* table = nullptr;
         if (natural) {
             a.dif = true;  // natural evals -> bit-reversed coefficients
-            EON_TRY(get_power_table(ctx, n, shift, n_inv, true, &table));
+            EON_TRY(get_power_table(ctx, n, shift, ntt_scale_form(n_inv), true, &table));
             f.dif = false;
             f.first_stage = b;
             f.load_mode = LOAD_SPREAD;
@@ -138,12 +138,15 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
             a.dif = false;  // bit-reversed gather -> natural coefficients
             a.load_mode = LOAD_BITREV;
             a.load_param = n;
-            EON_TRY(get_power_table(ctx, n, shift, n_inv, false, &table));
+            EON_TRY(get_power_table(ctx, n, shift, ntt_scale_form(n_inv), false, &table));
             f.dif = true;
             f.load_mode = LOAD_ZEROPAD;
             f.load_param = (uint32_t)height;
         }
-        f.load_scale = table;
+        // coefficient j times shift^j / N, applied as the inverse network stores coefficient j
+        // (its output row; the table is in that row order): once per coefficient, where the
+        // forward network's loads would read each coefficient 2^b times
+        a.store_scale = table;
         a.max_stages_per_pass = f.max_stages_per_pass = ctx->ntt_max_stages;
         a.max_threads = f.max_threads = ctx->ntt_tpb;
         a.log_tile = f.log_tile = ctx->ntt_log_tile;
@@ -159,7 +162,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         // committed coefficients (kzg/src/pcs.rs:267-287; commit/src/testing.rs:93-105)
         if (in == out) return Status::err(EON_E_ARG, "padded coset DFT cannot run in place");
         const Fr* table = nullptr;
-        EON_TRY(get_power_table(ctx, n, shift, Fr::one(), false, &table));
+        EON_TRY(get_power_table(ctx, n, shift, ntt_scale_form(Fr::one()), false, &table));
         NetworkSpec f;
         f.log_m = n + b;
         f.src = in;
@@ -205,18 +208,18 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
     }
     if (op == Op::CosetDft) {
         const Fr* table = nullptr;
-        EON_TRY(get_power_table(ctx, n, shift, Fr::one(), false, &table));
+        EON_TRY(get_power_table(ctx, n, shift, ntt_scale_form(Fr::one()), false, &table));
         s.load_scale = table;
     }
     if (inv) {
         s.has_load_const = 1;
-        s.load_const = n_inv;
+        s.load_const = ntt_scale_form(n_inv);
     }
     // coset_idft with shift 1 (KzgPcs::commit of the trace, kzg/src/pcs.rs:242) is the idft: no
     // output scaling by the all-ones powers of 1^-1
     if (op == Op::CosetIdft && !(shift == Fr::one())) {
         const Fr* table = nullptr;
-        EON_TRY(get_power_table(ctx, n, inverse(shift), Fr::one(), false, &table));
+        EON_TRY(get_power_table(ctx, n, inverse(shift), ntt_scale_form(Fr::one()), false, &table));
         s.store_scale = table;
     }
     s.max_stages_per_pass = ctx->ntt_max_stages;

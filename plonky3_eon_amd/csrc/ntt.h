@@ -81,6 +81,11 @@ struct Profiler {
     }
 };
 
+// The form in which k_ntt_pass29 takes every multiplier -- twiddle tables, load / store scale
+// tables and the load constant: 32 c (in Montgomery form), so that the 29-limb product
+// mul29(x, 32 c) = x c 2^256 mod p needs no conversion of the multiplier.
+inline Fr ntt_scale_form(const Fr& c) { return mul(c, from_u64<FrP>(32)); }
+
 hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof = nullptr);
 hipError_t launch_powers(Fr* out, uint64_t n, const Fr& base, const Fr& scale, uint32_t rev_log,
                          hipStream_t st);

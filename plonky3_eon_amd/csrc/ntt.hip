@@ -56,11 +56,11 @@ __device__ __forceinline__ void gstore(Fr* p, const Fr& x) {
 
 // ---- the pass kernel ----------------------------------------------------------------------------
 // The tile is held in LDS as 9 x 29-bit limbs (three planes: limbs 0-3, 4-7, 8)
-// and lazy values < 4p: the product is mul29 (162 carry-free multiply-adds, no carry captures)
-// against twiddles converted to 29-Montgomery form (w 2^261) at staging, so y w 2^256 comes out
-// directly in the radix-2^32 Montgomery form of the product; a butterfly input is brought below
-// 2p by one conditional subtraction, its outputs stay below 4p; the store canonicalises.  Input
-// and output scalings keep the radix-2^32 product (once per element per pass).
+// and lazy values: the product is mul29 (162 carry-free multiply-adds, no carry captures) against
+// twiddles held as w 2^261 = (32 w) 2^256, i.e. the twiddle tables store the Montgomery form of
+// 32 w (launch_twiddles), so y w 2^256 comes out directly in the radix-2^32 Montgomery form of
+// the product and staging a twiddle is a load and an unpack.  The input / output scalings (coset
+// powers, 1/n) are tables and constants in the same 32 c form, applied with mul29 as well.
 
 __device__ __forceinline__ void lds_put29(uint4* lo, uint4* hi, uint32_t* top, uint32_t i, const F29& x) {
     lo[i] = make_uint4(x.l[0], x.l[1], x.l[2], x.l[3]);
@@ -122,9 +122,7 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         const uint32_t l = 31 - __builtin_clz(q);
         const uint32_t r = q - (1u << l);
         const uint64_t s = s0 + l;
-        const F29 w = mul29<FrP>(unpack29(gload(a.tw + (1ull << s) + low + ((uint64_t)r << s0))),
-                                 const29<FrP>(R29<FrP>::TO261));
-        lds_put29(tlo, thi, ttop, q, w);
+        lds_put29(tlo, thi, ttop, q, unpack29(gload(a.tw + (1ull << s) + low + ((uint64_t)r << s0))));
     }
 
     for (uint32_t e = threadIdx.x; e < ne; e += T) {
@@ -132,7 +130,7 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         const uint32_t m = e >> LOG_CB;
         const uint64_t p = base_row + ((uint64_t)m << s0);
         const uint64_t col = col0 + c;
-        Fr x = Fr::zero();
+        F29 x = unpack29(Fr::zero());
         if (col < width) {
             uint64_t r = p;
             bool present = true;
@@ -151,12 +149,13 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
                 default: break;
             }
             if (present) {
-                x = gload(a.src + r * width + col);
-                if (a.load_scale) x = mul(x, ld_pinned(a.load_scale + r));
-                if (a.has_load_const) x = mul(x, a.load_const);
+                // canonical in, below 2p out of a product (the first stage's input bound)
+                x = unpack29(gload(a.src + r * width + col));
+                if (a.load_scale) x = mul29<FrP>(x, unpack29(ld_pinned(a.load_scale + r)));
+                if (a.has_load_const) x = mul29<FrP>(x, unpack29(a.load_const));
             }
         }
-        lds_put29(lo, hi, top, e, unpack29(x));
+        lds_put29(lo, hi, top, e, x);
     }
     __syncthreads();
 
@@ -194,11 +193,14 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
                 u = add29_norm(x, t);
                 v = sub29<FrP, 2>(x, t);
             } else {
-                // DIF butterfly: (x + y, (x - y) * w) with inputs < 2p: the sum brought back below
-                // 2p by reduce_top29, the difference < 4p into the product (< 2p) -- or kept below
-                // 4p at the unit stage, which is the pass's last (reduce_top29 at the store)
-                u = reduce_top29(add29_norm(x, y));
-                const F29 d = sub29<FrP, 2>(x, y);
+                // DIF butterfly: (x + y, (x - y) * w).  The pass's inputs are below 2p; the sum is
+                // brought back below 2p by reduce_top29 only at odd stages of the pass, so every
+                // stage sees inputs below 4p: the sum < 8p, the difference x - y + 4p < 8p into
+                // the product (< 2p) -- or kept at the unit stage, which is the pass's last
+                // (reduce_top29 at the store)
+                const F29 sum = add29_norm(x, y);
+                u = (it & 1) ? reduce_top29(sum) : sum;
+                const F29 d = sub29<FrP, 4>(x, y);
                 v = unit ? d : mul29<FrP>(d, w);
             }
             lds_put29(lo, hi, top, i0, u);
@@ -214,10 +216,9 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         const uint64_t col = col0 + c;
         if (col < width) {
             // below 2p (fits 256 bits) between passes, canonical after the last one
-            const F29 r = reduce_top29(lds_get29(lo, hi, top, e));
-            Fr x = pack29<FrP>(a.last ? canon29<FrP>(r) : r);
-            if (a.store_scale) x = mul(x, ld_pinned(a.store_scale + p));
-            gstore(a.dst + p * width + col, x);
+            F29 r = reduce_top29(lds_get29(lo, hi, top, e));
+            if (a.store_scale) r = mul29<FrP>(r, unpack29(ld_pinned(a.store_scale + p)));
+            gstore(a.dst + p * width + col, pack29<FrP>(a.last ? canon29<FrP>(r) : r));
         }
     }
 }
@@ -291,9 +292,10 @@ hipError_t launch_powers(Fr* out, uint64_t n, const Fr& base, const Fr& scale, u
 }
 
 hipError_t launch_twiddles(Fr* tw, uint32_t L, const Fr& root_L, hipStream_t st) {
-    // tw has 2^L entries; tw[0] unused.  Stage L-1 table = root_L^j, j < 2^(L-1).
+    // tw has 2^L entries; tw[0] unused.  Stage L-1 table = 32 root_L^j, j < 2^(L-1) (the 29-limb
+    // product form, see k_ntt_pass29)
     if (L == 0) return hipSuccess;
-    hipError_t e = launch_powers(tw + (1ull << (L - 1)), 1ull << (L - 1), root_L, Fr::one(),
+    hipError_t e = launch_powers(tw + (1ull << (L - 1)), 1ull << (L - 1), root_L, ntt_scale_form(Fr::one()),
                                  NATURAL_IDX, st);
     if (e != hipSuccess || L == 1) return e;
     const uint64_t n = 1ull << (L - 1);

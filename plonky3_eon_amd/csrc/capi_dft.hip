@@ -32,9 +32,11 @@ Status ensure_twiddles(eon_ctx* ctx, uint32_t log_n) {
     const size_t bytes = ((size_t)1 << L) * sizeof(Fr);
     EON_HIP(ctx->tw_fwd.ensure(bytes));
     EON_HIP(ctx->tw_inv.ensure(bytes));
+    EON_HIP(ctx->twq_fwd.ensure(((size_t)1 << L) * TWQ_STRIDE * sizeof(uint32_t)));
+    EON_HIP(ctx->twq_inv.ensure(((size_t)1 << L) * TWQ_STRIDE * sizeof(uint32_t)));
     const Fr root = fr_two_adic_generator(L);
-    EON_HIP(launch_twiddles(ctx->tw_fwd.as<Fr>(), L, root, ctx->stream));
-    EON_HIP(launch_twiddles(ctx->tw_inv.as<Fr>(), L, inverse(root), ctx->stream));
+    EON_HIP(launch_twiddles(ctx->tw_fwd.as<Fr>(), ctx->twq_fwd.as<uint32_t>(), L, root, ctx->stream));
+    EON_HIP(launch_twiddles(ctx->tw_inv.as<Fr>(), ctx->twq_inv.as<uint32_t>(), L, inverse(root), ctx->stream));
     ctx->tw_log = L;
     return Status::ok();
 }
@@ -120,12 +122,14 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         a.dst = coeffs;
         a.width = width;
         a.tw = ctx->tw_inv.as<Fr>();
+        a.twq = ctx->twq_inv.as<uint32_t>();
         NetworkSpec f;  // coefficients -> evaluations on shift * K
         f.log_m = n + b;
         f.src = coeffs;
         f.dst = out;
         f.width = width;
         f.tw = ctx->tw_fwd.as<Fr>();
+        f.twq = ctx->twq_fwd.as<uint32_t>();
         const Fr* table = nullptr;
         if (natural) {
             a.dif = true;  // natural evals -> bit-reversed coefficients
@@ -169,6 +173,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         f.dst = out;
         f.width = width;
         f.tw = ctx->tw_fwd.as<Fr>();
+        f.twq = ctx->twq_fwd.as<uint32_t>();
         f.load_scale = table;  // coefficient j times shift^j, indexed by source row
         if (natural) {
             f.dif = false;
@@ -195,6 +200,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
     s.width = width;
     const bool inv = op == Op::Idft || op == Op::CosetIdft;
     s.tw = inv ? ctx->tw_inv.as<Fr>() : ctx->tw_fwd.as<Fr>();
+    s.twq = inv ? ctx->twq_inv.as<uint32_t>() : ctx->twq_fwd.as<uint32_t>();
     // idft / coset_idft always return natural-order coefficients (RowMajorMatrix)
     s.dif = !(inv || natural);
     if (!s.dif) {
@@ -327,6 +333,8 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->msm_sort);
     ctx->tw_fwd.release();
     ctx->tw_inv.release();
+    ctx->twq_fwd.release();
+    ctx->twq_inv.release();
     for (auto& kv : ctx->tables) kv.second.release();
     for (auto& r : ctx->prof.recs) {
         (void)hipEventDestroy(r.start);

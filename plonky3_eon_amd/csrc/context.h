@@ -99,8 +99,9 @@ struct eon_ctx {
     std::mutex mu;
     std::string last_error;
 
-    // stage-concatenated twiddles for sizes up to 2^tw_log (forward and inverse)
-    eon::DevBuf tw_fwd, tw_inv;
+    // stage-concatenated twiddles for sizes up to 2^tw_log (forward and inverse): the plain roots w
+    // (32 B each) and their Shoup quotients floor(w 2^261 / p) (9 limbs of 29 bits in 48 B)
+    eon::DevBuf tw_fwd, tw_inv, twq_fwd, twq_inv;
     uint32_t tw_log = 0;
 
     // coset / scaling tables keyed by (kind, log_n, base, scale)

@@ -55,7 +55,11 @@ struct R29<FrP> {
     static constexpr uint32_t TO256[9] = {0xffffffbu,  0x4b1a0e2u,  0x18334a6bu, 0x18ed2b3eu, 0x1462e36fu,
                                           0x11b7bc3cu, 0x1cbd99bau, 0x183340fbu, 0xe0a77u};
     static constexpr uint32_t TO261[9] = {0xfffead7u, 0x1d5444f4u, 0x4438aa5u,  0x3b4d096u, 0x134c84dau,
-                                          0xe92d304u, 0x14cb95b3u, 0x41b9d3du,  0x58003u};
+                                          0xe92d304u, 0x14cb95b3u, 0x41b9d3du,  0x58003u};    // 2^261 - p and p^-1 mod 2^261 (Shoup products by twiddles, mul29_shoup / the twiddle tables)
+    static constexpr uint32_t NEGP261[9] = {0xfffffffu, 0xf05360u,   0x11a3dbafu, 0x182f6f0cu, 0xa7a2d7cu,
+                                            0x1d24bf3fu, 0x1f591ebeu, 0x11a3d9cbu, 0x1fcf9bb1u};
+    static constexpr uint32_t PINV261[9] = {0x10000001u, 0x8f05360u,  0x5bb930fu,  0x12f36967u, 0x1dc6e9a7u,
+                                            0x13ebb37cu, 0x19347195u, 0x1c5e4f97u, 0xd8c07d0u};
 };
 
 // K p as normalised limbs (compile-time)
@@ -304,6 +308,79 @@ EON_HD F29 mul29(const F29& a, const F29& b) {
     }
     r.l[8] = (uint32_t)acc;
     return r;
+}
+
+// y w mod p for a constant w < p with its Shoup quotient wq = floor(w 2^261 / p), both as
+// normalised 29-bit limbs (the NTT's twiddles): q = floor(y wq / 2^261) from the product's columns
+// 7..16 -- the columns below 7 sum to less than 2^235, so the estimate is q or q - 1 -- then
+// r = y w - q p modulo 2^261, as y w + q (2^261 - p) with positive limbs only.  q <= y w / p and
+// q >= y w / p - y / 2^261 - 2, so r is in [0, 3p) for any normalised y < 2^261, exact modulo
+// 2^261.  143 multiply-adds and no Montgomery multipliers (mul29: 162 + 9 v_mul_lo).  The product
+// is not divided by any power of two, so y in Montgomery form gives y w in Montgomery form for
+// the plain integer w.
+template <class M>
+EON_HD F29 mul29_shoup(const F29& y, const F29& w, const F29& wq) {
+    uint64_t acc;
+    uint32_t q[9];
+    mul29_vv(acc, y.l[0], wq.l[7]);
+#pragma unroll
+    for (int i = 1; i <= 7; i++) mad29_vv(acc, y.l[i], wq.l[7 - i]);
+    acc >>= 29;
+#pragma unroll
+    for (int i = 0; i <= 8; i++) mad29_vv(acc, y.l[i], wq.l[8 - i]);
+    acc >>= 29;
+#pragma unroll
+    for (int k = 9; k < 17; k++) {
+#pragma unroll
+        for (int i = k - 8; i < 9; i++) mad29_vv(acc, y.l[i], wq.l[k - i]);
+        q[k - 9] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
+    q[8] = (uint32_t)acc;  // q < y < 2^261
+    F29 r;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        // column k: (k + 1) products of each half, at most 18 products < 2^58 (< 2^62.2 with carry)
+        if (k == 0)
+            mul29_vv(acc, y.l[0], w.l[0]);
+        else
+            mad29_vv(acc, y.l[0], w.l[k]);
+#pragma unroll
+        for (int i = 1; i <= k; i++) mad29_vv(acc, y.l[i], w.l[k - i]);
+#pragma unroll
+        for (int i = 0; i <= k; i++) mad29_vs(acc, q[i], R29<M>::NEGP261[k - i]);
+        r.l[k] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
+    return r;
+}
+
+// The twiddle pair of mul29_shoup from T = w 2^261 mod p (canonical; the Montgomery form of 32 w,
+// which is how the twiddle tables are first built): w = T 2^-261 mod p (a product by the integer
+// 1, canonicalised) and wq = floor(w 2^261 / p) = (w 2^261 - T) / p, an exact quotient, i.e.
+// (2^261 - T) p^-1 mod 2^261 (a low-half product).
+template <class M>
+EON_HD void shoup_pair29(const F29& T, F29& w, F29& wq) {
+    F29 one;
+#pragma unroll
+    for (int i = 0; i < 9; i++) one.l[i] = i == 0 ? 1u : 0u;
+    w = canon29<M>(mul29<M>(T, one));
+    uint32_t n[9];
+    uint32_t c = 1;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {  // 2^261 - T = (2^261 - 1 - T) + 1
+        const uint32_t v = (M29 - T.l[i]) + c;
+        n[i] = v & M29;
+        c = v >> 29;
+    }
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+#pragma unroll
+        for (int i = 0; i <= k; i++) acc += (uint64_t)n[i] * R29<M>::PINV261[k - i];
+        wq.l[k] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
 }
 
 // a^2 2^-261 mod p (limbs < 2^30, a^2 < 0.99 p 2^261, as mul29): each column's cross products

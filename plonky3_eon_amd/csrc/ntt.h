@@ -19,6 +19,9 @@ enum LoadMode : uint32_t {
 
 constexpr uint32_t NATURAL_IDX = 0xffffffffu;
 
+// words per Shoup-quotient table entry (9 limbs of 29 bits, padded to three 16-B loads)
+constexpr uint32_t TWQ_STRIDE = 12;
+
 // One radix-2 network of size 2^log_m over `width` independent columns.
 //   DIT (dif=false): stages first_stage .. log_m-1 ascending; bit-reversed input -> natural output.
 //   DIF (dif=true):  stages log_m-1 .. first_stage descending; natural input -> bit-reversed output.
@@ -31,7 +34,8 @@ struct NetworkSpec {
     const Fr* src = nullptr;
     Fr* dst = nullptr;
     uint64_t width = 0;
-    const Fr* tw = nullptr;  // stage-concatenated twiddles (forward or inverse)
+    const Fr* tw = nullptr;         // stage-concatenated twiddles (forward or inverse), plain roots
+    const uint32_t* twq = nullptr;  // their Shoup quotients, TWQ_STRIDE words per entry
     uint32_t load_mode = LOAD_DIRECT;
     uint32_t load_param = 0;
     const Fr* load_scale = nullptr;
@@ -89,6 +93,6 @@ inline Fr ntt_scale_form(const Fr& c) { return mul(c, from_u64<FrP>(32)); }
 hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof = nullptr);
 hipError_t launch_powers(Fr* out, uint64_t n, const Fr& base, const Fr& scale, uint32_t rev_log,
                          hipStream_t st);
-hipError_t launch_twiddles(Fr* tw, uint32_t L, const Fr& root_L, hipStream_t st);
+hipError_t launch_twiddles(Fr* tw, uint32_t* twq, uint32_t L, const Fr& root_L, hipStream_t st);
 
 }  // namespace eon

@@ -25,7 +25,8 @@ namespace eon {
 struct PassArgs {
     const Fr* src;
     Fr* dst;
-    const Fr* tw;
+    const Fr* tw;          // plain roots
+    const uint32_t* twq;   // their Shoup quotients (TWQ_STRIDE words per entry)
     const Fr* load_scale;   // indexed by source row, or null
     const Fr* store_scale;  // indexed by output row, or null
     Fr load_const;
@@ -38,6 +39,10 @@ struct PassArgs {
     uint32_t col_tiles;
     uint32_t last;  // the network's last pass: canonical output (earlier passes store values < 2p)
 };
+
+// LDS bytes of one twiddle set (roots or quotients) of nt entries: two 16-B planes and a 4-B one,
+// rounded up to 16 B so the next set's planes stay aligned
+__host__ __device__ constexpr uint32_t tw_set_bytes(uint32_t nt) { return 32u * nt + ((4u * nt + 15u) & ~15u); }
 
 __device__ __forceinline__ Fr gload(const Fr* p) {
     const uint4* q = reinterpret_cast<const uint4*>(p);
@@ -56,11 +61,11 @@ __device__ __forceinline__ void gstore(Fr* p, const Fr& x) {
 
 // ---- the pass kernel ----------------------------------------------------------------------------
 // The tile is held in LDS as 9 x 29-bit limbs (three planes: limbs 0-3, 4-7, 8)
-// and lazy values: the product is mul29 (162 carry-free multiply-adds, no carry captures) against
-// twiddles held as w 2^261 = (32 w) 2^256, i.e. the twiddle tables store the Montgomery form of
-// 32 w (launch_twiddles), so y w 2^256 comes out directly in the radix-2^32 Montgomery form of
-// the product and staging a twiddle is a load and an unpack.  The input / output scalings (coset
-// powers, 1/n) are tables and constants in the same 32 c form, applied with mul29 as well.
+// and lazy values: the butterfly product is Shoup's by the plain root w with its precomputed
+// quotient floor(w 2^261 / p) (mul29_shoup: 143 carry-free multiply-adds, no Montgomery
+// multipliers, output < 3p), so y w 2^256 comes out in the radix-2^32 Montgomery form and staging
+// a twiddle is two loads and an unpack.  The input / output scalings (coset powers, 1/n) are
+// tables and constants in the 32 c form (ntt_scale_form), applied with mul29.
 
 __device__ __forceinline__ void lds_put29(uint4* lo, uint4* hi, uint32_t* top, uint32_t i, const F29& x) {
     lo[i] = make_uint4(x.l[0], x.l[1], x.l[2], x.l[3]);
@@ -109,6 +114,11 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
     uint4* tlo = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + ((36u * ne + 15u) & ~15u));
     uint4* thi = tlo + nt;
     uint32_t* ttop = reinterpret_cast<uint32_t*>(thi + nt);
+    // the Shoup quotients of the same twiddles, three planes again (after the roots' top plane,
+    // 16-B aligned)
+    uint4* qlo = reinterpret_cast<uint4*>(reinterpret_cast<char*>(tlo) + tw_set_bytes(nt));
+    uint4* qhi = qlo + nt;
+    uint32_t* qtop = reinterpret_cast<uint32_t*>(qhi + nt);
 
     const uint32_t s0 = a.s0;
     const uint64_t g = blockIdx.x / a.col_tiles;
@@ -122,7 +132,13 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         const uint32_t l = 31 - __builtin_clz(q);
         const uint32_t r = q - (1u << l);
         const uint64_t s = s0 + l;
-        lds_put29(tlo, thi, ttop, q, unpack29(gload(a.tw + (1ull << s) + low + ((uint64_t)r << s0))));
+        const uint64_t ti = (1ull << s) + low + ((uint64_t)r << s0);
+        lds_put29(tlo, thi, ttop, q, unpack29(gload(a.tw + ti)));
+        const uint4* wq = reinterpret_cast<const uint4*>(a.twq + ti * TWQ_STRIDE);
+        const uint4 q0 = wq[0], q1 = wq[1], q2 = wq[2];
+        qlo[q] = q0;
+        qhi[q] = q1;
+        qtop[q] = q2.x;
     }
 
     for (uint32_t e = threadIdx.x; e < ne; e += T) {
@@ -164,6 +180,11 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         pin29(w);
         return w;
     };
+    auto twq29 = [&](uint32_t q) {
+        F29 w = lds_get29(qlo, qhi, qtop, q);
+        pin29(w);
+        return w;
+    };
     for (uint32_t it = 0; it < k; it++) {
         const uint32_t l = DIF ? (k - 1 - it) : it;
         const uint32_t half = 1u << l;
@@ -181,27 +202,30 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
             // any other (its 29-form is 2^261 mod p), as a per-lane choice would run both paths
             const bool unit = half == 1 && low == 0;
             F29 u, v;
-            F29 w;
-            if (!unit) w = tw29(half + r);
+            F29 w, wq;
+            if (!unit) {
+                w = tw29(half + r);
+                wq = twq29(half + r);
+            }
             if (!DIF) {
-                // DitButterfly (dft/src/butterflies.rs:177-185): (x + w*y, x - w*y).  Lazy: t < 2p
-                // (the product, or y itself at the unit stage, which is the pass's first and sees
-                // loaded values < 2p), so both outputs are below x + 2p -- a pass of k <= 10
-                // stages ends below 22p, far inside mul29's input bound (84p against a twiddle
-                // < 2p); the store brings it back below 2p (reduce_top29)
-                const F29 t = unit ? y : mul29<FrP>(y, w);
+                // DitButterfly (dft/src/butterflies.rs:177-185): (x + w*y, x - w*y).  Lazy: t < 3p
+                // (the Shoup product, or y itself at the unit stage, which is the pass's first and
+                // sees loaded values < 2p), so both outputs are below x + 3p -- a pass of k <= 10
+                // stages ends below 32p, inside the normalised range mul29_shoup takes (any value
+                // < 2^261 = 169p); the store brings it back below 2p (reduce_top29)
+                const F29 t = unit ? y : mul29_shoup<FrP>(y, w, wq);
                 u = add29_norm(x, t);
-                v = sub29<FrP, 2>(x, t);
+                v = sub29<FrP, 3>(x, t);
             } else {
                 // DIF butterfly: (x + y, (x - y) * w).  The pass's inputs are below 2p; the sum is
                 // brought back below 2p by reduce_top29 only at odd stages of the pass, so every
                 // stage sees inputs below 4p: the sum < 8p, the difference x - y + 4p < 8p into
-                // the product (< 2p) -- or kept at the unit stage, which is the pass's last
+                // the Shoup product (< 3p) -- or kept at the unit stage, which is the pass's last
                 // (reduce_top29 at the store)
                 const F29 sum = add29_norm(x, y);
                 u = (it & 1) ? reduce_top29(sum) : sum;
                 const F29 d = sub29<FrP, 4>(x, y);
-                v = unit ? d : mul29<FrP>(d, w);
+                v = unit ? d : mul29_shoup<FrP>(d, w, wq);
             }
             lds_put29(lo, hi, top, i0, u);
             lds_put29(lo, hi, top, i1, v);
@@ -245,6 +269,20 @@ __global__ void k_powers(Fr* out, uint64_t n, Fr base, Fr scale, uint32_t rev_lo
     }
 }
 
+// Every entry T = 32 w (Montgomery form, i.e. w 2^261 mod p) becomes the plain root w, and its
+// Shoup quotient floor(w 2^261 / p) goes to twq (shoup_pair29).
+__global__ void k_tw_shoup(Fr* tw, uint32_t* twq, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    F29 w, wq;
+    shoup_pair29<FrP>(unpack29(gload(tw + i)), w, wq);
+    gstore(tw + i, pack29<FrP>(w));
+    uint4* q = reinterpret_cast<uint4*>(twq + i * TWQ_STRIDE);
+    q[0] = make_uint4(wq.l[0], wq.l[1], wq.l[2], wq.l[3]);
+    q[1] = make_uint4(wq.l[4], wq.l[5], wq.l[6], wq.l[7]);
+    q[2] = make_uint4(wq.l[8], 0u, 0u, 0u);
+}
+
 // tw[2^s + j] = tw[2^(L-1) + (j << (L-1-s))] for s < L-1 (sub-sampling the largest stage).
 __global__ void k_tw_fill_lower(Fr* tw, uint32_t L) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -263,7 +301,7 @@ static hipError_t launch_pass(bool dif, uint32_t log_cb, const PassArgs& a, uint
     uint32_t threads = ne / 2;
     if (threads > max_threads) threads = max_threads;
     if (threads < 64) threads = 64;
-    const size_t lds = (((size_t)ne * 36 + 15) & ~(size_t)15) + ((size_t)1 << a.k) * 36;
+    const size_t lds = (((size_t)ne * 36 + 15) & ~(size_t)15) + 2 * (size_t)tw_set_bytes(1u << a.k);
     dim3 grid((unsigned)(groups * col_tiles));
 #define EON_LAUNCH(D, C) hipLaunchKernelGGL((k_ntt_pass29<D, C>), grid, dim3(threads), lds, st, a)
     switch ((dif ? 4 : 0) + log_cb) {
@@ -291,15 +329,19 @@ hipError_t launch_powers(Fr* out, uint64_t n, const Fr& base, const Fr& scale, u
     return hipGetLastError();
 }
 
-hipError_t launch_twiddles(Fr* tw, uint32_t L, const Fr& root_L, hipStream_t st) {
-    // tw has 2^L entries; tw[0] unused.  Stage L-1 table = 32 root_L^j, j < 2^(L-1) (the 29-limb
-    // product form, see k_ntt_pass29)
+hipError_t launch_twiddles(Fr* tw, uint32_t* twq, uint32_t L, const Fr& root_L, hipStream_t st) {
+    // tw has 2^L entries; tw[0] unused.  Stage L-1 table = root_L^j, j < 2^(L-1), first built as
+    // 32 root_L^j in Montgomery form, then split into the plain roots and their Shoup quotients
     if (L == 0) return hipSuccess;
     hipError_t e = launch_powers(tw + (1ull << (L - 1)), 1ull << (L - 1), root_L, ntt_scale_form(Fr::one()),
                                  NATURAL_IDX, st);
-    if (e != hipSuccess || L == 1) return e;
+    if (e != hipSuccess) return e;
     const uint64_t n = 1ull << (L - 1);
-    hipLaunchKernelGGL(k_tw_fill_lower, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, tw, L);
+    if (L > 1) {
+        hipLaunchKernelGGL(k_tw_fill_lower, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, tw, L);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_tw_shoup, dim3((unsigned)((2 * n + 255) / 256)), dim3(256), 0, st, tw, twq, 2 * n);
     return hipGetLastError();
 }
 
@@ -335,6 +377,7 @@ hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
         a.src = first ? s.src : s.dst;
         a.dst = s.dst;
         a.tw = s.tw;
+        a.twq = s.twq;
         a.width = s.width;
         a.s0 = s0s[i];
         a.k = ks[i];

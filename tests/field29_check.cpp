@@ -83,9 +83,30 @@ static void run(const char* name, int trials) {
     }
 }
 
+// mul29_shoup (the NTT's twiddle product) and shoup_pair29 (its table entries): T < p canonical,
+// y any normalised value < 2^261 (all limbs at 2^29 - 1 on the edge draws)
+static void run_shoup(int trials) {
+    for (int t = 0; t < trials; t++) {
+        const F29 T = random_below<FrP>(1);
+        F29 y;
+        const bool edge = (next64() & 3) == 0;
+        for (int i = 0; i < 9; i++) y.l[i] = edge ? M29 : (uint32_t)(next64() & M29);
+        F29 w, wq;
+        shoup_pair29<FrP>(T, w, wq);
+        printf("fr shoup ");
+        put(T);
+        put(y);
+        put(w);
+        put(wq);
+        put(mul29_shoup<FrP>(y, w, wq));
+        printf("\n");
+    }
+}
+
 int main(int argc, char** argv) {
     const int trials = argc > 1 ? atoi(argv[1]) : 2000;
     run<FqP>("fq", trials);
     run<FrP>("fr", trials);
+    run_shoup(trials);
     return 0;
 }

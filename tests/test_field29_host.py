@@ -1,5 +1,6 @@
 """CPU: the radix-2^29 Montgomery products (plonky3_eon_amd/csrc/field29.h: mul29 with eight
-unmasked reduction multipliers, sqr29, mul29_sum2) compiled for the host and run on operands at
+unmasked reduction multipliers, sqr29, mul29_sum2; and the NTT's Shoup product mul29_shoup with
+its table pair shoup_pair29) compiled for the host and run on operands at
 the edges of their contracts (tests/field29_check.cpp), checked against big integers:
 r = a b 2^-261 mod p, r < 2p, limbs normalised.  The device code is the same C++ (its inline-asm
 multiply-add is the host expression's one-instruction form), so an overflowing column sum or a
@@ -47,7 +48,14 @@ def test_products_at_contract_edges(results):
     seen = set()
     for f, op, *v in results:
         p, rinv = P[f], RINV[f]
-        if op == "mul":
+        if op == "shoup":
+            # twiddle pair from T = w 2^261 mod p, then r = y w mod p with r < 3p, exact
+            (t, _), (y, _), (w, _), (wq, _), (r, rl) = (limbs(x) for x in v[:5])
+            assert w < p and (w << 261) % p == t
+            assert wq == (w << 261) // p
+            assert all(x < (1 << 29) for x in rl)
+            assert r < 3 * p and r % p == (y * w) % p
+        elif op == "mul":
             (a, al), (b, bl) = limbs(v[0]), limbs(v[1])
             assert max(al + bl) < (1 << 30)
             check_out(f, a * b * rinv, v[2])
@@ -59,7 +67,7 @@ def test_products_at_contract_edges(results):
             assert max(bl) < (1 << 31)
             check_out(f, (a * b + c * d) * rinv, v[4])
         seen.add((f, op))
-    assert seen == {(f, o) for f in P for o in ("mul", "sqr", "sum2")}
+    assert seen == {(f, o) for f in P for o in ("mul", "sqr", "sum2")} | {("fr", "shoup")}
     # the widened operands really reach past 2^29 (the case the column bounds are about)
     assert any(max(limbs(v[0])[1]) >= (1 << 29) for f, op, *v in results if op == "mul")
     assert any(max(limbs(v[1])[1]) >= (1 << 30) for f, op, *v in results if op == "sum2")

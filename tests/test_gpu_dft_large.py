@@ -92,3 +92,35 @@ def test_c2_full_size_properties(gpu_ctx):
     for k, col in [(0, 0), (1, 5), (n + 3, 63), ((n << b) - 1, 17)]:
         pt = C.fr_mul(gen(), C.fr_pow(g, k))
         np.testing.assert_array_equal(lh[k, col], C.eval_poly_col(ch, col, pt))
+
+
+# p - 1 as raw limbs: the largest canonical representation, the worst case of the lazy NTT bounds
+# (DIT outputs grow by < 3p per stage, DIF sums are reduced every other stage)
+P_MINUS_1 = np.array([0x43E1F593F0000000, 0x2833E84879B97091, 0xB85045B68181585D, 0x30644E72E131A029],
+                     dtype=np.uint64)
+
+
+@pytest.mark.parametrize("pattern", ["all_max", "alternating", "max_rows_then_random"])
+@pytest.mark.parametrize("log_h,w", [(12, 8), (11, 3), (15, 1)])
+def test_extreme_inputs_vs_c_oracle(gpu_ctx, log_h, w, pattern):
+    n = 1 << log_h
+    x = np.zeros((n, w, 4), dtype=np.uint64)
+    if pattern == "all_max":
+        x[:] = P_MINUS_1
+    elif pattern == "alternating":
+        x[::2] = P_MINUS_1
+    else:
+        x[:] = C.random_fr(3 * log_h + w, n * w).reshape(n, w, 4)
+        x[: n // 2] = P_MINUS_1
+    d = Radix2Dit(gpu_ctx)
+    np.testing.assert_array_equal(d.dft_batch(x), C.dft_batch(x))
+    np.testing.assert_array_equal(d.idft_batch(x), C.idft_batch(x))
+    np.testing.assert_array_equal(d.coset_dft_batch(x, gen()), C.coset_dft_batch(x, gen()))
+    np.testing.assert_array_equal(d.coset_idft_batch(x, gen()), C.coset_idft_batch(x, gen()))
+    np.testing.assert_array_equal(Radix2DitParallel(gpu_ctx).dft_batch(x).storage, C.r2dp_dft_batch(x))
+    for b in (1, 2):
+        np.testing.assert_array_equal(d.coset_lde_batch(x, b, gen()), C.coset_lde_batch(x, b, gen()))
+        np.testing.assert_array_equal(Radix2DitParallel(gpu_ctx).coset_lde_batch(x, b, gen()).storage,
+                                      C.r2dp_coset_lde_batch(x, b, gen()))
+        padded = np.concatenate([x, np.zeros(((n << b) - n, w, 4), dtype=np.uint64)])
+        np.testing.assert_array_equal(d.coset_dft_padded_batch(x, b, gen()), C.coset_dft_batch(padded, gen()))

@@ -9,7 +9,8 @@
 //                         dft_batch's (dft/src/traits.rs:61) on the whole column.
 //   eon_msm_sharded_dev   one MSM split by contiguous term range: a full Pippenger per rank
 //                         (msm.hip), an all-gather of the `world` affine partials, their sum by
-//                         EC additions on the host (a handful of points; RCCL cannot add them).
+//                         EC additions on the device (k_sum_partials, in rank order; RCCL has no
+//                         elliptic-curve reduction op), so every rank returns the same bytes.
 #include <cstring>
 #include <vector>
 

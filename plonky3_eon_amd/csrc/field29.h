@@ -383,6 +383,23 @@ EON_HD void shoup_pair29(const F29& T, F29& w, F29& wq) {
     }
 }
 
+// a - q p with q = floor(a_8 / (p_8 + 1)) (a normalised, any value < 2^261): q p <= a_8 2^232
+// <= a, and a - q p < p + (q + 1) 2^232 < 2p (q <= 169 for Fr, 2^232 < p / 3.1e6) -- one
+// small-quotient step instead of a chain of conditional subtractions, so lazy values can grow
+template <class M>
+EON_HD F29 reduce_top29(const F29& a) {
+    const uint32_t q = a.l[8] / (R29<M>::P[8] + 1);
+    F29 r;
+    int64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        const int64_t t = (int64_t)a.l[i] - (int64_t)q * R29<M>::P[i] + c;
+        r.l[i] = (uint32_t)t & M29;
+        c = t >> 29;  // arithmetic
+    }
+    return r;
+}
+
 // a^2 2^-261 mod p (limbs < 2^30, a^2 < 0.99 p 2^261, as mul29): each column's cross products
 // once, summed apart and doubled by a shift (45 instead of 81 limb products; cross sums < 2^62)
 template <class M, int U = 8>

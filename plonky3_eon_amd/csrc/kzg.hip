@@ -9,6 +9,8 @@
 //   k_horner_apply   per (block, column): the local recurrence again from carry_b, writing q
 // Two mulmods per coefficient; threads = (n / BL) x width, adjacent threads = adjacent columns.
 #include "context.h"
+#include "field29.h"
+#include "ntt.h"
 
 #include <algorithm>
 
@@ -85,22 +87,30 @@ struct Pts {
     Fr z[MAX_PTS];
 };
 
-__global__ void k_eval_block(const Fr* c, uint64_t n, uint32_t width, Pts zs, uint32_t np, Fr* totals) {
+// the points as Shoup multipliers (plain root z and floor(z 2^261 / p), field29.h mul29_shoup):
+// r <- c + z r per coefficient is then 143 multiply-adds with no Montgomery multipliers, the
+// running value kept lazy (< 4p) in 29-bit limbs
+struct PtsShoup {
+    F29 w[MAX_PTS], q[MAX_PTS];
+};
+
+__global__ void k_eval_block(const Fr* c, uint64_t n, uint32_t width, PtsShoup zs, uint32_t np, Fr* totals) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nblk = (n + BL - 1) / BL;
     if (t >= nblk * width) return;
     const uint32_t col = (uint32_t)(t % width);
     const uint64_t b = t / width;
     const uint64_t lo = b * BL, hi = lo + BL < n ? lo + BL : n;
-    Fr r[MAX_PTS];
-    for (uint32_t p = 0; p < MAX_PTS; p++) r[p] = Fr::zero();
+    F29 r[MAX_PTS];
+    for (uint32_t p = 0; p < MAX_PTS; p++) r[p] = unpack29(Fr::zero());
     for (uint64_t i = hi; i-- > lo;) {
-        const Fr x = ld(c + i * width + col);
+        const F29 x = unpack29(ld(c + i * width + col));  // canonical
 #pragma unroll
         for (uint32_t p = 0; p < MAX_PTS; p++)
-            if (p < np) r[p] = add(x, mul(zs.z[p], r[p]));
+            if (p < np) r[p] = add29_norm(x, mul29_shoup<FrP>(r[p], zs.w[p], zs.q[p]));  // < p + 3p
     }
-    for (uint32_t p = 0; p < np; p++) st(totals + ((uint64_t)p * nblk + b) * width + col, r[p]);
+    for (uint32_t p = 0; p < np; p++)
+        st(totals + ((uint64_t)p * nblk + b) * width + col, pack29<FrP>(canon29<FrP>(reduce_top29<FrP>(r[p]))));
 }
 
 // per (point, chunk of CH blocks, column): P_q = sum_{b in chunk} T_b Z^(b - q CH)
@@ -152,15 +162,18 @@ int eon_eval_columns_dev(eon_ctx* ctx, const eon_fr* coeffs, uint64_t rows, uint
         for (uint32_t p0 = 0; p0 < npoints; p0 += MAX_PTS) {
             const uint32_t np = std::min<uint32_t>(MAX_PTS, npoints - p0);
             Pts zs{}, zbl{}, zch{};
+            PtsShoup zsh{};
             for (uint32_t p = 0; p < np; p++) {
                 zs.z[p] = fr_from_abi(points + p0 + p);
                 if (!fr_is_canonical(zs.z[p])) return Status::err(EON_E_ARG, "point is not a canonical Fr");
                 zbl.z[p] = pow_u64(zs.z[p], BL);
                 zch.z[p] = pow_u64(zbl.z[p], CH);
+                // z 2^261 mod p (the Montgomery form of 32 z) -> plain z and its Shoup quotient
+                shoup_pair29<FrP>(unpack29(ntt_scale_form(zs.z[p])), zsh.w[p], zsh.q[p]);
             }
             ctx->prof.begin("k_eval_block", rows * width * 32ull, ctx->stream);
             hipLaunchKernelGGL(k_eval_block, dim3((unsigned)((nblk * width + 127) / 128)), dim3(128), 0, ctx->stream,
-                               c, rows, width, zs, np, totals);
+                               c, rows, width, zsh, np, totals);
             ctx->prof.end(ctx->stream);
             hipLaunchKernelGGL(k_eval_chunks, dim3((unsigned)((np * nq * width + 127) / 128)), dim3(128), 0,
                                ctx->stream, totals, nblk, width, zbl, np, part);

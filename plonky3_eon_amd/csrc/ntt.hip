@@ -82,22 +82,6 @@ __device__ __forceinline__ F29 lds_get29(const uint4* lo, const uint4* hi, const
     return x;
 }
 
-// a - q p with q = floor(a_8 / (p_8 + 1)) (a normalised, any value < 2^261): q p <= a_8 2^232 <= a,
-// and a - q p < p + (q + 1) 2^232 < 2p (q <= 169, 2^232 < p / 3.1e6) -- one small-quotient step
-// instead of a chain of conditional subtractions, so the butterflies can let values grow
-__device__ __forceinline__ F29 reduce_top29(const F29& a) {
-    const uint32_t q = a.l[8] / (R29<FrP>::P[8] + 1);
-    F29 r;
-    int64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 9; i++) {
-        const int64_t t = (int64_t)a.l[i] - (int64_t)q * R29<FrP>::P[i] + c;
-        r.l[i] = (uint32_t)t & M29;
-        c = t >> 29;  // arithmetic
-    }
-    return r;
-}
-
 template <bool DIF, int LOG_CB>
 __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
     constexpr uint32_t CB = 1u << LOG_CB;
@@ -223,7 +207,7 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
                 // the Shoup product (< 3p) -- or kept at the unit stage, which is the pass's last
                 // (reduce_top29 at the store)
                 const F29 sum = add29_norm(x, y);
-                u = (it & 1) ? reduce_top29(sum) : sum;
+                u = (it & 1) ? reduce_top29<FrP>(sum) : sum;
                 const F29 d = sub29<FrP, 4>(x, y);
                 v = unit ? d : mul29_shoup<FrP>(d, w, wq);
             }
@@ -240,7 +224,7 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         const uint64_t col = col0 + c;
         if (col < width) {
             // below 2p (fits 256 bits) between passes, canonical after the last one
-            F29 r = reduce_top29(lds_get29(lo, hi, top, e));
+            F29 r = reduce_top29<FrP>(lds_get29(lo, hi, top, e));
             if (a.store_scale) r = mul29<FrP>(r, unpack29(ld_pinned(a.store_scale + p)));
             gstore(a.dst + p * width + col, pack29<FrP>(a.last ? canon29<FrP>(r) : r));
         }

@@ -456,6 +456,89 @@ class QuotientWorkload:
                 "sample": f"C restatement of quotient_values on {rows} of {q} rows ({dt:.2f} s), scaled linearly"}
 
 
+class VerifyWorkload:
+    """SURVEY.md 8(f) N4: KzgPcs::verify's verify_batch (kzg/src/util.rs:245-292) of every opening
+    of the configs[3] proof -- 1312 trace columns at zeta and zeta h plus the quotient chunks at
+    zeta, 2626 (commitment, witness, value, point) quadruples -- on the GPU
+    (eon_kzg_verify_batch: the product of the 2 x 2626 pairings, merged per opening point by
+    bilinearity into 3 pairs, Miller loops and one final exponentiation).  The proof is made once
+    by the configs[3] prove (untimed); the openings are host arrays, as a verifier receives them."""
+
+    latency_bound = True
+
+    def __init__(self, args, ctx, dev, rank):
+        from oracle import pyoracle as O
+        from plonky3_eon_amd import verify as GV
+
+        args.transcript = "fs"
+        pw = ProveWorkload(args, ctx, dev, rank)
+        from plonky3_eon_amd.native import Challenger, Poseidon2Constants, prove_native
+
+        proof = prove_native(pw.air, pw.pcs, pw.trace, None, None,
+                             challenger=Challenger(Poseidon2Constants(*pw.ch_consts)))
+        self.GV, self.ctx = GV, ctx
+        log_n = args.log_trace
+
+        def fr_l(x):
+            return np.array(O.int_to_limbs(O.to_mont(x % O.P)), dtype=np.uint64)
+
+        tc = np.asarray(proof.trace_commit[0]).reshape(-1, 8)
+        tr, qo = proof.opened
+        zn = proof.zeta * O.two_adic_generator(log_n) % O.P
+        com, wit, val, pts = [], [], [], []
+        for p, z in enumerate((proof.zeta, zn)):
+            com.append(tc)
+            wit.append(np.asarray(tr.witnesses[0][p]).reshape(-1, 8))
+            val.append(np.asarray(tr.values[0][p]).reshape(-1, 4))
+            pts.append(np.tile(fr_l(z), (tc.shape[0], 1)))
+        for c, qc in enumerate(proof.quotient_commit):
+            com.append(np.asarray(qc).reshape(1, 8))
+            wit.append(np.asarray(qo.witnesses[c][0]).reshape(1, 8))
+            val.append(np.asarray(qo.values[c][0]).reshape(1, 4))
+            pts.append(fr_l(proof.zeta)[None])
+        self.com, self.wit, self.val, self.pts = (np.ascontiguousarray(np.concatenate(a), dtype=np.uint64)
+                                                  for a in (com, wit, val, pts))
+        self.n = self.com.shape[0]
+        self.g2a = GV.g2_mul(12345, ctx=ctx)
+        self.alg_bytes_per_step = self.n * (64 + 64 + 32 + 32)
+        del pw
+
+    def step(self):
+        if self.GV.verify_batch(self.com, self.wit, self.val, self.pts, self.g2a, ctx=self.ctx) is not True:
+            raise SystemExit("verify_batch rejected the configs[3] proof")
+
+    def describe(self, world):
+        return (f"N4: KzgPcs::verify_batch of the configs[3] proof's {self.n} openings (1312 trace columns at "
+                f"zeta and zeta h, quotient chunks at zeta) on the GPU: pairings merged per opening point",
+                world, self.n, "single")
+
+    def throughput(self, world, ms):
+        return {"openings_per_s": round(self.n / (ms * 1e-3), 1)}, None
+
+    def cpu_baseline(self):
+        # the restated verify_batch (oracle/pairing.py: 2 Miller loops per opening, one final
+        # exponentiation, pure Python) on 2 and 4 openings, extended linearly to all of them
+        from oracle import pairing as E
+        from oracle import pyoracle as O
+        from oracle import verify_oracle as V
+
+        def pt(row):
+            return O.g1_from_bytes(np.ascontiguousarray(row, dtype=np.uint64).reshape(8).tobytes())
+
+        ops = [(pt(self.com[i]), pt(self.wit[i]), V.fr_int(self.val[i]), V.fr_int(self.pts[i])) for i in range(4)]
+        g2a = E.g2_alpha(12345)
+        ts = {}
+        for k in (2, 4):
+            t0 = time.perf_counter()
+            assert E.verify_batch(ops[:k], g2a)
+            ts[k] = time.perf_counter() - t0
+        per = (ts[4] - ts[2]) / 2
+        fixed = max(ts[2] - 2 * per, 0.0)
+        return {"value": round((fixed + per * self.n) * 1e3, 1), "unit": "ms", "cores": 1, "kind": "port",
+                "sample": f"oracle/pairing.py verify_batch on 2 and 4 openings ({ts[2]:.2f} / {ts[4]:.2f} s), "
+                          f"linear in the openings to {self.n}"}
+
+
 class FourStepWorkload:
     """configs[4] (i): one forward DFT of 2^log_n Fr (natural in / natural out semantics) as a
     four-step N1 x N2 transform split over the ranks, one RCCL all_to_all for the transpose
@@ -578,7 +661,8 @@ def make_parser() -> argparse.ArgumentParser:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default: 3 (prove), 10 (lde, msm)")
     ap.add_argument("--warmup", type=int, default=None, help="default: 1 (prove), 3 (lde, msm)")
-    ap.add_argument("--workload", choices=["prove", "lde", "msm", "ntt4", "msm-shard", "quotient"], default="prove")
+    ap.add_argument("--workload", choices=["prove", "lde", "msm", "ntt4", "msm-shard", "quotient", "verify"],
+                    default="prove")
     ap.add_argument("--air", choices=["fused", "generic"], default="fused",
                     help="prove / quotient: the Poseidon2-AIR's quotient through the fused kernel or the "
                          "generic compiled constraint program")
@@ -671,7 +755,8 @@ def main() -> int:
     ctx = Context(local_dev)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     wl = {"lde": LdeWorkload, "msm": MsmWorkload, "prove": ProveWorkload, "ntt4": FourStepWorkload,
-          "msm-shard": MsmShardWorkload, "quotient": QuotientWorkload}[args.workload](args, ctx, dev, rank)
+          "msm-shard": MsmShardWorkload, "quotient": QuotientWorkload,
+          "verify": VerifyWorkload}[args.workload](args, ctx, dev, rank)
 
     if args.serial:
         ctx.set_serial(True)
@@ -774,6 +859,11 @@ def main() -> int:
         if "valu" not in roof:
             roof["valu"] = dict(roof["valu_whole_step"], binding=True,
                                 peak_mulmod_per_s=MULMOD_PEAK_PER_S)
+    if getattr(wl, "latency_bound", False):
+        # a handful of pairs: single-thread Miller loops and final exponentiation chains, bound by
+        # their dependent-instruction latency, not by HBM or the VALU throughput
+        roof["bound"] = "latency"
+        roof["hbm_frac"] = roof["frac"]
     if "valu" in roof:
         # the binding resource is the VALU issue of the 256-bit Montgomery products (SURVEY.md
         # 8(d)); achieved / peak / frac stay the HBM figures of section 8(d)'s algorithmic bytes

@@ -272,9 +272,13 @@ Status pair_product(eon_ctx* ctx, const G1Affine* P, const G2Affine* Q, uint32_t
     DevBuf f, res;
     EON_HIP(f.ensure((size_t)std::max<uint32_t>(m, 1) * sizeof(Fq12)));
     EON_HIP(res.ensure(sizeof(Fq12) + 16));
+    ctx->prof.begin("k_miller", (uint64_t)m * (64 + 128 + 384), ctx->stream);
     if (m) hipLaunchKernelGGL(k_miller, dim3((m + 63) / 64), dim3(64), 0, ctx->stream, P, Q, m, f.as<Fq12>());
+    ctx->prof.end(ctx->stream);
+    ctx->prof.begin("k_final_exp", (uint64_t)m * 384 + 384, ctx->stream);
     hipLaunchKernelGGL(k_final_exp, dim3(1), dim3(64), 0, ctx->stream, f.as<Fq12>(), m, hard_exp(), res.as<Fq12>(),
                        reinterpret_cast<uint32_t*>(res.as<char>() + sizeof(Fq12)));
+    ctx->prof.end(ctx->stream);
     EON_HIP(hipGetLastError());
     struct {
         Fq12 v;
@@ -411,11 +415,16 @@ int eon_kzg_verify_batch(eon_ctx* ctx, const eon_g1_affine* commitments, const e
         EON_HIP(hipMemcpyAsync(dord.p, ord.data(), n * 4, hipMemcpyHostToDevice, st));
         EON_HIP(hipMemcpyAsync(dgs.p, gs.data(), (G + 1) * 4, hipMemcpyHostToDevice, st));
         EON_HIP(hipMemcpyAsync(dz.p, zs.data(), G * sizeof(Fr), hipMemcpyHostToDevice, st));
+        // algorithmic bytes: each opening's commitment, witness, value and point read once
+        ctx->prof.begin("k_vb_sums", n * (64 + 64 + 32 + 32), st);
         hipLaunchKernelGGL(k_vb_sums, dim3(G + 1), dim3(VB_THREADS), 0, st, dc.as<G1Affine>(), dw.as<G1Affine>(),
                            dv.as<Fr>(), dord.as<uint32_t>(), dgs.as<uint32_t>(), G, (uint32_t)n, dsums.as<G1Xyzz>(),
                            dvsum.as<Fr>());
+        ctx->prof.end(st);
+        ctx->prof.begin("k_vb_pairs", (uint64_t)(G + 1) * (96 + 192), st);
         hipLaunchKernelGGL(k_vb_pairs, dim3((G + 1 + 63) / 64), dim3(64), 0, st, dsums.as<G1Xyzz>(), dvsum.as<Fr>(),
                            dz.as<Fr>(), G, ga, dP.as<G1Affine>(), dQ.as<G2Affine>());
+        ctx->prof.end(st);
         EON_HIP(hipGetLastError());
         bool one = false;
         EON_TRY(pair_product(ctx, dP.as<G1Affine>(), dQ.as<G2Affine>(), G + 1, nullptr, &one));

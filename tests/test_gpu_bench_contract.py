@@ -1,6 +1,7 @@
 """GPU: bench.py keeps its output contract (the driver parses it): exactly one JSON line with the
 required keys, `roofline` (bound / achieved / peak / unit / frac / traffic, frac = achieved / peak)
-and `cpu_baseline` (value / unit / cores / kind / sample).  Runs the quick configs[2] workload."""
+and `cpu_baseline` (value / unit / cores / kind / sample).  Runs the quick configs[2] workload and
+a small GPU verify_batch (N4; its single-thread pairing chains report the bound "latency")."""
 
 import json
 import subprocess
@@ -13,8 +14,10 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
 
 
-def test_bench_json_contract():
-    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--workload", "msm", "--steps", "3", "--warmup", "1"],
+@pytest.mark.parametrize("extra", [["--workload", "msm"],
+                                   ["--workload", "verify", "--log-trace", "6", "--vector-len", "1"]])
+def test_bench_json_contract(extra):
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), *extra, "--steps", "3", "--warmup", "1"],
                          cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
@@ -27,7 +30,7 @@ def test_bench_json_contract():
     assert d["value"] > 0 and d["higher_is_better"] is False and d["scaling"] in ("weak", "strong")
     assert "workload" in d["config"]
     r = d["roofline"]
-    assert r["bound"] in ("hbm", "mfma", "valu") and r["unit"] in ("GB/s", "TFLOP/s")
+    assert r["bound"] in ("hbm", "mfma", "valu", "latency") and r["unit"] in ("GB/s", "TFLOP/s")
     if r["bound"] == "valu":  # the binding integer roofline beside the HBM figures
         v = r["valu"]
         assert v["unit"] == "mulmod/s" and 0 < v["frac"] <= 1.2 and r["hbm_frac"] == r["frac"]

@@ -56,6 +56,11 @@ MULMOD_PEAK_PER_S = 1.80e11
 FR_P = [0x43E1F593F0000001, 0x2833E84879B97091, 0xB85045B68181585D, 0x30644E72E131A029]
 
 
+def _sig(x: float, n: int = 4) -> float:
+    """x to n significant figures (a latency-bound workload's GB/s is far below 0.01)."""
+    return float(f"{x:.{n}g}")
+
+
 def synthetic_fr(rows: int, cols: int, seed: int) -> np.ndarray:
     """Uniform-ish canonical Fr Montgomery limbs: the top limb is drawn below P's top limb, so
     every value is < P (synthetic data; the distribution is irrelevant to the kernels' cost)."""
@@ -812,10 +817,10 @@ def main() -> int:
     roof = {
         "bound": "hbm",
         "kernel": kname,
-        "achieved": round(achieved, 2),
+        "achieved": _sig(achieved),
         "peak": HBM_PEAK_GBPS,
         "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBPS, 4),
+        "frac": _sig(achieved / HBM_PEAK_GBPS),
         "traffic": None,
         "avg_launch_ms": round(avg_ms, 4),
         "alg_bytes_per_launch": int(bytes_per_launch),
@@ -833,8 +838,8 @@ def main() -> int:
             sum(v["launches"] for v in prof.values()) // prof_steps, ", ".join(sorted(prof)))
         roof["avg_launch_ms"] = round(gpu_total_ms, 4)
         roof["alg_bytes_per_launch"] = int(step_bytes)
-        roof["achieved"] = round(step_bytes / (gpu_total_ms * 1e-3) / 1e9, 2)
-        roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBPS, 4)
+        roof["achieved"] = _sig(step_bytes / (gpu_total_ms * 1e-3) / 1e9)
+        roof["frac"] = _sig(step_bytes / (gpu_total_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS)
         roof["kernel_ms_per_step"] = round(gpu_total_ms, 3)
     if kst.get("design_bytes"):
         # what the kernel's access pattern moves (fixed-base table gathers) vs section 8(d)'s bytes

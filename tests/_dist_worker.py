@@ -402,7 +402,15 @@ def main():
 
     mode, out = sys.argv[1], sys.argv[2]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # EON_T_BACKEND=nccl: RCCL on device buffers (one rank per GPU, so a one-GPU box runs world 1
+    # only) -- the backend bench.py uses at N > 1; gloo ranks may share one GPU
+    if os.environ.get("EON_T_BACKEND", "gloo") == "nccl":
+        import torch
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda:0"))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         fn = {"cpu": run_cpu, "gpu": run_gpu, "a2a": run_a2a, "fourstep": run_fourstep,
               "msmshard": run_msmshard, "native": run_native, "openshard": run_openshard,

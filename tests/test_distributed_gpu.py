@@ -44,3 +44,14 @@ def test_sharded_opening_bases(world):
     rows (world 3: uneven slices)."""
     res = run_world("openshard", world, timeout=900)
     assert all(r["ok"] for r in res), [r["why"] for r in res]
+
+
+@pytest.mark.parametrize("mode,env", [("native", {"EON_T_LOG_N": "5", "EON_T_VL": "4"}), ("fourstep", {}),
+                                      ("msmshard", {}), ("openshard", {})])
+def test_rccl_process_group_world1(mode, env):
+    """The same exchanges over torch.distributed's nccl backend (RCCL, device buffers), the
+    backend bench.py runs at N > 1 GPUs: all_gather_into_tensor / all_to_all_single through
+    TorchCollective.  RCCL takes one rank per GPU, so one box runs world 1; the N-rank exchange
+    layouts are the gloo tests above."""
+    res = run_world(mode, 1, timeout=900, extra_env=dict(env, EON_T_BACKEND="nccl"))
+    assert all(r["ok"] for r in res), [r["why"] for r in res]

@@ -41,18 +41,25 @@ def test_bench_json_contract(extra):
     assert c["value"] > 0 and c["cores"] >= 1 and c["kind"] in ("reference", "port") and c["sample"]
 
 
-def test_bench_self_launch_two_ranks():
-    """`bench.py --gpus 2` with no launcher starts its own two ranks (here gloo ranks sharing cuda:0,
-    EON_BENCH_BACKEND=gloo EON_BENCH_ONE_DEVICE=1) and rank 0 prints n_gpus 2."""
+@pytest.mark.parametrize("gpus,extra", [
+    (2, ["--workload", "ntt4", "--log-ntt", "16"]),
+    # the driver's multi-GPU configuration of the headline (lane-sharded prove), small trace
+    (2, ["--log-trace", "8", "--vector-len", "2"]),
+    (4, ["--log-trace", "8", "--vector-len", "8"]),
+])
+def test_bench_self_launch_ranks(gpus, extra):
+    """`bench.py --gpus N` with no launcher starts its own N ranks (here gloo ranks sharing cuda:0,
+    EON_BENCH_BACKEND=gloo EON_BENCH_ONE_DEVICE=1) and rank 0 prints n_gpus N."""
     import os
 
     env = dict(os.environ, EON_BENCH_BACKEND="gloo", EON_BENCH_ONE_DEVICE="1")
     env.pop("WORLD_SIZE", None)
-    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--workload", "ntt4", "--log-ntt", "16",
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(gpus), *extra,
                           "--steps", "2", "--warmup", "1"], cwd=ROOT, capture_output=True, text=True, timeout=240,
                          env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["cpu_baseline"] is None
+    assert d["n_gpus"] == gpus and d["steps"] == 2 and d["cpu_baseline"] is None
+    assert d["value"] > 0 and d["roofline"]["achieved"] > 0

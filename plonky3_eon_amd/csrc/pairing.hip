@@ -14,9 +14,11 @@
 //                 sum C_i and sum v_i (XYZZ partial sums per thread, LDS tree)
 //   k_vb_pairs    the merged pairs: P_0 = sum C - (sum v) G1 with Q_0 = G2, P_z = -sum W with
 //                 Q_z = [alpha]G2 - z G2 (Jacobian double-and-add over Fq2, then affine)
-//   k_miller      one thread per pair: f_{6x+2,Q}(P) and the two Frobenius-twisted lines
+//   k_miller      one thread per pair: f_{6x+2,Q}(P) and the two Frobenius-twisted lines, T in
+//                 projective coordinates (no inversions; lines scaled by Fq2 factors)
 //   k_final_exp   product of the Miller values, easy part f^((q^6-1)(q^2+1)), hard part
-//                 f^((q^4-q^2+1)/r) by square-and-multiply, and the test against 1
+//                 f^((q^4-q^2+1)/r) from f^x, f^(x^2), f^(x^3) and Frobenius maps, and the test
+//                 against 1
 #include <algorithm>
 #include <map>
 #include <vector>
@@ -28,53 +30,81 @@ using namespace eon;
 
 namespace {
 
-struct HardExp {
-    uint32_t w[pc::HARD_EXP_WORDS];
+// ---- Miller loop --------------------------------------------------------------------------------
+//
+// T runs in homogeneous projective coordinates on the twist (x = X / Z, y = Y / Z), so no step
+// inverts.  Each line is the affine line through T and A, untwisted and evaluated at P,
+//   l = -yp + (lambda xp) w + (y_T - lambda x_T) w^3,
+// times a factor in Fq2 (2 Y Z for a tangent, X - x_A Z for a chord): Fq2 lies in Fq6, whose
+// nonzero elements the easy part of the final exponentiation sends to 1, so the pairing -- the Gt
+// value after the final exponentiation -- is the affine loop's exactly (Costello-Lange-Naehrig;
+// Aranha et al. 2011, the D-type twist forms).
+
+struct G2Proj {
+    Fq2 X, Y, Z;
 };
 
-// ---- Miller loop --------------------------------------------------------------------------------
-
-// The line through T and A (tangent when equal, vertical when A = -T) on the twist, untwisted
-// and evaluated at P = (xp, yp): with lambda the twist slope,
-//   l = -yp + (lambda xp) w + (y_T - lambda x_T) w^3,   vertical: l = xp - x_T w^2.
-// Also returns T + A (affine; the Miller loop never meets the identity before its last line).
-__device__ __noinline__ Fq12 line_and_step(G2Affine& T, const G2Affine& A, const Fq& xp, const Fq& yp) {
+// tangent at T: T <- 2T, returns 2YZ times the affine tangent line
+// (the published X3 = XY/2 (B - F), Y3 = ((B + F)/2)^2 - 3E^2, Z3 = B H, all scaled by 4: no halving)
+__device__ __noinline__ Fq12 dbl_line(G2Proj& T, const Fq& xp, const Fq& yp) {
+    const Fq2 A = f2_dbl(f2_mul(T.X, T.Y));              // 2 X Y
+    const Fq2 B = f2_sqr(T.Y), C = f2_sqr(T.Z);
+    const Fq2 E = f2_mul(f2_add(f2_dbl(C), C), f2_c(pc::TWIST_B));  // 3 b' Z^2
+    const Fq2 F = f2_add(f2_dbl(E), E);
+    const Fq2 G = f2_add(B, F);
+    const Fq2 H = f2_sub(f2_sqr(f2_add(T.Y, T.Z)), f2_add(B, C));   // 2 Y Z
+    const Fq2 J = f2_sqr(T.X);
+    const Fq2 E2 = f2_sqr(E);
     Fq12 l = {f6_zero(), f6_zero()};
-    Fq2 lam;
-    if (!f2_eq(T.x, A.x)) {
-        lam = f2_mul(f2_sub(A.y, T.y), f2_inv(f2_sub(A.x, T.x)));
-    } else if (f2_eq(T.y, A.y)) {
-        const Fq2 x2 = f2_sqr(T.x);
-        lam = f2_mul(f2_add(f2_dbl(x2), x2), f2_inv(f2_dbl(T.y)));
-    } else {
-        l.c0.c0 = {xp, Fq::zero()};
-        l.c0.c1 = f2_neg(T.x);
-        T = {f2_zero(), f2_zero()};
+    l.c0.c0 = f2_mul_fq(f2_neg(H), yp);                  // -2YZ yp
+    l.c1.c0 = f2_mul_fq(f2_add(f2_dbl(J), J), xp);        // 3 X^2 xp (= 2YZ lambda xp)
+    l.c1.c1 = f2_sub(E, B);                               // 2YZ (y - lambda x) = 3 b' Z^2 - Y^2
+    const Fq2 E2x3 = f2_add(f2_dbl(E2), E2);
+    T.X = f2_mul(A, f2_sub(B, F));
+    T.Y = f2_sub(f2_sqr(G), f2_dbl(f2_dbl(E2x3)));
+    T.Z = f2_dbl(f2_dbl(f2_mul(B, H)));
+    return l;
+}
+
+// chord through T and the affine A: T <- T + A, returns (X - x_A Z) times the affine line
+// (vertical when x_T = x_A: Z (xp - x_T w^2), and T becomes the identity)
+__device__ __noinline__ Fq12 add_line(G2Proj& T, const G2Affine& A, const Fq& xp, const Fq& yp) {
+    const Fq2 theta = f2_sub(T.Y, f2_mul(A.y, T.Z));    // Y - y_A Z
+    const Fq2 lam = f2_sub(T.X, f2_mul(A.x, T.Z));      // X - x_A Z
+    Fq12 l = {f6_zero(), f6_zero()};
+    if (f2_is_zero(lam)) {
+        if (f2_is_zero(theta)) return dbl_line(T, xp, yp);  // T = A
+        l.c0.c0 = f2_mul_fq(T.Z, xp);
+        l.c0.c1 = f2_neg(T.X);
+        T = {f2_one(), f2_one(), f2_zero()};
         return l;
     }
-    l.c0.c0 = {neg(yp), Fq::zero()};
-    l.c1.c0 = f2_mul_fq(lam, xp);
-    l.c1.c1 = f2_sub(T.y, f2_mul(lam, T.x));
-    const Fq2 x3 = f2_sub(f2_sub(f2_sqr(lam), T.x), A.x);
-    const Fq2 y3 = f2_sub(f2_mul(lam, f2_sub(T.x, x3)), T.y);
-    T = {x3, y3};
+    const Fq2 C = f2_sqr(theta), D = f2_sqr(lam);
+    const Fq2 E = f2_mul(lam, D), F = f2_mul(T.Z, C), G = f2_mul(T.X, D);
+    const Fq2 H = f2_sub(f2_add(E, F), f2_dbl(G));
+    l.c0.c0 = f2_mul_fq(f2_neg(lam), yp);                        // -lambda' yp
+    l.c1.c0 = f2_mul_fq(theta, xp);                              // theta xp (= lambda' slope xp)
+    l.c1.c1 = f2_sub(f2_mul(lam, A.y), f2_mul(theta, A.x));      // lambda' y_A - theta x_A
+    T.X = f2_mul(lam, H);
+    T.Y = f2_sub(f2_mul(theta, f2_sub(G, H)), f2_mul(E, T.Y));
+    T.Z = f2_mul(T.Z, E);
     return l;
 }
 
 __device__ __noinline__ Fq12 miller_loop(const G1Affine& p, const G2Affine& q) {
     if (is_inf(p) || g2_is_inf(q)) return f12_one();
     Fq12 f = f12_one();
-    G2Affine T = q;
+    G2Proj T = {q.x, q.y, f2_one()};
     for (int b = 63; b >= 0; b--) {  // 6x + 2 below its top bit, MSB first
-        f = f12_mul(f12_sqr(f), line_and_step(T, T, p.x, p.y));
-        if ((pc::ATE_LOOP_LOW >> b) & 1) f = f12_mul(f, line_and_step(T, q, p.x, p.y));
+        f = f12_mul(f12_sqr(f), dbl_line(T, p.x, p.y));
+        if ((pc::ATE_LOOP_LOW >> b) & 1) f = f12_mul(f, add_line(T, q, p.x, p.y));
     }
     // Q1 = pi(Q), -Q2 = -pi^2(Q) on the twist: pi(x, y) = (conj(x) g_x, conj(y) g_y),
     // pi^2(x, y) = (x g2_x, -y)
     const G2Affine q1 = {f2_mul(f2_conj(q.x), f2_c(pc::TWIST_FROB_X)), f2_mul(f2_conj(q.y), f2_c(pc::TWIST_FROB_Y))};
     const G2Affine nq2 = {f2_mul_fq(q.x, fq_c(pc::TWIST_FROB2_X)), q.y};
-    f = f12_mul(f, line_and_step(T, q1, p.x, p.y));
-    f = f12_mul(f, line_and_step(T, nq2, p.x, p.y));
+    f = f12_mul(f, add_line(T, q1, p.x, p.y));
+    f = f12_mul(f, add_line(T, nq2, p.x, p.y));
     return f;
 }
 
@@ -85,30 +115,46 @@ __global__ void __launch_bounds__(64) k_miller(const G1Affine* __restrict__ P, c
     out[i] = miller_loop(P[i], Q[i]);
 }
 
-__device__ __noinline__ Fq12 final_exponentiation(const Fq12& f, const HardExp& e) {
-    // easy part: f^((q^6 - 1)(q^2 + 1))
-    Fq12 t = f12_mul(f12_conj(f), f12_inv(f));
-    t = f12_mul(f12_frob<2>(t), t);
-    // hard part: t^((q^4 - q^2 + 1) / r), MSB first
-    Fq12 r = f12_one();
-    bool started = false;
-    for (int w = (int)pc::HARD_EXP_WORDS - 1; w >= 0; w--)
-        for (int b = 31; b >= 0; b--) {
-            if (started) r = f12_sqr(r);
-            if ((e.w[w] >> b) & 1) {
-                r = started ? f12_mul(r, t) : t;
-                started = true;
-            }
-        }
+// a^x for a unitary a (x = pc::BN_X, 63 bits), square-and-multiply MSB first
+__device__ __noinline__ Fq12 f12_pow_x(const Fq12& a) {
+    Fq12 r = a;
+    for (int b = 61; b >= 0; b--) {
+        r = f12_sqr(r);
+        if ((pc::BN_X >> b) & 1) r = f12_mul(r, a);
+    }
     return r;
 }
 
-__global__ void k_final_exp(const Fq12* __restrict__ f, uint32_t m, HardExp e, Fq12* __restrict__ out,
-                            uint32_t* __restrict__ is_one) {
+__device__ __noinline__ Fq12 final_exponentiation(const Fq12& f) {
+    // easy part: f^((q^6 - 1)(q^2 + 1)); t is unitary from here on (its inverse is its conjugate)
+    Fq12 t = f12_mul(f12_conj(f), f12_inv(f));
+    t = f12_mul(f12_frob<2>(t), t);
+    // hard part: t^((q^4 - q^2 + 1) / r) = t^(l0 + l1 q + l2 q^2 + l3 q^3) exactly, the l_i
+    // polynomials in x (Scott et al. 2009; identity asserted in tools/pairing_consts.py):
+    //   y0 = t^(q + q^2 + q^3), y1 = t^-1, y2 = t^(x^2 q^2), y3 = t^(-x q), y4 = t^(-x - x^2 q),
+    //   y5 = t^(-x^2), y6 = t^(-x^3 - x^3 q), and y0 y1^2 y2^6 y3^12 y4^18 y5^30 y6^36 by the chain
+    const Fq12 fx = f12_pow_x(t), fx2 = f12_pow_x(fx), fx3 = f12_pow_x(fx2);
+    const Fq12 y0 = f12_mul(f12_mul(f12_frob<1>(t), f12_frob<2>(t)), f12_frob<3>(t));
+    const Fq12 y1 = f12_conj(t);
+    const Fq12 y2 = f12_frob<2>(fx2);
+    const Fq12 y3 = f12_conj(f12_frob<1>(fx));
+    const Fq12 y4 = f12_conj(f12_mul(fx, f12_frob<1>(fx2)));
+    const Fq12 y5 = f12_conj(fx2);
+    const Fq12 y6 = f12_conj(f12_mul(fx3, f12_frob<1>(fx3)));
+    Fq12 t0 = f12_mul(f12_mul(f12_sqr(y6), y4), y5);
+    Fq12 t1 = f12_mul(f12_mul(y3, y5), t0);
+    t0 = f12_mul(t0, y2);
+    t1 = f12_sqr(f12_mul(f12_sqr(t1), t0));
+    t0 = f12_sqr(f12_mul(t1, y1));
+    t1 = f12_mul(t1, y0);
+    return f12_mul(t0, t1);
+}
+
+__global__ void k_final_exp(const Fq12* __restrict__ f, uint32_t m, Fq12* __restrict__ out, uint32_t* __restrict__ is_one) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     Fq12 acc = f12_one();
     for (uint32_t i = 0; i < m; i++) acc = f12_mul(acc, f[i]);
-    const Fq12 r = final_exponentiation(acc, e);
+    const Fq12 r = final_exponentiation(acc);
     *out = r;
     *is_one = f12_is_one(r) ? 1u : 0u;
 }
@@ -261,12 +307,6 @@ void fq12_to_abi(const Fq12& a, eon_fq12& out) {
     }
 }
 
-HardExp hard_exp() {
-    HardExp e;
-    for (uint32_t i = 0; i < pc::HARD_EXP_WORDS; i++) e.w[i] = pc::HARD_EXP[i];
-    return e;
-}
-
 // product of the pairings of m device pairs -> Gt element and the is-one flag (host)
 Status pair_product(eon_ctx* ctx, const G1Affine* P, const G2Affine* Q, uint32_t m, Fq12* gt, bool* one) {
     DevBuf f, res;
@@ -276,7 +316,7 @@ Status pair_product(eon_ctx* ctx, const G1Affine* P, const G2Affine* Q, uint32_t
     if (m) hipLaunchKernelGGL(k_miller, dim3((m + 63) / 64), dim3(64), 0, ctx->stream, P, Q, m, f.as<Fq12>());
     ctx->prof.end(ctx->stream);
     ctx->prof.begin("k_final_exp", (uint64_t)m * 384 + 384, ctx->stream);
-    hipLaunchKernelGGL(k_final_exp, dim3(1), dim3(64), 0, ctx->stream, f.as<Fq12>(), m, hard_exp(), res.as<Fq12>(),
+    hipLaunchKernelGGL(k_final_exp, dim3(1), dim3(64), 0, ctx->stream, f.as<Fq12>(), m, res.as<Fq12>(),
                        reinterpret_cast<uint32_t*>(res.as<char>() + sizeof(Fq12)));
     ctx->prof.end(ctx->stream);
     EON_HIP(hipGetLastError());

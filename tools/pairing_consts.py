@@ -64,13 +64,24 @@ def main():
     out.append(f"constexpr uint32_t TWIST_B[2][8] = {f2_lit(b2)};  // 3 / xi")
     hard = (Q ** 4 - Q ** 2 + 1)
     assert hard % R == 0
-    e = hard // R
-    words = []
-    while e:
-        words.append(e & 0xFFFFFFFF)
-        e >>= 32
-    out.append(f"// (q^4 - q^2 + 1) / r, {len(words)} little-endian 32-bit words\nconstexpr uint32_t HARD_EXP_WORDS = {len(words)};\n"
-               f"constexpr uint32_t HARD_EXP[{len(words)}] = {{" + ", ".join(f"0x{w:08x}u" for w in words) + "};")
+    # the hard part (q^4 - q^2 + 1) / r = l0 + l1 q + l2 q^2 + l3 q^3 exactly, with the l_i
+    # polynomials in x (Scott et al., "On the final exponentiation for calculating pairings on
+    # ordinary elliptic curves", 2009): pairing.hip computes it from f^x, f^(x^2), f^(x^3)
+    x = X_BN
+    l3, l2 = 1, 6 * x * x + 1
+    l1 = -36 * x ** 3 - 18 * x * x - 12 * x + 1
+    l0 = -36 * x ** 3 - 30 * x * x - 18 * x - 2
+    assert l0 + l1 * Q + l2 * Q * Q + l3 * Q ** 3 == hard // R
+    # the addition chain of final_exponentiation (y_i exponents, then T0 / T1 as in the kernel)
+    y0, y1, y2, y3 = Q + Q * Q + Q ** 3, -1, x * x * Q * Q, -x * Q
+    y4, y5, y6 = -(x + x * x * Q), -x * x, -(x ** 3 + x ** 3 * Q)
+    t0 = 2 * y6 + y4 + y5
+    t1 = y3 + y5 + t0
+    t0 = t0 + y2
+    t1 = 4 * t1 + 2 * t0
+    t0, t1 = 2 * (t1 + y1), t1 + y0
+    assert t0 + t1 == hard // R
+    out.append(f"constexpr uint64_t BN_X = 0x{x:x}ull;  // the BN parameter x (q, r are polynomials in x)")
     # the standard BN254 G2 generator (EIP-197; halo2curves' G2::generator)
     gx = (10857046999023057135944570762232829481370756359578518086990519993285655852781,
           11559732032986387107991004021392285783925812861821192530917403151452391805634)

@@ -9,10 +9,11 @@
 // G2 lives on the sextic twist y^2 = x^3 + 3/xi over Fq2, untwisted by (x, y) -> (x w^2, y w^3).
 // Elements are Montgomery residues in 8 x 32-bit limbs (field.h), every value canonical.
 //
-// Verification is not on the prove path: these are plain (readable) formulas -- affine Miller
-// loop with the line through T and Q evaluated at P, and the exact final exponent
-// (q^12 - 1) / r = (q^6 - 1)(q^2 + 1) * (q^4 - q^2 + 1) / r, the hard part by square-and-multiply
-// -- so that the value of every pairing equals the definition's, bit for bit (tests/test_gpu_pairing.py).
+// Verification is not on the prove path: one thread per pair, plain formulas -- a projective
+// Miller loop whose lines differ from the affine ones by factors in Fq2 (removed by the easy part),
+// and the exact final exponent (q^12 - 1) / r = (q^6 - 1)(q^2 + 1) * (q^4 - q^2 + 1) / r, the hard
+// part from its base-q decomposition in x with cyclotomic squarings -- so that the value of every
+// pairing equals the definition's, bit for bit (tests/test_gpu_pairing.py).
 #pragma once
 #include "ec.h"
 #include "pairing_consts.h"
@@ -129,6 +130,50 @@ EON_NI Fq12 f12_sqr(const Fq12& a) {
     const Fq6 t = f6_mul(a.c0, a.c1);
     const Fq6 s = f6_mul(f6_add(a.c0, a.c1), f6_add(a.c0, f6_mul_v(a.c1)));
     return {f6_sub(f6_sub(s, t), f6_mul_v(t)), f6_add(t, t)};
+}
+
+// Granger-Scott squaring, valid on the cyclotomic subgroup (a^(q^6 + 1) = 1: the values after the
+// easy part of the final exponentiation).  Fq12 viewed as Fq4^3 with Fq4 = Fq2[y]/(y^2 - xi):
+// (z0 + z1 y), (z2 + z3 y), (z4 + z5 y) with z0 = c0.c0, z1 = c1.c1, z2 = c1.c0, z3 = c0.c2,
+// z4 = c0.c1, z5 = c1.c2; three Fq4 squarings (6 Fq2 products) instead of f12_sqr's 12.
+// (x + y Y)^2 = (x^2 + xi y^2) + 2 x y Y in Fq4 = Fq2[Y]/(Y^2 - xi), as (x + y)(x + xi y) - t - xi t
+// with t = x y
+EON_HD void fq4_sqr(const Fq2& x, const Fq2& y, Fq2& s0, Fq2& s1) {
+    const Fq2 t = f2_mul(x, y);
+    s0 = f2_sub(f2_sub(f2_mul(f2_add(x, y), f2_add(x, f2_mul_xi(y))), t), f2_mul_xi(t));
+    s1 = f2_dbl(t);
+}
+
+EON_NI Fq12 f12_cyc_sqr(const Fq12& a) {
+    const Fq2 &z0 = a.c0.c0, &z4 = a.c0.c1, &z3 = a.c0.c2, &z2 = a.c1.c0, &z1 = a.c1.c1, &z5 = a.c1.c2;
+    Fq2 t0, t1, t2, t3, t4, t5;
+    fq4_sqr(z0, z1, t0, t1);
+    fq4_sqr(z2, z3, t2, t3);
+    fq4_sqr(z4, z5, t4, t5);
+    Fq12 r;
+    r.c0.c0 = f2_add(f2_dbl(f2_sub(t0, z0)), t0);  // 3 t0 - 2 z0
+    r.c1.c1 = f2_add(f2_dbl(f2_add(t1, z1)), t1);  // 3 t1 + 2 z1
+    const Fq2 x5 = f2_mul_xi(t5);
+    r.c1.c0 = f2_add(f2_dbl(f2_add(x5, z2)), x5);  // 3 xi t5 + 2 z2
+    r.c0.c2 = f2_add(f2_dbl(f2_sub(t4, z3)), t4);  // 3 t4 - 2 z3
+    r.c0.c1 = f2_add(f2_dbl(f2_sub(t2, z4)), t2);  // 3 t2 - 2 z4
+    r.c1.c2 = f2_add(f2_dbl(f2_add(t3, z5)), t3);  // 3 t3 + 2 z5
+    return r;
+}
+
+// a (b0 + b1 v) (the sparse Fq6 factor of a line): 5 Fq2 products
+EON_NI Fq6 f6_mul_01(const Fq6& a, const Fq2& b0, const Fq2& b1) {
+    const Fq2 t0 = f2_mul(a.c0, b0), t1 = f2_mul(a.c1, b1);
+    return {f2_add(f2_mul_xi(f2_mul(a.c2, b1)), t0), f2_sub(f2_sub(f2_mul(f2_add(a.c0, a.c1), f2_add(b0, b1)), t0), t1),
+            f2_add(f2_sub(f2_mul(f2_add(a.c0, a.c2), b0), t0), t1)};
+}
+
+// f * l for a line l = l0 + l1 w + l3 w^3 (l.c0 = (l0, 0, 0), l.c1 = (l1, l3, 0)): 13 Fq2 products
+EON_NI Fq12 f12_mul_line(const Fq12& f, const Fq2& l0, const Fq2& l1, const Fq2& l3) {
+    const Fq6 t0 = {f2_mul(f.c0.c0, l0), f2_mul(f.c0.c1, l0), f2_mul(f.c0.c2, l0)};
+    const Fq6 t1 = f6_mul_01(f.c1, l1, l3);
+    const Fq6 s = f6_mul_01(f6_add(f.c0, f.c1), f2_add(l0, l1), l3);
+    return {f6_add(t0, f6_mul_v(t1)), f6_sub(f6_sub(s, t0), t1)};
 }
 
 // a^(q^6): w -> -w

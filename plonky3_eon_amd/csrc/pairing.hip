@@ -91,20 +91,26 @@ __device__ __noinline__ Fq12 add_line(G2Proj& T, const G2Affine& A, const Fq& xp
     return l;
 }
 
+// f times a line of dbl_line / add_line: sparse (l0 + l1 w + l3 w^3) except the vertical line
+__device__ __forceinline__ Fq12 mul_line(const Fq12& f, const Fq12& l) {
+    if (f2_is_zero(l.c1.c0) && f2_is_zero(l.c1.c1)) return f12_mul(f, l);  // vertical: l0 + l2 w^2
+    return f12_mul_line(f, l.c0.c0, l.c1.c0, l.c1.c1);
+}
+
 __device__ __noinline__ Fq12 miller_loop(const G1Affine& p, const G2Affine& q) {
     if (is_inf(p) || g2_is_inf(q)) return f12_one();
     Fq12 f = f12_one();
     G2Proj T = {q.x, q.y, f2_one()};
     for (int b = 63; b >= 0; b--) {  // 6x + 2 below its top bit, MSB first
-        f = f12_mul(f12_sqr(f), dbl_line(T, p.x, p.y));
-        if ((pc::ATE_LOOP_LOW >> b) & 1) f = f12_mul(f, add_line(T, q, p.x, p.y));
+        f = mul_line(f12_sqr(f), dbl_line(T, p.x, p.y));
+        if ((pc::ATE_LOOP_LOW >> b) & 1) f = mul_line(f, add_line(T, q, p.x, p.y));
     }
     // Q1 = pi(Q), -Q2 = -pi^2(Q) on the twist: pi(x, y) = (conj(x) g_x, conj(y) g_y),
     // pi^2(x, y) = (x g2_x, -y)
     const G2Affine q1 = {f2_mul(f2_conj(q.x), f2_c(pc::TWIST_FROB_X)), f2_mul(f2_conj(q.y), f2_c(pc::TWIST_FROB_Y))};
     const G2Affine nq2 = {f2_mul_fq(q.x, fq_c(pc::TWIST_FROB2_X)), q.y};
-    f = f12_mul(f, add_line(T, q1, p.x, p.y));
-    f = f12_mul(f, add_line(T, nq2, p.x, p.y));
+    f = mul_line(f, add_line(T, q1, p.x, p.y));
+    f = mul_line(f, add_line(T, nq2, p.x, p.y));
     return f;
 }
 
@@ -115,11 +121,12 @@ __global__ void __launch_bounds__(64) k_miller(const G1Affine* __restrict__ P, c
     out[i] = miller_loop(P[i], Q[i]);
 }
 
-// a^x for a unitary a (x = pc::BN_X, 63 bits), square-and-multiply MSB first
+// a^x for a unitary a (x = pc::BN_X, 63 bits), square-and-multiply MSB first with cyclotomic
+// squarings
 __device__ __noinline__ Fq12 f12_pow_x(const Fq12& a) {
     Fq12 r = a;
     for (int b = 61; b >= 0; b--) {
-        r = f12_sqr(r);
+        r = f12_cyc_sqr(r);
         if ((pc::BN_X >> b) & 1) r = f12_mul(r, a);
     }
     return r;
@@ -141,11 +148,11 @@ __device__ __noinline__ Fq12 final_exponentiation(const Fq12& f) {
     const Fq12 y4 = f12_conj(f12_mul(fx, f12_frob<1>(fx2)));
     const Fq12 y5 = f12_conj(fx2);
     const Fq12 y6 = f12_conj(f12_mul(fx3, f12_frob<1>(fx3)));
-    Fq12 t0 = f12_mul(f12_mul(f12_sqr(y6), y4), y5);
+    Fq12 t0 = f12_mul(f12_mul(f12_cyc_sqr(y6), y4), y5);
     Fq12 t1 = f12_mul(f12_mul(y3, y5), t0);
     t0 = f12_mul(t0, y2);
-    t1 = f12_sqr(f12_mul(f12_sqr(t1), t0));
-    t0 = f12_sqr(f12_mul(t1, y1));
+    t1 = f12_cyc_sqr(f12_mul(f12_cyc_sqr(t1), t0));
+    t0 = f12_cyc_sqr(f12_mul(t1, y1));
     t1 = f12_mul(t1, y0);
     return f12_mul(t0, t1);
 }
@@ -210,6 +217,15 @@ __device__ __noinline__ G1Xyzz g1_mul_words(const G1Affine& p, const uint32_t (&
     return acc;
 }
 
+// k G2 for the fixed generator: the sum of the table entries 2^i G2 of k's set bits (additions
+// only -- a double-and-add pays 256 doublings on top)
+__device__ __noinline__ G2Jac g2_gen_mul_words(const uint32_t (&k)[8]) {
+    G2Jac acc = {f2_one(), f2_one(), f2_zero()};
+    for (int i = 0; i < 256; i++)
+        if ((k[i >> 5] >> (i & 31)) & 1) acc = g2j_add_affine(acc, {f2_c(pc::G2_POW2[i][0]), f2_c(pc::G2_POW2[i][1])});
+    return acc;
+}
+
 __global__ void __launch_bounds__(64) k_vb_pairs(const G1Xyzz* __restrict__ sums, const Fr* __restrict__ vsum,
                                                  const Fr* __restrict__ zs, uint32_t G, G2Affine g2_alpha,
                                                  G1Affine* __restrict__ P, G2Affine* __restrict__ Q) {
@@ -231,7 +247,7 @@ __global__ void __launch_bounds__(64) k_vb_pairs(const G1Xyzz* __restrict__ sums
         const Fr z = to_canonical(zs[t - 1]);
         uint32_t k[8];
         for (int i = 0; i < 8; i++) k[i] = z.v[i];
-        G2Jac zg = g2_mul_words(g2_generator(), k);
+        G2Jac zg = g2_gen_mul_words(k);
         if (!f2_is_zero(zg.Z)) zg.Y = f2_neg(zg.Y);
         P[t] = xyzz_to_affine(sums[t - 1]);
         Q[t] = g2j_to_affine(g2j_add_affine(zg, g2_alpha));

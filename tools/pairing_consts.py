@@ -93,6 +93,25 @@ def main():
     assert lhs == rhs
     out.append(f"constexpr uint32_t G2_GEN_X[2][8] = {f2_lit(gx)};")
     out.append(f"constexpr uint32_t G2_GEN_Y[2][8] = {f2_lit(gy)};")
+    # 2^i G2 (affine), i = 0..255: [z] G2 for verify_batch by additions only (fixed base)
+    def f2_inv(a):
+        return f2_pow(a, Q * Q - 2)
+
+    def g2_dbl(p):
+        x, y = p
+        x2 = f2_mul(x, x)
+        lam = f2_mul((3 * x2[0] % Q, 3 * x2[1] % Q), f2_inv(((2 * y[0]) % Q, (2 * y[1]) % Q)))
+        l2 = f2_mul(lam, lam)
+        x3 = ((l2[0] - 2 * x[0]) % Q, (l2[1] - 2 * x[1]) % Q)
+        t = f2_mul(lam, ((x[0] - x3[0]) % Q, (x[1] - x3[1]) % Q))
+        return x3, ((t[0] - y[0]) % Q, (t[1] - y[1]) % Q)
+
+    p, rows = (gx, gy), []
+    for _ in range(256):
+        rows.append("{" + f2_lit(p[0]) + ", " + f2_lit(p[1]) + "}")
+        p = g2_dbl(p)
+    out.append("constexpr uint32_t G2_POW2[256][2][2][8] = {  // 2^i G2, i = 0..255 (x, y)\n    "
+               + ",\n    ".join(rows) + "};")
     ate = 6 * X_BN + 2
     assert ate.bit_length() == 65
     out.append(f"constexpr uint64_t ATE_LOOP_LOW = 0x{ate & ((1 << 64) - 1):x}ull;  // 6x + 2 below its top bit (bit 64)")

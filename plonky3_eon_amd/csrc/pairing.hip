@@ -121,13 +121,15 @@ __global__ void __launch_bounds__(64) k_miller(const G1Affine* __restrict__ P, c
     out[i] = miller_loop(P[i], Q[i]);
 }
 
-// a^x for a unitary a (x = pc::BN_X, 63 bits), square-and-multiply MSB first with cyclotomic
-// squarings
+// a^x for a unitary a (x = pc::BN_X, 63 bits): cyclotomic squarings and x's non-adjacent form,
+// MSB first, a^-1 being conj(a) (23 multiplications instead of 27)
 __device__ __noinline__ Fq12 f12_pow_x(const Fq12& a) {
+    const Fq12 ai = f12_conj(a);
     Fq12 r = a;
     for (int b = 61; b >= 0; b--) {
         r = f12_cyc_sqr(r);
-        if ((pc::BN_X >> b) & 1) r = f12_mul(r, a);
+        if ((pc::BN_X_NAF_POS >> b) & 1) r = f12_mul(r, a);
+        if ((pc::BN_X_NAF_NEG >> b) & 1) r = f12_mul(r, ai);
     }
     return r;
 }

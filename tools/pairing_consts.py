@@ -82,6 +82,22 @@ def main():
     t0, t1 = 2 * (t1 + y1), t1 + y0
     assert t0 + t1 == hard // R
     out.append(f"constexpr uint64_t BN_X = 0x{x:x}ull;  // the BN parameter x (q, r are polynomials in x)")
+    # x in non-adjacent form: x = sum of 2^i over NAF_POS's bits minus 2^i over NAF_NEG's (24 digits
+    # against x's 28 set bits); the top digit is bit 62
+    pos = neg = 0
+    k, i = x, 0
+    while k:
+        if k & 1:
+            d = 2 - (k % 4)
+            k -= d
+            if d == 1:
+                pos |= 1 << i
+            else:
+                neg |= 1 << i
+        k //= 2
+        i += 1
+    assert pos - neg == x and pos >> 62 == 1 and (pos | neg) >> 63 == 0
+    out.append(f"constexpr uint64_t BN_X_NAF_POS = 0x{pos:x}ull, BN_X_NAF_NEG = 0x{neg:x}ull;")
     # the standard BN254 G2 generator (EIP-197; halo2curves' G2::generator)
     gx = (10857046999023057135944570762232829481370756359578518086990519993285655852781,
           11559732032986387107991004021392285783925812861821192530917403151452391805634)

@@ -195,6 +195,24 @@ EON_HD F29 sub29_lazy(const F29& a, const F29& b) {
     return r;
 }
 
+// a - b + K p normalised, for a with limbs < 2^31 (an add29_lazy / sub29_lazy output) and b
+// normalised with b < K p: limb by limb a_i + (K p borrowed)_i - b_i + c in unsigned arithmetic
+// (never negative: the borrowed limbs are >= 2^29 - 1 >= b_i, and the top limb is the nonnegative
+// remainder of a - b + K p >= 0), so no signed column can overflow as in sub29
+template <class M, uint32_t K>
+EON_HD F29 sub29_wide(const F29& a, const F29& b) {
+    constexpr KPB29<M, K> kp{};
+    F29 r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        const uint32_t t = a.l[i] + kp.l[i] - b.l[i] + c;
+        r.l[i] = t & M29;
+        c = t >> 29;
+    }
+    return r;
+}
+
 template <class M>
 EON_HD F29 mulp29(uint32_t k) {
     F29 r;

@@ -194,12 +194,21 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
             if (!DIF) {
                 // DitButterfly (dft/src/butterflies.rs:177-185): (x + w*y, x - w*y).  Lazy: t < 3p
                 // (the Shoup product, or y itself at the unit stage, which is the pass's first and
-                // sees loaded values < 2p), so both outputs are below x + 3p -- a pass of k <= 10
-                // stages ends below 32p, inside the normalised range mul29_shoup takes (any value
+                // sees loaded values < 2p), so both outputs are below x + 4p -- a pass of k <= 10
+                // stages ends below 37p, inside the range mul29_shoup takes (any value
                 // < 2^261 = 169p); the store brings it back below 2p (reduce_top29)
                 const F29 t = unit ? y : mul29_shoup<FrP>(y, w, wq);
-                u = add29_norm(x, t);
-                v = sub29<FrP, 3>(x, t);
+                // carries propagated every other stage: a lazy stage (inputs normalised) leaves
+                // limbs < 2^31 (x + t, x - t + 4p), which the next stage's Shoup product (columns
+                // < 9 2^60 + 9 2^58) and its carry-propagating add / sub29_wide take; the pass's
+                // last stage normalises.  Values grow by <= 4p per stage: < 37p after 10
+                if ((k - 1 - it) & 1) {
+                    u = add29_lazy(x, t);
+                    v = sub29_lazy<FrP, 4>(x, t);
+                } else {
+                    u = add29_norm(x, t);
+                    v = sub29_wide<FrP, 3>(x, t);
+                }
             } else {
                 // DIF butterfly: (x + y, (x - y) * w).  The pass's inputs are below 2p; the sum is
                 // brought back below 2p by reduce_top29 only at odd stages of the pass, so every

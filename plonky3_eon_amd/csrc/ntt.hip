@@ -214,7 +214,8 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
                 // brought back below 2p by reduce_top29 only at odd stages of the pass, so every
                 // stage sees inputs below 4p: the sum < 8p, the difference x - y + 4p < 8p into
                 // the Shoup product (< 3p) -- or kept at the unit stage, which is the pass's last
-                // (reduce_top29 at the store)
+                // (reduce_top29 at the store).  (A carry-free difference into the product,
+                // x - y + 5p by sub29_lazy, measured slower: profiles/r03/ab_ntt_lazy.txt)
                 const F29 sum = add29_norm(x, y);
                 u = (it & 1) ? reduce_top29<FrP>(sum) : sum;
                 const F29 d = sub29<FrP, 4>(x, y);

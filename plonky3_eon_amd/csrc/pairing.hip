@@ -209,15 +209,6 @@ __global__ void __launch_bounds__(VB_THREADS) k_vb_sums(const G1Affine* __restri
     }
 }
 
-__device__ __noinline__ G1Xyzz g1_mul_words(const G1Affine& p, const uint32_t (&k)[8]) {
-    G1Xyzz acc = xyzz_inf();
-    for (int w = 7; w >= 0; w--)
-        for (int b = 31; b >= 0; b--) {
-            acc = xyzz_dbl(acc);
-            if ((k[w] >> b) & 1) acc = xyzz_add_affine(acc, p);
-        }
-    return acc;
-}
 
 // k G2 for the fixed generator: the sum of the table entries 2^i G2 of k's set bits (additions
 // only -- a double-and-add pays 256 doublings on top)
@@ -228,6 +219,14 @@ __device__ __noinline__ G2Jac g2_gen_mul_words(const uint32_t (&k)[8]) {
     return acc;
 }
 
+// k G1 for the generator (1, 2), likewise from the table 2^i G1
+__device__ __noinline__ G1Xyzz g1_gen_mul_words(const uint32_t (&k)[8]) {
+    G1Xyzz acc = xyzz_inf();
+    for (int i = 0; i < 256; i++)
+        if ((k[i >> 5] >> (i & 31)) & 1) acc = xyzz_add_affine(acc, {fq_c(pc::G1_POW2[i][0]), fq_c(pc::G1_POW2[i][1])});
+    return acc;
+}
+
 __global__ void __launch_bounds__(64) k_vb_pairs(const G1Xyzz* __restrict__ sums, const Fr* __restrict__ vsum,
                                                  const Fr* __restrict__ zs, uint32_t G, G2Affine g2_alpha,
                                                  G1Affine* __restrict__ P, G2Affine* __restrict__ Q) {
@@ -235,13 +234,10 @@ __global__ void __launch_bounds__(64) k_vb_pairs(const G1Xyzz* __restrict__ sums
     if (t > G) return;
     if (t == 0) {
         // P_0 = sum C - (sum v) G1, Q_0 = G2
-        G1Affine g1;
-        g1.x = from_u64<FqP>(1);
-        g1.y = from_u64<FqP>(2);
         const Fr v = to_canonical(*vsum);
         uint32_t k[8];
         for (int i = 0; i < 8; i++) k[i] = v.v[i];
-        G1Affine vg = xyzz_to_affine(g1_mul_words(g1, k));
+        G1Affine vg = xyzz_to_affine(g1_gen_mul_words(k));
         P[0] = xyzz_to_affine(xyzz_add_affine(sums[G], affine_neg(vg)));
         Q[0] = g2_generator();
     } else {

@@ -36,3 +36,21 @@ def test_g2_pow2_table_matches_oracle():
         ws = words[32 * i:32 * (i + 1)]
         got = ((fq(ws[0:8]), fq(ws[8:16])), (fq(ws[16:24]), fq(ws[24:32])))
         assert got == PO.g2_mul(p, 1 << i), i
+
+
+def test_g1_pow2_table_matches_oracle():
+    from oracle import pyoracle as O
+
+    header = (ROOT / "plonky3_eon_amd" / "csrc" / "pairing_consts.h").read_text()
+    table = header.split("G1_POW2[256][2][8] = {")[1].split("};")[0]
+    words = [int(w.rstrip("u"), 16) for w in table.replace("{", " ").replace("}", " ").replace(",", " ").split()
+             if w.startswith("0x")]
+    assert len(words) == 256 * 16
+
+    def fq(ws):
+        m = sum(w << (32 * i) for i, w in enumerate(ws))
+        return m * pow(1 << 256, -1, O.Q) % O.Q
+
+    for i in (0, 1, 3, 128, 255):
+        ws = words[16 * i:16 * (i + 1)]
+        assert (fq(ws[0:8]), fq(ws[8:16])) == O.g1_mul((1, 2), 1 << i), i

@@ -128,6 +128,19 @@ def main():
         p = g2_dbl(p)
     out.append("constexpr uint32_t G2_POW2[256][2][2][8] = {  // 2^i G2, i = 0..255 (x, y)\n    "
                + ",\n    ".join(rows) + "};")
+    # 2^i G1 (affine, G1 = (1, 2) on y^2 = x^3 + 3), i = 0..255: [sum v] G1 by additions only
+    def g1_dbl(p):
+        x, y = p
+        lam = 3 * x * x * pow(2 * y, Q - 2, Q) % Q
+        x3 = (lam * lam - 2 * x) % Q
+        return x3, (lam * (x - x3) - y) % Q
+
+    p, rows = (1, 2), []
+    for _ in range(256):
+        rows.append("{" + fq_lit(p[0]) + ", " + fq_lit(p[1]) + "}")
+        p = g1_dbl(p)
+    out.append("constexpr uint32_t G1_POW2[256][2][8] = {  // 2^i G1, i = 0..255 (x, y)\n    "
+               + ",\n    ".join(rows) + "};")
     ate = 6 * X_BN + 2
     assert ate.bit_length() == 65
     out.append(f"constexpr uint64_t ATE_LOOP_LOW = 0x{ate & ((1 << 64) - 1):x}ull;  // 6x + 2 below its top bit (bit 64)")

@@ -51,27 +51,28 @@ void fq_from_mont(const uint64_t a[4], uint64_t out[4]) {
     if (t[4] || geq(out, Q)) sub_in_place(out, Q);
 }
 
-Fr sbox(const Fr& x) {  // x^5
-    const Fr x2 = fr_mul(x, x);
-    return fr_mul(fr_mul(x2, x2), x);
+template <bool ADX>
+FrLazy sbox(const FrLazy& x) {  // x^5
+    const FrLazy x2 = lz_mul<ADX>(x, x);
+    return lz_mul<ADX>(lz_mul<ADX>(x2, x2), x);
 }
 
-void mds_light(Fr s[3]) {  // external.rs:128-133
-    const Fr t = fr_add(fr_add(s[0], s[1]), s[2]);
-    for (int i = 0; i < 3; i++) s[i] = fr_add(s[i], t);
+void mds_light(FrLazy s[3]) {  // external.rs:128-133
+    const FrLazy t = lz_add(lz_add(s[0], s[1]), s[2]);
+    for (int i = 0; i < 3; i++) s[i] = lz_add(s[i], t);
 }
 
-void matmul_internal(Fr s[3]) {  // bn254/src/poseidon2.rs:55-63
-    const Fr t = fr_add(s[0], fr_add(s[1], s[2]));
-    s[0] = fr_add(s[0], t);
-    s[1] = fr_add(s[1], t);
-    s[2] = fr_add(fr_add(s[2], s[2]), t);
+void matmul_internal(FrLazy s[3]) {  // bn254/src/poseidon2.rs:55-63
+    const FrLazy t = lz_add(s[0], lz_add(s[1], s[2]));
+    s[0] = lz_add(s[0], t);
+    s[1] = lz_add(s[1], t);
+    s[2] = lz_add(lz_add(s[2], s[2]), t);
 }
 
 }  // namespace
 
 Fr fr_add(const Fr& a, const Fr& b) {
-    // canonical inputs < r < 2^254: the sum fits in 255 bits
+    // canonical inputs < r < 2^254: the sum fits in 256 bits
     Fr s;
     unsigned __int128 c = 0;
     for (int i = 0; i < 4; i++) {
@@ -79,7 +80,7 @@ Fr fr_add(const Fr& a, const Fr& b) {
         s.l[i] = (uint64_t)c;
         c >>= 64;
     }
-    if (geq(s.l, Fr::P)) sub_in_place(s.l, Fr::P);
+    detail::cond_sub(s.l, Fr::P);
     return s;
 }
 
@@ -87,29 +88,57 @@ Poseidon2Bn254::Poseidon2Bn254(const eon_poseidon2_constants& c) : hf_(c.half_fu
     if ((hf_ && (!c.beginning || !c.ending)) || (c.partial_rounds && !c.partial))
         throw Error(EON_E_ARG, "null Poseidon2 round constants");
     for (uint32_t i = 0; i < 3 * hf_; i++) {
-        begin_.push_back(Fr::from_abi(c.beginning[i]));
-        end_.push_back(Fr::from_abi(c.ending[i]));
+        begin_.push_back(FrLazy::of(Fr::from_abi(c.beginning[i])));
+        end_.push_back(FrLazy::of(Fr::from_abi(c.ending[i])));
     }
-    for (uint32_t i = 0; i < c.partial_rounds; i++) partial_.push_back(Fr::from_abi(c.partial[i]));
+    for (uint32_t i = 0; i < c.partial_rounds; i++) partial_.push_back(FrLazy::of(Fr::from_abi(c.partial[i])));
     for (const auto* v : {&begin_, &end_, &partial_})
-        for (const Fr& x : *v)
+        for (const FrLazy& x : *v)
             if (geq(x.l, Fr::P)) throw Error(EON_E_ARG, "Poseidon2 round constant is not a canonical Fr");
 }
 
-void Poseidon2Bn254::permute(Fr s[3]) const {
+template <bool ADX>
+void Poseidon2Bn254::permute_impl(Fr st[3]) const {
+    // every intermediate stays below 2r (fr_host.h: FrLazy); the state is canonical again at the end
+    FrLazy s[3] = {FrLazy::of(st[0]), FrLazy::of(st[1]), FrLazy::of(st[2])};
     mds_light(s);  // external_initial_permute_state (external.rs:321-336)
     for (uint32_t r = 0; r < hf_; r++) {
-        for (int i = 0; i < 3; i++) s[i] = sbox(fr_add(s[i], begin_[3 * r + i]));
+        for (int i = 0; i < 3; i++) s[i] = sbox<ADX>(lz_add(s[i], begin_[3 * r + i]));
         mds_light(s);
     }
-    for (const Fr& rc : partial_) {  // internal_permute_state (internal.rs:70-84)
-        s[0] = sbox(fr_add(s[0], rc));
-        matmul_internal(s);
+    // internal_permute_state (internal.rs:70-84): s0 <- (s0 + rc)^5, then [2,1,1;1,2,1;1,1,3] s.
+    // Only s0 is a dependent chain, so the round is re-associated to keep one addition on it:
+    // with v = x^5 and p = s1 + s2, s0' = 2v + p = x^4 (2x) + p and the next round's input is
+    // s0' + rc' = x^4 (2x) + (p + rc'); v itself (for s1' = s1 + v + p, s2' = 2 s2 + v + p) is
+    // 2v halved beside the chain.  Same field values, so bit-identical after canonicalisation.
+    if (!partial_.empty()) {
+        FrLazy x = lz_add(s[0], partial_[0]);
+        for (size_t r = 0; r < partial_.size(); r++) {
+            const FrLazy p = lz_add(s[1], s[2]);
+            const FrLazy x2 = lz_mul<ADX>(x, x), xd = lz_add(x, x);
+            const FrLazy x4 = lz_mul<ADX>(x2, x2);
+            const FrLazy v2 = lz_mul<ADX>(x4, xd), v = lz_half(v2);
+            const FrLazy t = lz_add(v, p);
+            s[1] = lz_add(s[1], t);
+            s[2] = lz_add(lz_add(s[2], s[2]), t);
+            if (r + 1 < partial_.size())
+                x = lz_add(v2, lz_add(p, partial_[r + 1]));
+            else
+                s[0] = lz_add(v2, p);
+        }
     }
     for (uint32_t r = 0; r < hf_; r++) {  // external_terminal_permute_state (external.rs:288-306)
-        for (int i = 0; i < 3; i++) s[i] = sbox(fr_add(s[i], end_[3 * r + i]));
+        for (int i = 0; i < 3; i++) s[i] = sbox<ADX>(lz_add(s[i], end_[3 * r + i]));
         mds_light(s);
     }
+    for (int i = 0; i < 3; i++) st[i] = s[i].canonical();
+}
+
+void Poseidon2Bn254::permute(Fr st[3]) const {
+    if (detail::kCpuAdx)
+        permute_impl<true>(st);
+    else
+        permute_impl<false>(st);
 }
 
 void DuplexChallenger::duplexing() {

@@ -35,7 +35,9 @@ class Poseidon2Bn254 {
     void permute(Fr s[3]) const;
 
    private:
-    std::vector<Fr> begin_, partial_, end_;  // begin_/end_: half_full_rounds x 3
+    template <bool ADX>
+    void permute_impl(Fr s[3]) const;
+    std::vector<FrLazy> begin_, partial_, end_;  // begin_/end_: half_full_rounds x 3
     uint32_t hf_ = 0;
 };
 

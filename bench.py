@@ -339,7 +339,16 @@ class ProveWorkload:
         self.log_n, self.vl = args.log_trace, args.vector_len
         n = 1 << self.log_n
         world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.shard = Shard(rank, world, self.vl) if world > 1 else None
+        self.emulate = args.emulate_world
+        if self.emulate > 1 and world > 1:
+            raise SystemExit("--emulate-world is a one-process proxy (run it without --gpus)")
+        if self.emulate > 1:
+            # rank 0 of an `emulate`-rank lane-sharded prove on this one GPU: its lanes, its
+            # commit / LDE / quotient / open work, the replicated transcript over all
+            # 164 * VECTOR_LEN commitments, and device copies standing in for the exchanges
+            self.shard = Shard(0, self.emulate, self.vl)
+        else:
+            self.shard = Shard(rank, world, self.vl) if world > 1 else None
         l0, l1 = self.shard.lanes if self.shard else (0, self.vl)
         self.consts = p2_constants_limbs(99)
         self.air = Poseidon2Air(*self.consts, l1 - l0, ctx)
@@ -352,11 +361,13 @@ class ProveWorkload:
             from plonky3_eon_amd.air import AirProgram
 
             self.air = AirProgram(self.p2air, ctx)
-        from plonky3_eon_amd.native import NativeKzgPcs, RcclCollective, TorchCollective
+        from plonky3_eon_amd.native import EmulatedCollective, NativeKzgPcs, RcclCollective, TorchCollective
 
         self.pcs = NativeKzgPcs(n, 12345, ctx)
         self.coll = None
-        if world > 1:
+        if self.emulate > 1:
+            self.coll = EmulatedCollective(0, self.emulate)
+        elif world > 1:
             # torch's RCCL process group (all_gather_into_tensor on device) by default; the
             # driver's own communicator with --collective rccl
             self.coll = (RcclCollective(rank, world) if args.collective == "rccl"
@@ -383,11 +394,15 @@ class ProveWorkload:
 
     def describe(self, world):
         w = 164 * self.vl
+        par = f"lane-shard x{world}" if world > 1 else "single"
+        if self.emulate > 1:
+            par = (f"EMULATED rank 0 of lane-shard x{self.emulate} on one GPU (its lanes and the full "
+                   f"transcript; exchanges replaced by local device copies; not a valid proof)")
         return (f"configs[3]: eon-uni-stark prove, Poseidon2-AIR (VECTOR_LEN {self.vl}, width {w}) "
                 f"log-trace-length {self.log_n} (2^{self.log_n + (self.vl.bit_length() - 1)} permutations), "
                 f"KzgPcs over BN254" + (", Fiat-Shamir transcript" if self.fs else ", fixed alpha/zeta")
                 + (", generic AIR program quotient (k_air_quotient)" if self.args.air == "generic" else ""),
-                world, 1 << self.log_n, f"lane-shard x{world}" if world > 1 else "single")
+                world, 1 << self.log_n, par)
 
     def throughput(self, world, ms):
         n = 1 << self.log_n
@@ -691,6 +706,10 @@ def make_parser() -> argparse.ArgumentParser:
                          "whose per-kernel durations are isolated")
     ap.add_argument("--transcript", choices=["fs", "fixed"], default="fs",
                     help="prove: alpha/zeta from the Fiat-Shamir transcript (default) or fixed")
+    ap.add_argument("--emulate-world", type=int, default=1,
+                    help="prove: time rank 0 of an N-rank lane-sharded prove on this one GPU (its lanes, "
+                         "the full replicated transcript, local copies for the exchanges) -- a per-rank "
+                         "proxy, not a multi-GPU measurement")
     ap.add_argument("--collective", choices=["torch", "rccl"], default="torch",
                     help="prove at N > 1: all-gathers through torch.distributed (RCCL "
                          "process group) or the driver's own RCCL communicator")

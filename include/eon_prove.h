@@ -47,6 +47,11 @@ const char* eon_kzg_pcs_last_error(const eon_kzg_pcs* pcs);
 int eon_rccl_unique_id(uint8_t id[128]);
 int eon_rccl_collective_init(uint32_t rank, uint32_t world, const uint8_t id[128], eon_collective* out);
 void eon_rccl_collective_finalize(eon_collective* coll);
+/* The one-GPU proxy of rank `rank` in a `world`-rank lane-sharded prove (bench.py
+ * --emulate-world): its all-gather writes this rank's block into every slot, its all-to-all
+ * keeps every block, both as device copies on the given stream.  Results are NOT a valid
+ * proof; the point is the rank's own work, including the full replicated transcript. */
+int eon_emulated_collective_init(uint32_t rank, uint32_t world, eon_collective* out);
 
 enum {
     EON_STAGE_COMMIT_TRACE = 0,    /* "commit to trace data" (prover.rs:186-187) */

@@ -35,21 +35,34 @@ class _DevBytes:
 
 
 class TorchCollective:
-    """eon_collective whose all-gather / all-to-all are torch.distributed over `group`."""
+    """eon_collective whose all-gather / all-to-all are torch.distributed over `group`.
+
+    Stream-ordered and copy-free: the callback makes the library's stream (`hip_stream`, the
+    context's) torch's current stream for the call, so that the collective is ordered after the
+    kernels that produced `send` and everything later on that stream is ordered after the
+    collective -- no device-wide synchronize.  With the nccl (RCCL) backend the exchange writes
+    straight into `recv` (all_gather_into_tensor / all_to_all_single on views of the caller's
+    buffers); gloo stages through host memory (the CPU-hosted tests, several ranks per GPU)."""
 
     def __init__(self, rank: int, world: int, group=None, device=0):
         self.rank, self.world = rank, world
         self.group = group
         self.device = device
+        self._streams = {}
 
         def wrap(body):
             def fn(user, send, recv, nbytes, stream):
                 try:
                     import torch
 
-                    torch.cuda.synchronize(self.device)  # the library's stream has produced `send`
-                    body(send, recv, nbytes)
-                    torch.cuda.synchronize(self.device)
+                    dev = torch.device("cuda", self.device)
+                    ext = self._streams.get(stream)
+                    if ext is None:
+                        ext = (torch.cuda.ExternalStream(stream, device=dev) if stream
+                               else torch.cuda.default_stream(dev))  # NULL: the device's null stream
+                        self._streams[stream] = ext
+                    with torch.cuda.stream(ext):
+                        body(send, recv, nbytes, dev)
                     return 0
                 except Exception:  # a Python exception must not unwind through the C caller
                     import traceback
@@ -58,23 +71,38 @@ class TorchCollective:
                     return 1
             return fn
 
-        def all_gather(send, recv, nbytes):
+        def nccl(group):
+            import torch.distributed as dist
+
+            return dist.get_backend(group) == "nccl"
+
+        def all_gather(send, recv, nbytes, dev):
             import torch
+            import torch.distributed as dist
 
-            from .distributed import all_gather_rows
+            s = torch.as_tensor(_DevBytes(send, nbytes), device=dev)
+            r = torch.as_tensor(_DevBytes(recv, nbytes * world), device=dev)
+            if nccl(self.group):
+                dist.all_gather_into_tensor(r, s, group=self.group)
+            else:
+                h = s.cpu()
+                parts = [torch.empty_like(h) for _ in range(world)]
+                dist.all_gather(parts, h, group=self.group)
+                r.copy_(torch.cat(parts))
 
-            s = torch.as_tensor(_DevBytes(send, nbytes), device=f"cuda:{self.device}")
-            r = torch.as_tensor(_DevBytes(recv, nbytes * world), device=f"cuda:{self.device}")
-            r.copy_(all_gather_rows(s, self.group).reshape(-1))
-
-        def all_to_all(send, recv, nbytes):
+        def all_to_all(send, recv, nbytes, dev):
             import torch
+            import torch.distributed as dist
 
-            from .distributed import all_to_all_blocks
-
-            s = torch.as_tensor(_DevBytes(send, nbytes * world), device=f"cuda:{self.device}")
-            r = torch.as_tensor(_DevBytes(recv, nbytes * world), device=f"cuda:{self.device}")
-            r.copy_(all_to_all_blocks(s.reshape(world, -1), self.group).reshape(-1))
+            s = torch.as_tensor(_DevBytes(send, nbytes * world), device=dev)
+            r = torch.as_tensor(_DevBytes(recv, nbytes * world), device=dev)
+            if nccl(self.group):
+                dist.all_to_all_single(r, s, group=self.group)
+            else:
+                h = s.cpu()
+                hr = torch.empty_like(h)
+                dist.all_to_all_single(hr, h, group=self.group)
+                r.copy_(hr)
 
         self._fns = (ALL_GATHER_FN(wrap(all_gather)), ALL_TO_ALL_FN(wrap(all_to_all)))  # keep the thunks alive
         self.c = eon_collective(rank, world, self._fns[0], None, self._fns[1])

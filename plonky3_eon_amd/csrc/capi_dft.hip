@@ -352,6 +352,8 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     ctx->fin_U.release();
     ctx->fs_a.release();
     ctx->fs_b.release();
+    ctx->shard_send.release();
+    ctx->shard_recv.release();
     ctx->scratch.release();
     ctx->stage_in.release();
     ctx->stage_out.release();

@@ -142,8 +142,8 @@ struct eon_ctx {
     // call-wide first-level segment sums of the MSM bucket reduction (msm.hip DeferredFinish)
     eon::DevBuf fin_T, fin_U;
 
-    // four-step DFT working blocks (sharded.hip)
-    eon::DevBuf fs_a, fs_b;
+    // four-step DFT working blocks; the sharded MSM's partials (sharded.hip)
+    eon::DevBuf fs_a, fs_b, shard_send, shard_recv;
 
     // quotient: vanishing-polynomial table; KZG opening scan workspace
     eon::DevBuf sel_tab, kzg_tmp;

@@ -874,7 +874,7 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     bt.groups = L.precomputed ? bt.cols : bt.cols * bt.W;
     bt.nb = bt.groups * bt.B;
     bt.E = n * bt.W * bt.cols;
-    if (bt.E >= (1ull << 32)) return Status::err(EON_E_SHAPE, "MSM too large for 32-bit pair indices");
+    if (bt.E > RADIX_SORT_MAX_PAIRS) return Status::err(EON_E_SHAPE, "MSM batch too large for 32-bit pair indices");
     // keys are (group << c) | (|digit| - 1); only the low c bits are sorted
     if (((uint64_t)bt.groups << bt.c) > 0xFFFFFFFFull)
         return Status::err(EON_E_SHAPE, "too many MSM groups for 32-bit digit keys");

@@ -211,14 +211,18 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
                 }
             } else {
                 // DIF butterfly: (x + y, (x - y) * w).  The pass's inputs are below 2p; the sum is
-                // brought back below 2p by reduce_top29 only at odd stages of the pass, so every
-                // stage sees inputs below 4p: the sum < 8p, the difference x - y + 4p < 8p into
-                // the Shoup product (< 3p) -- or kept at the unit stage, which is the pass's last
-                // (reduce_top29 at the store).  (A carry-free difference into the product,
-                // x - y + 5p by sub29_lazy, measured slower: profiles/r03/ab_ntt_lazy.txt)
+                // brought back below 2p by reduce_top29 only at odd stages of the pass.  A Shoup
+                // output is below 3p (2p when its quotient estimate is exact or one short -- the
+                // dropped low columns can make it one shorter), so an even stage's inputs are below
+                // 3p and its unreduced sum below 6p, which is the worst input of the odd stage after
+                // it: the difference x - y + 6p (< 12p) never goes negative and stays well inside
+                // the Shoup product's range (< 2^261 = 169p); the sum (< 12p) goes through
+                // reduce_top29.  At the unit stage, the pass's last, the difference is kept and
+                // reduce_top29 runs at the store.  (A carry-free difference into the product by
+                // sub29_lazy measured slower: profiles/r03/ab_ntt_lazy.txt)
                 const F29 sum = add29_norm(x, y);
                 u = (it & 1) ? reduce_top29<FrP>(sum) : sum;
-                const F29 d = sub29<FrP, 4>(x, y);
+                const F29 d = sub29<FrP, 6>(x, y);
                 v = unit ? d : mul29_shoup<FrP>(d, w, wq);
             }
             lds_put29(lo, hi, top, i0, u);

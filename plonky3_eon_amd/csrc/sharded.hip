@@ -112,14 +112,14 @@ Status msm_sharded(eon_ctx* ctx, const eon_msm_bases* bases, const Fr* scalars, 
         return Status::ok();
     }
     const uint32_t world = coll->world;
-    DevBuf send, recv;
-    struct Free {
-        DevBuf *a, *b;
-        ~Free() {
-            a->release();
-            b->release();
-        }
-    } fr{&send, &recv};
+    // context-owned (reused across calls); every exit drains the stream first, so neither the
+    // host-side `pa` nor a later reuse of the buffers can race work still queued on it
+    DevBuf& send = ctx->shard_send;
+    DevBuf& recv = ctx->shard_recv;
+    struct Drain {
+        hipStream_t s;
+        ~Drain() { (void)hipStreamSynchronize(s); }
+    } drain{ctx->stream};
     EON_HIP(send.ensure(sizeof(eon_g1_affine)));
     EON_HIP(recv.ensure(world * sizeof(eon_g1_affine)));
     const eon_g1_affine pa = to_abi(part);

@@ -8,10 +8,14 @@
 
 namespace eon {
 
+// Largest n radix_sort_pairs takes: u32 positions, the last tile's indices must not wrap.
+constexpr uint64_t RADIX_SORT_MAX_PAIRS = (1ull << 32) - 8192;
+
 // Scratch bytes of radix_sort_pairs for n pairs sorted on `bits` low key bits.
 size_t radix_sort_temp_bytes(uint64_t n, uint32_t bits);
 
-// Stable sort of the pairs (keys_in[i], vals_in[i]), i < n (n < 2^30), by key bits [0, bits)
+// Stable sort of the pairs (keys_in[i], vals_in[i]), i < n (n <= RADIX_SORT_MAX_PAIRS), by key
+// bits [0, bits)
 // into keys_out / vals_out; the inputs are left unchanged.  LSD passes of <= 8-bit digits (16
 // bits: 2 passes); each pass is one kernel that ranks a tile of pairs in LDS and finds the tile's
 // global digit offsets by a decoupled look-back over the preceding tiles, after one histogram

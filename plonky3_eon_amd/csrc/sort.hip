@@ -11,8 +11,8 @@
 //                 same digit found by one ballot per digit bit, the per-wave digit counters in
 //                 LDS -- publishes the tile's digit counts, scatters the pairs into LDS in digit
 //                 order, and then finds the digit's global offset by a decoupled look-back over the
-//                 preceding tiles' published counts (a 2-bit flag and a 30-bit count in one word:
-//                 aggregate or inclusive).  The tile's pairs leave LDS in digit runs, so the global
+//                 preceding tiles' published counts (a 2-bit flag and a 62-bit count in one 64-bit
+//                 word: aggregate or inclusive).  The tile's pairs leave LDS in digit runs, so the global
 //                 writes are contiguous per run.  Stability: the slots are walked in input order
 //                 (slot j of a wave covers its pairs j 64 .. j 64 + 63).
 // Traffic per pass: 8 B read + 8 B written per pair (plus 4 B per pair once for the histograms).
@@ -28,7 +28,8 @@ namespace {
 
 constexpr uint32_t SORT_THREADS = 512, SORT_WAVES = SORT_THREADS / 64, SORT_ITEMS = 16;
 constexpr uint32_t SORT_TILE = SORT_THREADS * SORT_ITEMS;
-constexpr uint32_t ST_AGG = 1u << 30, ST_INC = 2u << 30, ST_COUNT = (1u << 30) - 1;
+constexpr uint64_t ST_AGG = 1ull << 62, ST_INC = 2ull << 62, ST_COUNT = (1ull << 62) - 1;
+static_assert(RADIX_SORT_MAX_PAIRS == (1ull << 32) - SORT_TILE, "sort.h's limit is this tile's");
 constexpr uint32_t MAX_PASSES = 4;
 constexpr size_t SORT_LDS = (size_t)SORT_TILE * 8 + SORT_WAVES * 256 * 4 + 2 * 256 * 4 + 64;
 
@@ -115,17 +116,17 @@ __global__ void __launch_bounds__(256) k_sort_base(const uint32_t* __restrict__ 
     }
 }
 
-__device__ __forceinline__ void st_status(uint32_t* p, uint32_t v) {
+__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint32_t ld_status(uint32_t* p) {
+__device__ __forceinline__ uint64_t ld_status(uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __restrict__ ks, const uint32_t* __restrict__ vs,
                                                             uint32_t* __restrict__ kd, uint32_t* __restrict__ vd, uint32_t n,
                                                             uint32_t shift, uint32_t dbits,
-                                                            const uint32_t* __restrict__ base, uint32_t* status,
+                                                            const uint32_t* __restrict__ base, uint64_t* status,
                                                             uint32_t* tile_ctr) {
     extern __shared__ uint32_t lds[];
     uint32_t* sk = lds;                                 // SORT_TILE keys in digit order
@@ -181,7 +182,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
             tcount += c;
         }
         // publish this tile's counts before anything else, so the next tiles can look back
-        st_status(status + (size_t)tile * 256 + tid, (tile == 0 ? ST_INC : ST_AGG) | tcount);
+        st_status(status + (size_t)tile * 256 + tid, (tile == 0 ? ST_INC : ST_AGG) | (uint64_t)tcount);
     }
     uint32_t tot;
     const uint32_t ts = scan256(tid < 256 ? tcount : 0u, misc + 4, tot);
@@ -200,12 +201,12 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
         uint32_t excl = 0;
         if (tile > 0) {
             for (uint32_t k = tile - 1;; k--) {
-                uint32_t v;
-                while (((v = ld_status(status + (size_t)k * 256 + tid)) >> 30) == 0) __builtin_amdgcn_s_sleep(1);
-                excl += v & ST_COUNT;
+                uint64_t v;
+                while (((v = ld_status(status + (size_t)k * 256 + tid)) >> 62) == 0) __builtin_amdgcn_s_sleep(1);
+                excl += (uint32_t)(v & ST_COUNT);  // a digit's running count is below n < 2^32
                 if (v & ST_INC) break;
             }
-            st_status(status + (size_t)tile * 256 + tid, ST_INC | (excl + tcount));
+            st_status(status + (size_t)tile * 256 + tid, ST_INC | (uint64_t)(excl + tcount));
         }
         goff[tid] = base[tid] + excl;
     }
@@ -281,13 +282,13 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(const uint32_t* __r
 size_t radix_sort_temp_bytes(uint64_t n, uint32_t bits) {
     const uint64_t tiles = (n + SORT_TILE - 1) / SORT_TILE;
     (void)bits;
-    return 2 * align256(n * 4) + 2 * align256(MAX_PASSES * 256 * 4) + 256 + align256(tiles * 256 * 4 + 4);
+    return 2 * align256(n * 4) + 2 * align256(MAX_PASSES * 256 * 4) + 256 + align256(tiles * 256 * 8 + 8);
 }
 
 hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, uint64_t n, uint32_t bits, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    if (n >= (1ull << 30) || bits > 32) return hipErrorInvalidValue;
+    if (n > RADIX_SORT_MAX_PAIRS || bits > 32) return hipErrorInvalidValue;
     if (bits == 0) {
         hipError_t e = hipMemcpyAsync(keys_out, keys_in, n * 4, hipMemcpyDeviceToDevice, st);
         if (e == hipSuccess) e = hipMemcpyAsync(vals_out, vals_in, n * 4, hipMemcpyDeviceToDevice, st);
@@ -306,7 +307,7 @@ hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_
     p += align256(MAX_PASSES * 256 * 4);
     uint32_t* ctr = reinterpret_cast<uint32_t*>(p);
     p += 256;
-    uint32_t* status = reinterpret_cast<uint32_t*>(p);
+    uint64_t* status = reinterpret_cast<uint64_t*>(p);
 
     hipError_t e = hipMemsetAsync(hist, 0, MAX_PASSES * 256 * 4, st);
     if (e != hipSuccess) return e;
@@ -325,7 +326,7 @@ hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_
         uint32_t* dk = to_out ? keys_out : ktmp;
         uint32_t* dv = to_out ? vals_out : vtmp;
         if ((e = hipMemsetAsync(ctr, 0, 4, st)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(status, 0, (size_t)tiles * 256 * 4, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(status, 0, (size_t)tiles * 256 * 8, st)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_sort_pass, dim3(tiles), dim3(SORT_THREADS), SORT_LDS, st, sk, sv, dk, dv, (uint32_t)n,
                            pb.shift[q], pb.bits[q], base + q * 256, status, ctr);
         if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -237,7 +237,7 @@ DeviceMatrix KzgPcs::get_evaluations_on_domain(const std::vector<MatrixProverDat
 
 void KzgPcs::commit_quotient(const Domain& quotient_domain, const DeviceMatrix& quotient_evals, uint32_t num_chunks,
                              std::vector<std::vector<eon_g1_affine>>& commitments,
-                             std::vector<MatrixProverData>& data) {
+                             std::vector<MatrixProverData>& data, const std::vector<uint32_t>* only) {
     // split_evals: chunk c holds rows {i * num_chunks + c} (a strided column gather on device)
     if (quotient_evals.width != 1 || quotient_evals.height != quotient_domain.size() || num_chunks == 0 ||
         quotient_evals.height % num_chunks)
@@ -246,7 +246,10 @@ void KzgPcs::commit_quotient(const Domain& quotient_domain, const DeviceMatrix& 
     hipStream_t st = static_cast<hipStream_t>(eon_ctx_stream(ctx_));
     std::vector<std::pair<Domain, DeviceMatrix>> chunks;
     const std::vector<Domain> doms = quotient_domain.split_domains(num_chunks);
-    for (uint32_t c = 0; c < num_chunks; c++) {
+    std::vector<uint32_t> all(num_chunks);
+    for (uint32_t c = 0; c < num_chunks; c++) all[c] = c;
+    for (const uint32_t c : only ? *only : all) {
+        if (c >= num_chunks) throw Error(EON_E_ARG, "quotient chunk index out of range");
         DeviceMatrix m = DeviceMatrix::alloc(rows, 1);
         hip_check(hipMemcpy2DAsync(m.mutable_data(), sizeof(eon_fr), quotient_evals.data() + c,
                                    sizeof(eon_fr) * num_chunks, sizeof(eon_fr), rows, hipMemcpyDeviceToDevice, st),

@@ -128,14 +128,16 @@ class KzgPcs {
     // the auxiliary context, unless the main one is in serial mode (eon_ctx_set_serial: every
     // kernel alone on the device, for isolated profiles)
     eon_ctx* aux_live() const { return aux_ && !eon_ctx_serial(ctx_) ? aux_ : nullptr; }
-    // commit/src/pcs.rs:82-101 with split_evals (domain.rs:188-221)
+    // commit/src/pcs.rs:82-101 with split_evals (domain.rs:188-221).  `only` (optional) lists the
+    // chunks to commit, in order (the sharded prove gives chunk c to rank c % world); commitments
+    // and data then hold those chunks only.
     void commit_quotient(const Domain& quotient_domain, const DeviceMatrix& quotient_evals, uint32_t num_chunks,
-                         std::vector<std::vector<eon_g1_affine>>& commitments, std::vector<MatrixProverData>& data);
+                         std::vector<std::vector<eon_g1_affine>>& commitments, std::vector<MatrixProverData>& data,
+                         const std::vector<uint32_t>* only = nullptr);
     // pcs.rs:289-335: per (matrix, point) every column's value and witness.  The witness of
     // column c at z is the MSM of c's own coefficients against the opening bases H(z)
-    // (eon_kzg_opening_bases_create), reusing the digits sorted at commit time; without prepared
-    // digits (EON_KZG_OPEN=quotient) the synthetic-division quotients of one height are committed
-    // by one batched column MSM instead.
+    // (eon_kzg_opening_bases_create), reusing the digits sorted at commit time, so every matrix
+    // must come from commit / commit_columns (which keep those digits); otherwise EON_E_ARG.
     std::vector<Opened> open(const std::vector<OpenRound>& rounds);
 
   private:

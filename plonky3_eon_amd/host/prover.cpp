@@ -165,13 +165,34 @@ Proof prove(KzgPcs& pcs, const AirRef& air, const eon_fr* trace, uint64_t height
         (void)tick();
     }
     auto t3x = tick();
+    // commit_quotient (prover.rs:371-372).  Sharded, chunk c is committed and opened by rank
+    // c % world alone (commit/src/pcs.rs:82-101 commits the chunks independently) and the chunk
+    // commitments are all-gathered before zeta; unsharded, every chunk here.
+    std::vector<uint32_t> my_chunks;
+    for (uint32_t c = rank; c < num_chunks; c += world) my_chunks.push_back(c);
+    const uint32_t chunk_slots = (num_chunks + world - 1) / world;  // per rank, padded
     std::vector<std::vector<eon_g1_affine>> quotient_commit;
     std::vector<MatrixProverData> quotient_data;
-    pcs.commit_quotient(quotient_domain, qv, num_chunks, quotient_commit, quotient_data);  // :371-372
+    pcs.commit_quotient(quotient_domain, qv, num_chunks, quotient_commit, quotient_data, &my_chunks);
+    std::vector<eon_g1_affine> chunk_commit(num_chunks);
+    if (shard) {
+        std::vector<eon_g1_affine> mine(chunk_slots, eon_g1_affine{});
+        for (size_t i = 0; i < my_chunks.size(); i++) mine[i] = quotient_commit[i][0];
+        const uint64_t bytes = chunk_slots * sizeof(eon_g1_affine);
+        DeviceBuffer send(bytes), recv(bytes * world);
+        hip_ok(hipMemcpyAsync(send.get(), mine.data(), bytes, hipMemcpyHostToDevice, st), "quotient commit");
+        all_gather(ctx, shard, send.get(), recv.get(), bytes);
+        std::vector<eon_g1_affine> all((uint64_t)chunk_slots * world);
+        hip_ok(hipMemcpyAsync(all.data(), recv.get(), bytes * world, hipMemcpyDeviceToHost, st), "quotient commit");
+        hip_ok(hipStreamSynchronize(st), "quotient commit");
+        for (uint32_t c = 0; c < num_chunks; c++) chunk_commit[c] = all[(uint64_t)(c % world) * chunk_slots + c / world];
+    } else {
+        for (uint32_t c = 0; c < num_chunks; c++) chunk_commit[c] = quotient_commit[c][0];
+    }
     Fr zeta = zeta_in;
     if (challenger) {
-        for (const auto& m : quotient_commit) challenger->observe_g1(m.data(), m.size());  // :373
-        zeta = challenger->sample();                                                       // :416
+        for (const auto& q : chunk_commit) challenger->observe_g1(&q, 1);  // :373
+        zeta = challenger->sample();                                        // :416
     }
     proof.alpha = alpha;
     proof.zeta = zeta;
@@ -181,9 +202,9 @@ Proof prove(KzgPcs& pcs, const AirRef& air, const eon_fr* trace, uint64_t height
     rounds[0].data = &trace_data;
     rounds[0].points = {{zeta, zeta_next}};
     rounds[1].data = &quotient_data;
-    rounds[1].points.assign(num_chunks, std::vector<Fr>{zeta});
+    rounds[1].points.assign(quotient_data.size(), std::vector<Fr>{zeta});
     // the opening bases are the same on every rank: sharded over the process group
-    // (eon_ctx_set_collective; EON_OPEN_BASES_NO_SHARD=1 keeps them replicated)
+    // (eon_ctx_set_collective)
     struct CollectiveScope {
         eon_ctx* c;
         CollectiveScope(eon_ctx* c_, const eon_collective* s) : c(c_) {
@@ -198,13 +219,34 @@ Proof prove(KzgPcs& pcs, const AirRef& air, const eon_fr* trace, uint64_t height
     }
     auto t5 = tick();
 
-    proof.quotient_commit.resize(num_chunks);
+    proof.quotient_commit = chunk_commit;
     proof.quotient_opened.resize(num_chunks);
     proof.quotient_witnesses.resize(num_chunks);
-    for (uint32_t c = 0; c < num_chunks; c++) {
-        proof.quotient_commit[c] = quotient_commit[c][0];
-        proof.quotient_opened[c] = opened[1].values[c][0][0];
-        proof.quotient_witnesses[c] = opened[1].witnesses[c][0][0];
+    if (!shard) {
+        for (uint32_t c = 0; c < num_chunks; c++) {
+            proof.quotient_opened[c] = opened[1].values[c][0][0];
+            proof.quotient_witnesses[c] = opened[1].witnesses[c][0][0];
+        }
+    } else {
+        // every rank's chunk openings to every rank: value (4 u64) | witness (8 u64) per slot
+        constexpr uint32_t QREC = 12;
+        std::vector<uint64_t> rec((uint64_t)chunk_slots * QREC, 0);
+        for (size_t i = 0; i < my_chunks.size(); i++) {
+            std::memcpy(&rec[i * QREC], &opened[1].values[i][0][0], 32);
+            std::memcpy(&rec[i * QREC + 4], &opened[1].witnesses[i][0][0], 64);
+        }
+        const uint64_t bytes = rec.size() * sizeof(uint64_t);
+        DeviceBuffer send(bytes), recv(bytes * world);
+        hip_ok(hipMemcpyAsync(send.get(), rec.data(), bytes, hipMemcpyHostToDevice, st), "quotient openings");
+        all_gather(ctx, shard, send.get(), recv.get(), bytes);
+        std::vector<uint64_t> all(rec.size() * world);
+        hip_ok(hipMemcpyAsync(all.data(), recv.get(), bytes * world, hipMemcpyDeviceToHost, st), "quotient openings");
+        hip_ok(hipStreamSynchronize(st), "quotient openings");
+        for (uint32_t c = 0; c < num_chunks; c++) {
+            const uint64_t* r = &all[((uint64_t)(c % world) * chunk_slots + c / world) * QREC];
+            std::memcpy(&proof.quotient_opened[c], r, 32);
+            std::memcpy(&proof.quotient_witnesses[c], r + 4, 64);
+        }
     }
     const Opened& tr = opened[0];
     if (!shard) {

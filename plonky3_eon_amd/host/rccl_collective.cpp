@@ -2,6 +2,7 @@
 // per-column records) as ncclAllGather and the four-step DFT's transposes as ncclAllToAll, on
 // device buffers, enqueued on the context's stream -- xGMI peer-to-peer on an MI355X node, no host
 // staging.
+#include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
 #include <cstring>
@@ -24,9 +25,40 @@ int rccl_all_to_all(void* user, const void* send, void* recv, uint64_t bytes, vo
     return r == ncclSuccess ? 0 : -(int)r;
 }
 
+// Emulated exchanges for the one-GPU proxy of an N-rank prove: every slot of the all-gather's
+// output receives this rank's own block, and the all-to-all sends every block to itself, as
+// device-to-device copies on the same stream.  The bytes and the stream ordering are the real
+// collective's; the other ranks' data are not (the results are meaningless by design).
+int emulated_all_gather(void* user, const void* send, void* recv, uint64_t bytes, void* stream) {
+    const uint32_t world = (uint32_t)(uintptr_t)user;
+    for (uint32_t g = 0; g < world; g++)
+        if (hipMemcpyAsync(static_cast<char*>(recv) + (uint64_t)g * bytes, send, bytes, hipMemcpyDeviceToDevice,
+                           static_cast<hipStream_t>(stream)) != hipSuccess)
+            return 1;
+    return 0;
+}
+
+int emulated_all_to_all(void* user, const void* send, void* recv, uint64_t bytes, void* stream) {
+    const uint32_t world = (uint32_t)(uintptr_t)user;
+    return hipMemcpyAsync(recv, send, bytes * world, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)) ==
+                   hipSuccess
+               ? 0
+               : 1;
+}
+
 }  // namespace
 
 extern "C" {
+
+int eon_emulated_collective_init(uint32_t rank, uint32_t world, eon_collective* out) {
+    if (!out || world == 0 || rank >= world) return EON_E_ARG;
+    out->rank = rank;
+    out->world = world;
+    out->all_gather = emulated_all_gather;
+    out->all_to_all = emulated_all_to_all;
+    out->user = (void*)(uintptr_t)world;
+    return EON_OK;
+}
 
 int eon_rccl_unique_id(uint8_t id[128]) {
     if (!id) return EON_E_ARG;

@@ -51,6 +51,7 @@ SIGNATURES = {
     "eon_rccl_unique_id": (_INT, [_P]),
     "eon_rccl_collective_init": (_INT, [_U32, _U32, _P, ctypes.POINTER(eon_collective)]),
     "eon_rccl_collective_finalize": (None, [ctypes.POINTER(eon_collective)]),
+    "eon_emulated_collective_init": (_INT, [_U32, _U32, ctypes.POINTER(eon_collective)]),
     "eon_prove_p2air": (_INT, [_P, _P, _P, _U64, _P, _P, _U32, ctypes.POINTER(eon_collective),
                                ctypes.POINTER(eon_proof)]),
     "eon_poseidon2_bn254_permute": (_INT, [_P, _P]),
@@ -147,6 +148,18 @@ class RcclCollective:
             self.close()
         except Exception:
             pass
+
+
+class EmulatedCollective:
+    """eon_emulated_collective_init: the exchanges of rank `rank` in a `world`-rank prove emulated
+    on one GPU (bench.py --emulate-world): same bytes and stream order, own data in every slot."""
+
+    def __init__(self, rank: int, world: int):
+        self.lib = load()
+        self.c = eon_collective()
+        rc = self.lib.eon_emulated_collective_init(rank, world, ctypes.byref(self.c))
+        if rc != 0:
+            raise _lib.EonError(rc, "eon_emulated_collective_init")
 
 
 def _p(a):

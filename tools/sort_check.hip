@@ -44,6 +44,23 @@ __global__ void k_fill(uint32_t* k, uint32_t* v, uint32_t n, uint32_t c, uint32_
     v[i] = i;
 }
 
+// device check of a sort too large for the host: out[i] is input pair v[i] (k2[i] == k[v2[i]]),
+// keys non-decreasing on the sorted bits, values increasing within equal keys (stability), every
+// input index exactly once (bitmap)
+__global__ void k_check_big(const uint32_t* k, const uint32_t* k2, const uint32_t* v2, uint64_t n, uint32_t m,
+                            uint32_t* seen, unsigned long long* bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t vi = v2[i];
+    bool ok = vi < n && k2[i] == k[vi];
+    if (i > 0) {
+        const uint32_t a = k2[i - 1] & m, b = k2[i] & m;
+        ok = ok && (a < b || (a == b && v2[i - 1] < vi));
+    }
+    if (vi < n && (atomicOr(seen + vi / 32, 1u << (vi % 32)) >> (vi % 32) & 1)) ok = false;
+    if (!ok) atomicAdd(bad, 1ull);
+}
+
 static bool check(const std::vector<uint32_t>& kin, const std::vector<uint32_t>& kout, const std::vector<uint32_t>& vout,
                   uint32_t bits) {
     const size_t n = kin.size();
@@ -58,6 +75,48 @@ static bool check(const std::vector<uint32_t>& kin, const std::vector<uint32_t>&
 
 int main(int argc, char** argv) {
     const bool big = argc > 1 && std::string(argv[1]) == "big";
+    if (argc > 1 && std::string(argv[1]) == "huge") {
+        // beyond the 30-bit look-back counts of the round-3 sort: 2^30 + 4097 and
+        // 2^31 + 3 pairs, 16 key bits, checked on the device
+        for (uint64_t n : {(1ull << 30) + 4097, (1ull << 31) + 3}) {
+            const uint32_t bits = 16;
+            uint32_t *k, *v, *k2, *v2, *seen;
+            unsigned long long* bad;
+            CK(hipMalloc(&k, n * 4));
+            CK(hipMalloc(&v, n * 4));
+            CK(hipMalloc(&k2, n * 4));
+            CK(hipMalloc(&v2, n * 4));
+            CK(hipMalloc(&seen, (n / 32 + 1) * 4));
+            CK(hipMalloc(&bad, 8));
+            CK(hipMemset(seen, 0, (n / 32 + 1) * 4));
+            CK(hipMemset(bad, 0, 8));
+            hipLaunchKernelGGL(k_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, k, v, (uint32_t)n, bits,
+                               1u << 21, 0);
+            void* tmp;
+            CK(hipMalloc(&tmp, eon::radix_sort_temp_bytes(n, bits)));
+            hipEvent_t a, b;
+            hipEventCreate(&a);
+            hipEventCreate(&b);
+            hipEventRecord(a);
+            CK(eon::radix_sort_pairs(tmp, k, k2, v, v2, n, bits, 0));
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            float ms;
+            hipEventElapsedTime(&ms, a, b);
+            hipLaunchKernelGGL(k_check_big, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, k, k2, v2, n,
+                               (1u << bits) - 1, seen, bad);
+            unsigned long long nbad = 1;
+            CK(hipMemcpy(&nbad, bad, 8, hipMemcpyDeviceToHost));
+            printf("{\"case\":\"huge\",\"n\":%llu,\"bits\":%u,\"ms\":%.3f,\"bad\":%llu,\"ok\":%d}\n",
+                   (unsigned long long)n, bits, ms, nbad, (int)(nbad == 0));
+            // one past the limit must be refused, not sorted
+            const hipError_t e = eon::radix_sort_pairs(tmp, k, k2, v, v2, eon::RADIX_SORT_MAX_PAIRS + 1, bits, 0);
+            printf("{\"case\":\"limit\",\"n\":%llu,\"refused\":%d}\n",
+                   (unsigned long long)eon::RADIX_SORT_MAX_PAIRS + 1, (int)(e == hipErrorInvalidValue));
+            hipFree(tmp); hipFree(k); hipFree(v); hipFree(k2); hipFree(v2); hipFree(seen); hipFree(bad);
+        }
+        return 0;
+    }
     struct Case { uint32_t n, bits, mode; };
     std::vector<Case> cases = {{0, 16, 0}, {1, 16, 0}, {1000, 16, 0}, {8191, 16, 1}, {8192, 16, 0}, {8193, 16, 2},
                                {100003, 8, 1}, {100003, 19, 0}, {100003, 23, 1}, {1u << 20, 16, 0}, {(1u << 20) + 7, 32, 1},

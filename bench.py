@@ -76,6 +76,79 @@ def lde_mulmods(log_n: int, width: int, b: int) -> float:
     return width * ((1 + (1 << b)) * (n / 2) * log_n + n)
 
 
+class SclkSampler:
+    """The GPU's current shader clock (sysfs pp_dpm_sclk, the '*' level) sampled every 0.2 s in a
+    background thread while the timed steps run, so box-to-box clock differences under this VALU
+    load show in the bench line.  Only the card whose PCI address matches the device is read
+    when torch reports it; readings that are unavailable (no sysfs access) leave the field null."""
+
+    def __init__(self, dev):
+        import glob
+        import threading
+
+        self.samples = []
+        self.paths = sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk"))
+        try:
+            import torch
+
+            pr = torch.cuda.get_device_properties(dev)
+            bus = getattr(pr, "pci_bus_id", None)
+            dom = getattr(pr, "pci_domain_id", 0) or 0
+            pdev = getattr(pr, "pci_device_id", 0) or 0
+            if bus is not None:
+                tag = f"{dom:04x}:{bus:02x}:{pdev:02x}."
+                mine = [q for q in self.paths if tag in os.path.realpath(os.path.dirname(q))]
+                if mine:
+                    self.paths = mine
+        except Exception:
+            pass
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _read(self):
+        out = []
+        for q in self.paths:
+            try:
+                for line in open(q):
+                    if line.rstrip().endswith("*"):
+                        out.append(int(line.split(":")[1].strip().split("Mhz")[0].split("MHz")[0]))
+            except (OSError, ValueError, IndexError):
+                pass
+        return out
+
+    def _run(self):
+        while not self._stop.wait(0.2):
+            v = self._read()
+            if v:
+                self.samples.append(max(v) if len(v) > 1 and len(self.paths) > 1 else v[0])
+
+    def start(self):
+        if self.paths:
+            self._t.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        if self._t.is_alive():
+            self._t.join(timeout=1)
+        if not self.samples:
+            return None
+        xs = sorted(self.samples)
+        return {"median_mhz": xs[len(xs) // 2], "min_mhz": xs[0], "max_mhz": xs[-1], "samples": len(xs),
+                "source": "sysfs pp_dpm_sclk" + (" (%d cards, max)" % len(self.paths) if len(self.paths) > 1 else "")}
+
+
+def host_cpu() -> str:
+    """The host CPU model (/proc/cpuinfo), recorded beside every CPU baseline."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline_lde(log_n: int, width: int, b: int, sample_cols: int) -> dict:
     from oracle import coracle
 
@@ -87,14 +160,23 @@ def cpu_baseline_lde(log_n: int, width: int, b: int, sample_cols: int) -> dict:
     coracle.r2dp_coset_lde_batch(x, b, shift)
     dt = time.perf_counter() - t0
     scale = width / sample_cols
+    # T = 1 beside T = nproc: one thread on 2 sample columns
+    with coracle.threads(1):
+        t0 = time.perf_counter()
+        coracle.r2dp_coset_lde_batch(x[:, :2].copy(), b, shift)
+        dt1 = time.perf_counter() - t0
     return {
         "value": round(dt * scale * 1e3, 1),
         "unit": "ms",
         "cores": coracle.num_threads(),
         "kind": "port",
+        "host_cpu": host_cpu(),
         "sample": f"2^{log_n} rows x {sample_cols} of {width} columns (C restatement of "
         f"Radix2DitParallel::coset_lde_batch, OpenMP), {dt:.2f} s measured, x{scale:g} "
         f"extrapolated linearly in columns",
+        "t1": {"value": round(dt1 * width / 2 * 1e3, 1), "unit": "ms", "cores": 1,
+               "sample": f"2^{log_n} rows x 2 columns on one thread, {dt1:.2f} s measured, x{width / 2:g} "
+                         f"extrapolated linearly in columns"},
     }
 
 
@@ -106,13 +188,23 @@ def cpu_baseline_msm(bases_host: np.ndarray, scalars_host: np.ndarray) -> dict:
     t0 = time.perf_counter()
     coracle.g1_msm(bases_host, scalars_host)
     dt = time.perf_counter() - t0
+    # T = 1 beside T = nproc: one thread on the first n / 4 points
+    m = max(n // 4, 1)
+    with coracle.threads(1):
+        t0 = time.perf_counter()
+        coracle.g1_msm(bases_host[:m], scalars_host[:m])
+        dt1 = time.perf_counter() - t0
     return {
         "value": round(dt * 1e3, 1),
         "unit": "ms",
         "cores": coracle.num_threads(),
         "kind": "port",
+        "host_cpu": host_cpu(),
         "sample": f"full input: {n} points (C Pippenger restatement: signed windows, XYZZ mixed additions, OpenMP over "
         f"window x point-chunk tasks; halo2curves msm_best is not in the reference tree)",
+        "t1": {"value": round(dt1 * n / m * 1e3, 1), "unit": "ms", "cores": 1,
+               "sample": f"{m} of {n} points on one thread, {dt1:.2f} s measured, x{n / m:g} extrapolated "
+                         f"linearly (Pippenger's cost per point falls slowly with n: an upper bound)"},
     }
 
 
@@ -260,9 +352,12 @@ def cpu_baseline_prove(log_n: int, vl: int, consts, full: bool = False) -> dict:
     from oracle import coracle as C
 
     C.build()
-    measured = [_cpu_prove_e2e(8, vl, consts, True), _cpu_prove_e2e(10, vl, consts, False)]
-    if full:  # --cpu-full: the larger C4 (i) points (minutes)
-        measured += [_cpu_prove_e2e(10, vl, consts, True), _cpu_prove_e2e(12, vl, consts, False)]
+    # measured end-to-end proves at n = 8 (reference Horner LDE), 10 and 12
+    # (coset-DFT LDE substituted: the Horner loop alone is quadratic)
+    measured = [_cpu_prove_e2e(8, vl, consts, True), _cpu_prove_e2e(10, vl, consts, False),
+                _cpu_prove_e2e(12, vl, consts, False)]
+    if full:  # --cpu-full: 2^10 with the reference's Horner LDE as well (minutes)
+        measured += [_cpu_prove_e2e(10, vl, consts, True)]
     n = 1 << log_n
     w = 164 * vl
     q = 2 * n
@@ -298,12 +393,29 @@ def cpu_baseline_prove(log_n: int, vl: int, consts, full: bool = False) -> dict:
     comp["quotient_values"] = dt * q / 4096
     total = sum(comp.values())
     alt = total - comp["lde horner (reference)"] + lde_fft
+    # T = 1 beside T = nproc: the same components on one thread, smaller samples
+    comp1 = {}
+    with C.threads(1):
+        t0 = time.perf_counter(); C.idft_batch(x[:, :2].copy()); dt = time.perf_counter() - t0
+        comp1["trace idft"] = dt * w / 2
+        t0 = time.perf_counter(); C.g1_msm(pts, s); dt = time.perf_counter() - t0
+        comp1["msm x%d" % n_msm] = dt * n_msm
+        t0 = time.perf_counter(); C.eval_poly_col(coeffs, 0, C.fr_from_u64(7)); dt = time.perf_counter() - t0
+        comp1["lde horner (reference)"] = dt * q * w
+        t0 = time.perf_counter(); C.p2_quotient_values(lde_s[:512].copy(), 8, 1, vl, k, alpha); dt = time.perf_counter() - t0
+        comp1["quotient_values"] = dt * q / 512
+    total1 = sum(comp1.values())
     return {
         "value": round(total * 1e3, 1),
         "unit": "ms",
         "cores": C.num_threads(),
         "kind": "port",
+        "host_cpu": host_cpu(),
         "projected": True,
+        "t1": {"value": round(total1 * 1e3, 1), "unit": "ms", "cores": 1, "projected": True,
+               "components_ms": {k2: round(v * 1e3, 1) for k2, v in comp1.items()},
+               "sample": "the same full-size components on one thread (trace idft 2 columns, one 2^%d MSM, "
+                         "one Horner point, quotient 512 rows), scaled as the T = nproc leg" % log_n},
         "sample": "value = full-size prove PROJECTED as the sum of full-size component samples of the C "
                   "restatement (trace idft 16/%d cols, one measured 2^%d MSM x %d, Horner LDE 16 points, "
                   "quotient 4096 rows), reference algorithms incl. the Horner get_evaluations_on_domain; "
@@ -790,12 +902,14 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    sclk = SclkSampler(dev).start()
     t0 = time.perf_counter()
     for i in range(args.steps):
         wl.step()
         print(f"step {i}: {(time.perf_counter() - t0) * 1e3:.1f} ms since start", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    sclk_stats = sclk.stop()
     if world > 1:
         dist.barrier()
     # per-launch HIP-event timings come from extra steps after the timed region, run in serial
@@ -909,6 +1023,7 @@ def main() -> int:
         "data": "synthetic uniform Fr, resident in HBM",
         "config": {"workload": workload, "global_batch": gbatch, "seq_len": seq, "parallelism": par},
         "throughput": thr,
+        "gpu_sclk": sclk_stats,
         "roofline": roof,
         "cpu_baseline": None,
     }

@@ -56,6 +56,8 @@ def lib():
         l.or_fr_pow.argtypes = [fr_t, U64]
         l.or_fr_pow.restype = fr_t
         l.or_num_threads.restype = ctypes.c_int
+        l.or_set_num_threads.argtypes = [ctypes.c_int]
+        l.or_set_num_threads.restype = None
         l.or_eval_poly_col.argtypes = [P, U64, U64, U64, fr_t]
         l.or_eval_poly_col.restype = fr_t
         l.or_kzg_evaluations_on_domain.argtypes = [P, U64, U64, U32, fr_t, P]
@@ -316,6 +318,22 @@ def bary_eval_cols(evals, points):
 
 def num_threads() -> int:
     return lib().or_num_threads()
+
+
+class threads:
+    """`with threads(n):` -- OpenMP threads of the C restatement inside the block."""
+
+    def __init__(self, n: int):
+        self.n = n
+
+    def __enter__(self):
+        self.prev = num_threads()
+        lib().or_set_num_threads(self.n)
+        return self
+
+    def __exit__(self, *exc):
+        lib().or_set_num_threads(self.prev)
+        return False
 
 
 def random_fr(seed: int, n: int) -> np.ndarray:

@@ -460,6 +460,16 @@ int or_num_threads(void) {
 #endif
 }
 
+/* threads of every later parallel region (the cpu_baseline's T = 1 beside T = nproc) */
+void or_set_num_threads(int n) {
+#ifdef _OPENMP
+    extern void omp_set_num_threads(int);
+    omp_set_num_threads(n > 0 ? n : 1);
+#else
+    (void)n;
+#endif
+}
+
 /* ---- KzgPcs::get_evaluations_on_domain (kzg/src/pcs.rs:267-287) ----------------------------- */
 fr_t or_eval_poly_col(const fr_t* coeffs, uint64_t h, uint64_t w, uint64_t col, fr_t point) {
     /* eval_poly (kzg/src/util.rs:63-68): Horner from the top coefficient */

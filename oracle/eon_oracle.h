@@ -32,6 +32,7 @@ void or_r2dp_coset_lde_batch(const fr_t* in, fr_t* out, uint64_t h, uint64_t w, 
                              fr_t shift);
 
 int or_num_threads(void);
+void or_set_num_threads(int n);
 
 /* BN254 G1: affine x, y as Fq Montgomery [u64;4] LE; identity = (0, 0) (the C-ABI layout) */
 typedef struct {

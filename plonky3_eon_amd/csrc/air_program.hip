@@ -16,8 +16,11 @@
 // accumulator as a Horner chain acc = acc * alpha + C_k (folder.rs:81-85 with the reversed alpha
 // powers of prover.rs:578-579).  out[i] = acc * inv_vanishing[i] (prover.rs:699).  Every lane of
 // a wave executes the same instruction (uniform program counter: scalar instruction fetch, no
-// divergence); the register file lives in LDS (two 16-byte planes, conflict-free b128 access)
-// sized by the program's register count, or in a global buffer for very large programs.
+// divergence), with the trace / constant / selector operands of the NEXT instruction loaded while
+// the current one computes.  A value read only by the next instruction is forwarded in registers
+// (operand mode M_PREV, no register-file round trip).  The register file lives in LDS (two
+// 16-byte planes, conflict-free b128 access) sized by the program's register count, or in a global
+// buffer for very large programs.
 #include <algorithm>
 #include <cstdlib>
 #include <map>
@@ -32,8 +35,9 @@ namespace {
 
 enum : uint32_t { OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_NEG = 3, OP_ASSERT = 4 };
 // operand = mode << 29 | index
-enum : uint32_t { M_REG = 0, M_LOCAL = 1, M_NEXT = 2, M_CONST = 3, M_FIRST = 4, M_LAST = 5, M_TRANS = 6 };
+enum : uint32_t { M_REG = 0, M_LOCAL = 1, M_NEXT = 2, M_CONST = 3, M_FIRST = 4, M_LAST = 5, M_TRANS = 6, M_PREV = 7 };
 constexpr uint32_t IDX_MASK = (1u << 29) - 1;
+constexpr uint32_t NO_DST = ~0u;  // result only forwarded to the next instruction (M_PREV)
 
 struct Instr {
     uint32_t op, dst, a, b;
@@ -41,7 +45,8 @@ struct Instr {
 
 __device__ __forceinline__ Fr ld(const Fr* p) { return ld_pinned(p); }
 
-struct Regs {
+// register file in LDS (LDS = true) or in a global buffer: two 16-byte planes per register
+struct MemRegs {
     uint4* base;
     uint64_t stride;  // uint4 units between planes
     __device__ __forceinline__ Fr get(uint32_t r) const {
@@ -51,7 +56,7 @@ struct Regs {
         x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
         return x;
     }
-    __device__ __forceinline__ void set(uint32_t r, const Fr& x) const {
+    __device__ __forceinline__ void set(uint32_t r, const Fr& x) {
         base[(uint64_t)(2 * r) * stride] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
         base[(uint64_t)(2 * r + 1) * stride] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
     }
@@ -65,20 +70,81 @@ struct Window {
     uint64_t row, q;
 };
 
-__device__ __forceinline__ Fr fetch(uint32_t opnd, const Regs& rf, const Window& w) {
+__device__ __forceinline__ bool is_leaf(uint32_t opnd) {
+    const uint32_t m = opnd >> 29;
+    return m != M_REG && m != M_PREV;
+}
+
+// a leaf operand (trace cell, constant, selector); anything else reads as zero (unused)
+__device__ __forceinline__ Fr leaf(uint32_t opnd, const Window& w) {
     const uint32_t i = opnd & IDX_MASK;
     switch (opnd >> 29) {
-        case M_REG: return rf.get(i);
         case M_LOCAL: return ld(w.local + i);
         case M_NEXT: return ld(w.next + i);
         case M_CONST: return ld(w.table + i);
         case M_FIRST: return ld(w.sels + w.row);
         case M_LAST: return ld(w.sels + w.q + w.row);
-        default: return ld(w.sels + 2 * w.q + w.row);
+        case M_TRANS: return ld(w.sels + 2 * w.q + w.row);
+        default: return Fr::zero();
     }
 }
 
-template <bool LDS>
+__device__ __forceinline__ Instr uniform(const Instr& x) {
+    return Instr{(uint32_t)__builtin_amdgcn_readfirstlane(x.op), (uint32_t)__builtin_amdgcn_readfirstlane(x.dst),
+                 (uint32_t)__builtin_amdgcn_readfirstlane(x.a), (uint32_t)__builtin_amdgcn_readfirstlane(x.b)};
+}
+
+// The program with its leaf operands loaded one instruction ahead: while instruction pc computes,
+// the trace / constant / selector loads of instruction pc + 1 are in flight (the row-per-thread
+// reads of the LDE are uncoalesced, so their latency is what an unpipelined interpreter waits on)
+// and the fetch of instruction pc + 2 too.  Register operands (written by the instruction before)
+// are read when used; a forwarded result (M_PREV) never leaves registers.
+template <class RF>
+__device__ __forceinline__ void run_program(const Instr* __restrict__ code, uint32_t n_code, RF& rf, const Window& w,
+                                            const Fr& alpha, Fr& acc) {
+    if (n_code == 0) return;
+    Fr prev = Fr::zero();
+    Instr cur = uniform(code[0]);
+    Fr ca = leaf(cur.a, w), cb = cur.op == OP_ASSERT || cur.op == OP_NEG ? Fr::zero() : leaf(cur.b, w);
+    Instr nx = n_code > 1 ? code[1] : cur;
+    for (uint32_t pc = 0; pc < n_code; pc++) {
+        const Instr in = cur;
+        const Instr nu = uniform(nx);
+        Fr na = Fr::zero(), nb = Fr::zero();
+        if (pc + 1 < n_code) {
+            na = leaf(nu.a, w);
+            if (nu.op != OP_ASSERT && nu.op != OP_NEG) nb = leaf(nu.b, w);
+            if (pc + 2 < n_code) nx = code[pc + 2];
+        }
+        const uint32_t ma = in.a >> 29;
+        const Fr x = ma == M_PREV ? prev : ma == M_REG ? rf.get(in.a & IDX_MASK) : ca;
+        if (in.op == OP_ASSERT) {
+            acc = add(mul(acc, alpha), x);  // folder.rs:81-85, alpha powers reversed
+        } else {
+            Fr r;
+            if (in.op == OP_NEG) {
+                r = neg(x);
+            } else {
+                const uint32_t mb = in.b >> 29;
+                const Fr y = mb == M_PREV ? prev : mb == M_REG ? rf.get(in.b & IDX_MASK) : cb;
+                if (in.op == OP_MUL)
+                    r = mul(x, y);
+                else if (in.op == OP_ADD)
+                    r = add(x, y);
+                else
+                    r = sub(x, y);
+            }
+            prev = r;
+            if (in.dst != NO_DST) rf.set(in.dst, r);
+        }
+        cur = nu;
+        ca = na;
+        cb = nb;
+    }
+}
+
+// MODE 0: registers in LDS; 1: in the global buffer `gregs`
+template <int MODE>
 __global__ void __launch_bounds__(256) k_air_quotient(const Instr* __restrict__ code, uint32_t n_code,
                                                       const Fr* __restrict__ lde, uint32_t width, uint64_t q,
                                                       uint64_t next_step, const Fr* __restrict__ table,
@@ -88,36 +154,17 @@ __global__ void __launch_bounds__(256) k_air_quotient(const Instr* __restrict__ 
     extern __shared__ uint4 lds_regs[];
     const uint64_t row = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= q) return;
-    Regs rf;
-    if (LDS) {
+    Window w{lde + row * width, lde + ((row + next_step) & (q - 1)) * width, table, sels, row, q};
+    Fr acc = Fr::zero();
+    MemRegs rf;
+    if (MODE == 0) {
         rf.base = lds_regs + threadIdx.x;
         rf.stride = blockDim.x;
     } else {
         rf.base = gregs + row;
         rf.stride = q;
     }
-    Window w{lde + row * width, lde + ((row + next_step) & (q - 1)) * width, table, sels, row, q};
-    Fr acc = Fr::zero();
-    for (uint32_t pc = 0; pc < n_code; pc++) {
-        const Instr in = code[pc];
-        const Fr x = fetch(in.a, rf, w);
-        Fr r;
-        if (in.op == OP_ASSERT) {
-            acc = add(mul(acc, alpha), x);  // folder.rs:81-85, alpha powers reversed
-            continue;
-        } else if (in.op == OP_NEG) {
-            r = neg(x);
-        } else {
-            const Fr y = fetch(in.b, rf, w);
-            if (in.op == OP_MUL)
-                r = mul(x, y);
-            else if (in.op == OP_ADD)
-                r = add(x, y);
-            else
-                r = sub(x, y);
-        }
-        rf.set(in.dst, r);
-    }
+    run_program(code, n_code, rf, w, alpha, acc);
     st_vec(out + row, mul(acc, ld(inv_van + (row & nr_mask))));  // prover.rs:699
 }
 
@@ -304,11 +351,41 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
             if (x.op != OP_NEG) last[x.b] = (int64_t)t;
         }
     }
+    // forwarding: a value whose only reader is the very next item never touches the register
+    // file (the kernel keeps the previous result in registers, operand mode M_PREV)
+    std::vector<int64_t> first_read(nv, -1);
+    std::vector<uint32_t> n_readers(nv, 0);
+    {
+        std::vector<int64_t> last_reader(nv, -1);
+        for (size_t t = 0; t < items.size(); t++) {
+            const Item& it = items[t];
+            uint32_t rd[2] = {it.v, LEAF};
+            if (!it.assert_) {
+                rd[0] = vals[it.v].a;
+                rd[1] = vals[it.v].op == OP_NEG ? LEAF : vals[it.v].b;
+            }
+            for (uint32_t v : rd) {
+                if (v == LEAF || vals[v].op == LEAF || last_reader[v] == (int64_t)t) continue;
+                last_reader[v] = (int64_t)t;
+                n_readers[v]++;
+                if (first_read[v] < 0) first_read[v] = (int64_t)t;
+            }
+        }
+    }
+    std::vector<size_t> pos_of(nv, 0);
+    for (size_t t = 0; t < items.size(); t++)
+        if (!items[t].assert_) pos_of[items[t].v] = t;
+    auto forwarded = [&](uint32_t v) {
+        return vals[v].op != LEAF && n_readers[v] == 1 && first_read[v] == (int64_t)pos_of[v] + 1;
+    };
     // register allocation (lowest free register; operands freed before the result is assigned)
     std::vector<uint32_t> reg(nv, ~0u);
     std::vector<uint32_t> free_regs;
     uint32_t n_regs = 0;
-    auto opnd = [&](uint32_t v) { return vals[v].op == LEAF ? vals[v].a : (M_REG << 29 | reg[v]); };
+    auto opnd = [&](uint32_t v) {
+        if (vals[v].op == LEAF) return vals[v].a;
+        return forwarded(v) ? (M_PREV << 29) : (M_REG << 29 | reg[v]);
+    };
     auto release = [&](uint32_t v, size_t t) {
         if (vals[v].op != LEAF && last[v] == (int64_t)t && reg[v] != ~0u) {
             free_regs.push_back(reg[v]);
@@ -327,6 +404,11 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
         release(x.a, t);
         if (x.op != OP_NEG && x.b != x.a) release(x.b, t);
         if (last[it.v] < 0) continue;  // never read (cannot happen for reachable values)
+        if (forwarded(it.v)) {
+            in.dst = NO_DST;
+            p->code.push_back(in);
+            continue;
+        }
         uint32_t r;
         if (!free_regs.empty()) {
             r = free_regs.back();
@@ -454,7 +536,8 @@ int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const e
             inv_van = zh_inv;
         }
         const uint32_t nr_mask = prog->uses_sels ? (uint32_t)(q - 1) : (1u << log_qd) - 1;
-        // register file: LDS (block size shrinks with the register count), or global
+        // register file: LDS (block size shrinks with the register count), or global for very large
+        // programs (EON_AIR_REGS=global forces it, for tests)
         static const bool force_global = [] {
             const char* e = getenv("EON_AIR_REGS");
             return e && std::string(e) == "global";
@@ -462,29 +545,34 @@ int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const e
         const uint64_t per_thread = (uint64_t)prog->n_regs * sizeof(Fr);
         uint32_t block = 256;
         while (block > 64 && block * per_thread > 64 * 1024) block /= 2;
-        const bool lds = !force_global && block * per_thread <= 160 * 1024;
-        if (!lds) block = 256;
-        if (!lds) EON_HIP(prog->d_regs.ensure(std::max<uint64_t>(1, q * per_thread)));
+        const int mode = !force_global && block * per_thread <= 160 * 1024 ? 0 : 1;
+        if (mode != 0) block = 256;
+        if (mode == 1) EON_HIP(prog->d_regs.ensure(std::max<uint64_t>(1, q * per_thread)));
         const unsigned grid = (unsigned)((q + block - 1) / block);
-        const size_t shmem = lds ? (size_t)block * per_thread : 0;
-        const uint64_t mulmods = q * (uint64_t)(prog->code.size() + 1);
-        ctx->prof.begin("k_air_quotient", q * (uint64_t)prog->width * 32 + q * 32, ctx->stream, mulmods);
-        if (lds) {
+        const size_t shmem = mode == 0 ? (size_t)block * per_thread : 0;
+        // algorithmic 256-bit products per row: the program's multiplications, one acc * alpha per
+        // constraint (ASSERT) and the final inv_vanishing product (additions, subtractions and
+        // negations are not products)
+        uint64_t products = 1;
+        for (const Instr& in : prog->code) products += (in.op == OP_MUL || in.op == OP_ASSERT) ? 1 : 0;
+        ctx->prof.begin("k_air_quotient", q * (uint64_t)prog->width * 32 + q * 32, ctx->stream, q * products);
+        const Instr* code = prog->d_code.as<Instr>();
+        const uint32_t n_code = (uint32_t)prog->code.size();
+        const Fr* lde_f = reinterpret_cast<const Fr*>(lde);
+        const Fr* sel = prog->uses_sels ? prog->d_sels.as<Fr>() : nullptr;
+        Fr* out_f = reinterpret_cast<Fr*>(out);
+        if (mode == 0) {
             // per launch: the attribute is per device, and this context's device may differ from
             // the one another context set it on
-            EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_air_quotient<true>),
+            EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_air_quotient<0>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            hipLaunchKernelGGL(k_air_quotient<true>, dim3(grid), dim3(block), shmem, ctx->stream,
-                               prog->d_code.as<Instr>(), (uint32_t)prog->code.size(), reinterpret_cast<const Fr*>(lde),
-                               prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(),
-                               prog->uses_sels ? prog->d_sels.as<Fr>() : nullptr, inv_van, nr_mask, al,
-                               reinterpret_cast<Fr*>(out), nullptr);
+            hipLaunchKernelGGL(k_air_quotient<0>, dim3(grid), dim3(block), shmem, ctx->stream, code, n_code, lde_f,
+                               prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(), sel, inv_van, nr_mask, al, out_f,
+                               nullptr);
         } else {
-            hipLaunchKernelGGL(k_air_quotient<false>, dim3(grid), dim3(block), 0, ctx->stream,
-                               prog->d_code.as<Instr>(), (uint32_t)prog->code.size(), reinterpret_cast<const Fr*>(lde),
-                               prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(),
-                               prog->uses_sels ? prog->d_sels.as<Fr>() : nullptr, inv_van, nr_mask, al,
-                               reinterpret_cast<Fr*>(out), prog->d_regs.as<uint4>());
+            hipLaunchKernelGGL(k_air_quotient<1>, dim3(grid), dim3(block), 0, ctx->stream, code, n_code, lde_f,
+                               prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(), sel, inv_van, nr_mask, al, out_f,
+                               prog->d_regs.as<uint4>());
         }
         ctx->prof.end(ctx->stream);
         EON_HIP(hipGetLastError());

@@ -67,9 +67,10 @@ def test_quotient_values_vs_oracle(gpu_ctx, air_cls, fn, log_n, log_qd):
     assert got == want
 
 
-def test_register_file_in_global_memory(gpu_ctx):
-    """EON_AIR_REGS=global path gives the same values (run in a child process: the knob is read
-    once per process)."""
+def test_register_file_modes(gpu_ctx):
+    """The two register files of k_air_quotient -- LDS (the default) and global memory
+    (EON_AIR_REGS=global) -- give the same values (run in child processes: the knob is read once
+    per process); the default run is checked against the oracle by test_quotient_values_vs_oracle."""
     import os
     import subprocess
     import sys

@@ -15,10 +15,10 @@
 // matrix/src/lib.rs:392-411), the selectors of selectors_on_coset at i, and the folder's
 // accumulator as a Horner chain acc = acc * alpha + C_k (folder.rs:81-85 with the reversed alpha
 // powers of prover.rs:578-579).  out[i] = acc * inv_vanishing[i] (prover.rs:699).  Every lane of
-// a wave executes the same instruction (uniform program counter: scalar instruction fetch, no
-// divergence), with the trace / constant / selector operands of the NEXT instruction loaded while
-// the current one computes.  A value read only by the next instruction is forwarded in registers
-// (operand mode M_PREV, no register-file round trip).  The register file lives in LDS (two
+// a wave executes the same instruction (uniform program counter: scalar instruction fetch, the next
+// instruction's fetch issued before the current one executes, no divergence).  A value read only
+// by the next instruction is forwarded in registers (operand mode M_PREV, no register-file round
+// trip).  The register file lives in LDS (two
 // 16-byte planes, conflict-free b128 access) sized by the program's register count, or in a global
 // buffer for very large programs.
 #include <algorithm>
@@ -70,76 +70,50 @@ struct Window {
     uint64_t row, q;
 };
 
-__device__ __forceinline__ bool is_leaf(uint32_t opnd) {
-    const uint32_t m = opnd >> 29;
-    return m != M_REG && m != M_PREV;
-}
-
-// a leaf operand (trace cell, constant, selector); anything else reads as zero (unused)
-__device__ __forceinline__ Fr leaf(uint32_t opnd, const Window& w) {
+template <class RF>
+__device__ __forceinline__ Fr fetch(uint32_t opnd, const RF& rf, const Fr& prev, const Window& w) {
     const uint32_t i = opnd & IDX_MASK;
     switch (opnd >> 29) {
+        case M_REG: return rf.get(i);
         case M_LOCAL: return ld(w.local + i);
         case M_NEXT: return ld(w.next + i);
         case M_CONST: return ld(w.table + i);
         case M_FIRST: return ld(w.sels + w.row);
         case M_LAST: return ld(w.sels + w.q + w.row);
         case M_TRANS: return ld(w.sels + 2 * w.q + w.row);
-        default: return Fr::zero();
+        default: return prev;
     }
 }
 
-__device__ __forceinline__ Instr uniform(const Instr& x) {
-    return Instr{(uint32_t)__builtin_amdgcn_readfirstlane(x.op), (uint32_t)__builtin_amdgcn_readfirstlane(x.dst),
-                 (uint32_t)__builtin_amdgcn_readfirstlane(x.a), (uint32_t)__builtin_amdgcn_readfirstlane(x.b)};
-}
-
-// The program with its leaf operands loaded one instruction ahead: while instruction pc computes,
-// the trace / constant / selector loads of instruction pc + 1 are in flight (the row-per-thread
-// reads of the LDE are uncoalesced, so their latency is what an unpipelined interpreter waits on)
-// and the fetch of instruction pc + 2 too.  Register operands (written by the instruction before)
-// are read when used; a forwarded result (M_PREV) never leaves registers.
 template <class RF>
 __device__ __forceinline__ void run_program(const Instr* __restrict__ code, uint32_t n_code, RF& rf, const Window& w,
                                             const Fr& alpha, Fr& acc) {
-    if (n_code == 0) return;
     Fr prev = Fr::zero();
-    Instr cur = uniform(code[0]);
-    Fr ca = leaf(cur.a, w), cb = cur.op == OP_ASSERT || cur.op == OP_NEG ? Fr::zero() : leaf(cur.b, w);
-    Instr nx = n_code > 1 ? code[1] : cur;
+    Instr nx = n_code ? code[0] : Instr{OP_ASSERT, NO_DST, M_PREV << 29, 0};
     for (uint32_t pc = 0; pc < n_code; pc++) {
-        const Instr in = cur;
-        const Instr nu = uniform(nx);
-        Fr na = Fr::zero(), nb = Fr::zero();
-        if (pc + 1 < n_code) {
-            na = leaf(nu.a, w);
-            if (nu.op != OP_ASSERT && nu.op != OP_NEG) nb = leaf(nu.b, w);
-            if (pc + 2 < n_code) nx = code[pc + 2];
-        }
-        const uint32_t ma = in.a >> 29;
-        const Fr x = ma == M_PREV ? prev : ma == M_REG ? rf.get(in.a & IDX_MASK) : ca;
+        // uniform: every lane runs the same instruction, so the operand switch is scalar
+        const Instr in{(uint32_t)__builtin_amdgcn_readfirstlane(nx.op), (uint32_t)__builtin_amdgcn_readfirstlane(nx.dst),
+                       (uint32_t)__builtin_amdgcn_readfirstlane(nx.a), (uint32_t)__builtin_amdgcn_readfirstlane(nx.b)};
+        if (pc + 1 < n_code) nx = code[pc + 1];  // in flight while this instruction computes
+        const Fr x = fetch(in.a, rf, prev, w);
         if (in.op == OP_ASSERT) {
             acc = add(mul(acc, alpha), x);  // folder.rs:81-85, alpha powers reversed
-        } else {
-            Fr r;
-            if (in.op == OP_NEG) {
-                r = neg(x);
-            } else {
-                const uint32_t mb = in.b >> 29;
-                const Fr y = mb == M_PREV ? prev : mb == M_REG ? rf.get(in.b & IDX_MASK) : cb;
-                if (in.op == OP_MUL)
-                    r = mul(x, y);
-                else if (in.op == OP_ADD)
-                    r = add(x, y);
-                else
-                    r = sub(x, y);
-            }
-            prev = r;
-            if (in.dst != NO_DST) rf.set(in.dst, r);
+            continue;
         }
-        cur = nu;
-        ca = na;
-        cb = nb;
+        Fr r;
+        if (in.op == OP_NEG) {
+            r = neg(x);
+        } else {
+            const Fr y = fetch(in.b, rf, prev, w);
+            if (in.op == OP_MUL)
+                r = mul(x, y);
+            else if (in.op == OP_ADD)
+                r = add(x, y);
+            else
+                r = sub(x, y);
+        }
+        prev = r;
+        if (in.dst != NO_DST) rf.set(in.dst, r);
     }
 }
 

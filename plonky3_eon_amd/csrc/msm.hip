@@ -96,42 +96,60 @@ __device__ __forceinline__ uint32_t window_bits(const uint32_t* s, uint32_t pos,
 // pairs run over buckets b' = (|digit| - 1) * groups + group, each contiguous.
 constexpr uint32_t DIGIT_COLS = 4;  // widest scalar tile of one 256-thread block: 64 rows x 4 cols
 
+// The digit sort's per-pass histograms of the keys (radix_sort_histograms) are counted here, in
+// LDS per block and added to the global bins once per block, so the sort never re-reads the keys
+// for them.
 __global__ void __launch_bounds__(256) k_msm_digits(const Fr* scalars, uint64_t n, uint64_t ld,
                                                     uint32_t cols, uint32_t c, uint32_t windows,
                                                     uint32_t ref_windows, uint32_t precomputed,
-                                                    uint32_t tile_cols, uint32_t* keys, uint32_t* vals) {
+                                                    uint32_t tile_cols, uint32_t* keys, uint32_t* vals,
+                                                    RadixPasses pb, uint32_t* hist) {
+    __shared__ uint32_t h[RADIX_SORT_MAX_PASSES][256];
+    for (uint32_t j = threadIdx.x; j < RADIX_SORT_MAX_PASSES * 256; j += 256) (&h[0][0])[j] = 0;
+    __syncthreads();
     // a block reads 256 / tile_cols row segments of tile_cols adjacent columns (up to 128
     // contiguous bytes), so the group-major writes stay in runs of consecutive rows
     const uint32_t col = blockIdx.y * tile_cols + threadIdx.x % tile_cols;
     const uint64_t i = (uint64_t)blockIdx.x * (256 / tile_cols) + threadIdx.x / tile_cols;
-    if (col >= cols || i >= n) return;
-    Fr s = to_canonical(ld_pinned(scalars + i * ld + col));
-    pin(s);
-    const uint32_t B = 1u << (c - 1);
-    uint32_t carry = 0;
-    for (uint32_t w = 0; w < windows; w++) {
-        const uint32_t raw = window_bits(s.v, w * c, c) + carry;
-        uint32_t mag;
-        uint32_t neg;
-        if (raw > B) {  // signed digit raw - 2^c in [-(B-1), -1], carry into the next window
-            mag = (1u << c) - raw;
-            neg = 1;
-            carry = 1;
-        } else {
-            mag = raw;
-            neg = 0;
-            carry = 0;
+    if (col < cols && i < n) {
+        Fr s = to_canonical(ld_pinned(scalars + i * ld + col));
+        pin(s);
+        const uint32_t B = 1u << (c - 1);
+        uint32_t carry = 0;
+        for (uint32_t w = 0; w < windows; w++) {
+            const uint32_t raw = window_bits(s.v, w * c, c) + carry;
+            uint32_t mag;
+            uint32_t neg;
+            if (raw > B) {  // signed digit raw - 2^c in [-(B-1), -1], carry into the next window
+                mag = (1u << c) - raw;
+                neg = 1;
+                carry = 1;
+            } else {
+                mag = raw;
+                neg = 0;
+                carry = 0;
+            }
+            const uint64_t e = ((uint64_t)col * windows + w) * n + i;
+            uint32_t key;
+            if (mag == 0) {
+                key = 0xFFFFFFFFu;
+                vals[e] = 0;
+            } else {
+                const uint32_t g = precomputed ? col : col * windows + w;
+                key = (g << c) | (mag - 1);
+                const uint32_t ref = precomputed ? (uint32_t)(i * ref_windows + w) : (uint32_t)i;
+                vals[e] = ref | (neg << 31);
+            }
+            keys[e] = key;
+#pragma unroll
+            for (uint32_t p = 0; p < RADIX_SORT_MAX_PASSES; p++)
+                if (p < pb.passes) atomicAdd(&h[p][(key >> pb.shift[p]) & ((1u << pb.bits[p]) - 1)], 1u);
         }
-        const uint64_t e = ((uint64_t)col * windows + w) * n + i;
-        if (mag == 0) {
-            keys[e] = 0xFFFFFFFFu;
-            vals[e] = 0;
-        } else {
-            const uint32_t g = precomputed ? col : col * windows + w;
-            keys[e] = (g << c) | (mag - 1);
-            const uint32_t ref = precomputed ? (uint32_t)(i * ref_windows + w) : (uint32_t)i;
-            vals[e] = ref | (neg << 31);
-        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < pb.passes * 256; j += 256) {
+        const uint32_t v = (&h[0][0])[j];
+        if (v) atomicAdd(hist + j, v);
     }
 }
 
@@ -203,22 +221,6 @@ __global__ void k_piece_owner(const uint32_t* piece_off, uint32_t nb, uint32_t* 
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     for (uint32_t p = piece_off[b]; p < piece_off[b + 1]; p++) owner[p] = b;
-}
-
-// count[b] = the chunk-aligned runs bucket b's pairs [start[b], start[b+1]) touch (0 if empty),
-// i.e. the pieces bucket b will hold; stat[0] = their maximum over buckets (atomicMax, one per
-// wave and only while it can raise the maximum; stat[0] zeroed before)
-__global__ void k_chunk_count(const uint32_t* start, uint32_t nb, uint32_t log_chunk, uint32_t* count,
-                              uint32_t* stat) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t v = 0;
-    if (b <= nb) {
-        const uint32_t s = b == nb ? 0 : start[b], e = b == nb ? 0 : start[b + 1];
-        v = s == e ? 0 : ((e - 1) >> log_chunk) - (s >> log_chunk) + 1;
-        count[b] = v;
-    }
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o));
-    if ((threadIdx.x & 63) == 0 && v > 1 && v > __atomic_load_n(stat, __ATOMIC_RELAXED)) atomicMax(stat, v);
 }
 
 #ifndef EON_PIECE_MINWAVES
@@ -860,8 +862,8 @@ static std::vector<Batch> make_batches(const Fr* scalars, uint32_t width, uint64
 
 // The digit sort: sort.hip's stable LSD radix sort (two 8-bit passes for c = 16)
 static hipError_t sort_pairs(void* temp, const uint32_t* k_in, uint32_t* k_out, const uint32_t* v_in,
-                             uint32_t* v_out, uint64_t n, uint32_t bits, hipStream_t st) {
-    return radix_sort_pairs(temp, k_in, k_out, v_in, v_out, n, bits, st);
+                             uint32_t* v_out, uint64_t n, uint32_t bits, hipStream_t st, bool hist_ready) {
+    return radix_sort_pairs(temp, k_in, k_out, v_in, v_out, n, bits, st, hist_ready);
 }
 
 // digits + radix sort + bucket starts + piece offsets of one batch into `out`; `wk` supplies the
@@ -888,7 +890,6 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     EON_HIP(out.vals2.ensure(E * 4));
     EON_HIP(out.start.ensure((nb + 1) * 4ull));
     EON_HIP(out.piece_off.ensure((nb + 1) * 4ull));
-    EON_HIP(wk.count.ensure((nb + 1) * 4ull));
     bt.sort_bytes = radix_sort_temp_bytes(E, bt.key_bits);
     bt.scan_bytes = exclusive_scan_temp_bytes(nb + 1);
     EON_HIP(wk.temp.ensure(std::max(bt.sort_bytes, bt.scan_bytes)));
@@ -898,27 +899,29 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     if (!wk.host_counts) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&wk.host_counts), 64));
 
     Profiler* prof = &ctx->prof;
+    uint32_t* hist = radix_sort_histograms(wk.temp.p, E);
+    EON_HIP(hipMemsetAsync(hist, 0, RADIX_SORT_MAX_PASSES * 256 * 4, st));
     prof->begin("k_msm_digits", n * bt.cols * 32 + E * 8, st);
     const uint32_t tile_cols = bt.cols >= DIGIT_COLS ? DIGIT_COLS : (bt.cols >= 2 ? 2 : 1);
     const uint32_t tile_rows = 256 / tile_cols;
     hipLaunchKernelGGL(k_msm_digits, dim3((unsigned)((n + tile_rows - 1) / tile_rows),
                                           (bt.cols + tile_cols - 1) / tile_cols),
                        dim3(256), 0, st, bt.scalars, n, ld, bt.cols, bt.c, bt.W, L.W, (uint32_t)L.precomputed,
-                       tile_cols, wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>());
+                       tile_cols, wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>(), radix_sort_passes(bt.key_bits),
+                       hist);
     prof->end(st);
     EON_HIP(hipGetLastError());
     prof->begin("radix_sort_pairs", E * 16, st);
     EON_HIP(sort_pairs(wk.temp.p, wk.keys.as<uint32_t>(), out.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
-                       out.vals2.as<uint32_t>(), E, bt.key_bits, st));
+                       out.vals2.as<uint32_t>(), E, bt.key_bits, st, true));
     prof->end(st);
     hipLaunchKernelGGL(k_bucket_start, dim3(blocks_for(E / 4 + 1, 256)), dim3(256), 0, st,
                        out.keys2.as<uint32_t>(), E, bt.c, bt.groups, nb, out.start.as<uint32_t>());
     // the most pieces one bucket holds fixes the combine levels (no read-backs in the reduction)
     EON_HIP(wk.stat.ensure(16));
     EON_HIP(hipMemsetAsync(wk.stat.p, 0, 16, st));
-    hipLaunchKernelGGL(k_chunk_count, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, st,
-                       out.start.as<uint32_t>(), nb, bt.log_chunk, wk.count.as<uint32_t>(), wk.stat.as<uint32_t>());
-    EON_HIP(exclusive_scan_u32(wk.temp.p, wk.count.as<uint32_t>(), out.piece_off.as<uint32_t>(), nb + 1, st));
+    EON_HIP(exclusive_scan_chunk_counts(wk.temp.p, out.start.as<uint32_t>(), nb, bt.log_chunk,
+                                        out.piece_off.as<uint32_t>(), wk.stat.as<uint32_t>(), st));
     // launches are sized by the real counts (12-byte read-back: pieces, nonzero digits, max pieces)
     EON_HIP(hipMemcpyAsync(wk.host_counts, out.piece_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
     EON_HIP(hipMemcpyAsync(wk.host_counts + 1, out.start.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));

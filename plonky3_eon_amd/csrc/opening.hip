@@ -23,7 +23,13 @@ using namespace eon;
 
 namespace {
 
-constexpr uint32_t SCAN = 16;  // points summed per thread at each level of the prefix sum
+// points summed per thread at each level of the prefix sum: 16 for long scans (fewer levels, the
+// chip full anyway); 4 below 2^16 points (a sharded slice), where the levels' serial chains of
+// additions on a few waves set the time
+constexpr uint32_t SCAN = 16, SCAN_SMALL = 4;
+inline uint32_t scan_chunk(uint64_t len) { return len >= (1ull << 16) ? SCAN : SCAN_SMALL; }
+// scratch points of scan_exclusive over len points: len / chunk + len / chunk^2 + ... < len / (chunk - 1)
+inline uint64_t scan_tmp_points(uint64_t len) { return len / (SCAN_SMALL - 1) + 64; }
 
 // k * G for an affine G and a canonical 254-bit k (double-and-add, MSB first)
 __device__ G1Xyzz smul_affine(const G1Affine& g, const Fr& k) {
@@ -51,23 +57,23 @@ __global__ void k_open_scale(const G1Affine* g, uint64_t n, Fr zinv, G1Xyzz* out
     st_xyzz(out + i, smul_affine(ld_affine(g + i), k));
 }
 
-// tot[t] = sum of a[SCAN t .. SCAN t + SCAN)
-__global__ void k_scan_totals(const G1Xyzz* a, uint64_t len, G1Xyzz* tot) {
+// tot[t] = sum of a[chunk t .. chunk t + chunk)
+__global__ void k_scan_totals(const G1Xyzz* a, uint64_t len, uint32_t chunk, G1Xyzz* tot) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t i0 = t * SCAN;
+    const uint64_t i0 = t * chunk;
     if (i0 >= len) return;
-    const uint64_t i1 = i0 + SCAN < len ? i0 + SCAN : len;
+    const uint64_t i1 = i0 + chunk < len ? i0 + chunk : len;
     G1Xyzz acc = ld_xyzz(a + i0);
     for (uint64_t i = i0 + 1; i < i1; i++) acc = xyzz_add(acc, ld_xyzz(a + i));
     st_xyzz(tot + t, acc);
 }
 
 // a <- exclusive prefix sums, chunk t starting from carry[t] (the exclusive prefix of the totals)
-__global__ void k_scan_apply(G1Xyzz* a, uint64_t len, const G1Xyzz* carry) {
+__global__ void k_scan_apply(G1Xyzz* a, uint64_t len, uint32_t chunk, const G1Xyzz* carry) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t i0 = t * SCAN;
+    const uint64_t i0 = t * chunk;
     if (i0 >= len) return;
-    const uint64_t i1 = i0 + SCAN < len ? i0 + SCAN : len;
+    const uint64_t i1 = i0 + chunk < len ? i0 + chunk : len;
     G1Xyzz acc = ld_xyzz(carry + t);
     for (uint64_t i = i0; i < i1; i++) {
         const G1Xyzz v = ld_xyzz(a + i);
@@ -241,13 +247,151 @@ __global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, const 
     st_xyzz(out + i, x29_to_xyzz(acc, inf));
 }
 
+// GLV for BN254 G1: phi(x, y) = (beta x, y) = lambda (x, y) with lambda^2 + lambda + 1 = 0 mod r
+// (beta a cube root of unity in Fq; the pair is fixed by phi(G) = lambda G for the generator,
+// tools/glv_consts.py).  k = k1 + k2 lambda mod r with |k1|, |k2| < 2^127 from the reduced lattice
+// basis (a1, b1), (a2, b2) of {(a, b) : a + b lambda = 0 mod r} (Gallant-Lambert-Vanstone):
+// c1 = floor(k g1 / 2^256), c2 = floor(k g2 / 2^256) with g1 = round(b2 2^256 / r),
+// g2 = round(-b1 2^256 / r); k1 = k - c1 a1 - c2 a2, k2 = -c1 b1 - c2 b2.  32-bit limbs.
+namespace glv {
+constexpr uint32_t G1[3] = {0xc7e0b3d7u, 0xd91d232eu, 0x2u};
+constexpr uint32_t G2[5] = {0x391eb18eu, 0x7a7bd9d4u, 0xa773d2cfu, 0x4ccef014u, 0x2u};
+constexpr uint32_t A1[2] = {0x94d213e3u, 0x89d32568u};                           // a1 = b2
+constexpr uint32_t A2[4] = {0x1221250bu, 0xbe4e154u, 0xeeb859fdu, 0x6f4d8248u};
+constexpr uint32_t NB1[4] = {0x7d4f1128u, 0x8211bbebu, 0xeeb859fcu, 0x6f4d8248u};  // -b1
+// beta in 29-Montgomery form (beta 2^261 mod q)
+constexpr uint32_t BETA29[9] = {0xa337995u, 0x158d1d23u, 0x189c9b98u, 0x12fa4e45u, 0x185faadcu,
+                                0x176f16du,  0xeed93bau,  0x14291140u, 0xc0afeu};
+}  // namespace glv
+
+// acc -= x c or acc += x c, modulo 2^160 (5 limbs); x, c small little-endian limb arrays
+template <int NX, int NC>
+__device__ __forceinline__ void mac160(uint32_t acc[5], const uint32_t (&x)[NX], const uint32_t (&c)[NC], bool sub) {
+    uint32_t p[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < NX; i++) {
+        uint64_t carry = 0;
+#pragma unroll
+        for (int j = 0; j < NC; j++) {
+            if (i + j >= 5) break;
+            const uint64_t t = (uint64_t)x[i] * c[j] + p[i + j] + carry;
+            p[i + j] = (uint32_t)t;
+            carry = t >> 32;
+        }
+        if (i + NC < 5) p[i + NC] = (uint32_t)carry;
+    }
+    uint64_t t = 0;
+    if (sub) {
+        uint32_t br = 0;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            t = (uint64_t)acc[i] - p[i] - br;
+            acc[i] = (uint32_t)t;
+            br = (uint32_t)(t >> 63);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            t = (uint64_t)acc[i] + p[i] + (t >> 32);
+            acc[i] = (uint32_t)t;
+        }
+    }
+}
+
+// floor(k g / 2^256) for the canonical k (8 limbs) and a constant g: the product's limbs >= 8
+template <int NG, int NOUT>
+__device__ __forceinline__ void mul_hi256(const uint32_t (&k)[8], const uint32_t (&g)[NG], uint32_t (&out)[NOUT]) {
+    uint32_t p[8 + NG];
+#pragma unroll
+    for (int i = 0; i < 8 + NG; i++) p[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint64_t carry = 0;
+#pragma unroll
+        for (int j = 0; j < NG; j++) {
+            const uint64_t t = (uint64_t)k[i] * g[j] + p[i + j] + carry;
+            p[i + j] = (uint32_t)t;
+            carry = t >> 32;
+        }
+        p[i + NG] = (uint32_t)carry;
+    }
+#pragma unroll
+    for (int i = 0; i < NOUT; i++) out[i] = p[8 + i];
+}
+
+// |k_i| (4 limbs, < 2^127) and sign of the GLV halves of the canonical k
+__device__ __forceinline__ void glv_split(const Fr& k, uint32_t (&u1)[4], bool& neg1, uint32_t (&u2)[4], bool& neg2) {
+    uint32_t kk[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) kk[i] = k.v[i];
+    uint32_t c1[3], c2[4];
+    mul_hi256(kk, glv::G1, c1);
+    mul_hi256(kk, glv::G2, c2);
+    uint32_t k1[5] = {kk[0], kk[1], kk[2], kk[3], kk[4]}, k2[5] = {0, 0, 0, 0, 0};
+    mac160(k1, c1, glv::A1, true);
+    mac160(k1, c2, glv::A2, true);
+    mac160(k2, c1, glv::NB1, false);
+    mac160(k2, c2, glv::A1, true);  // b2 = a1
+    auto mag = [](uint32_t (&v)[5], uint32_t (&u)[4], bool& neg) __attribute__((always_inline)) {
+        neg = (v[4] >> 31) != 0;  // |v| < 2^127: bit 159 is the sign
+        uint64_t t = neg ? 1 : 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            t += neg ? (uint64_t)(~v[i]) : (uint64_t)v[i];
+            u[i] = (uint32_t)t;
+            t >>= 32;
+        }
+    };
+    mag(k1, u1, neg1);
+    mag(k2, u2, neg2);
+}
+
+// odd u (< 2^128) -> 32 odd digits in [-15, 15]: nibble i of dg[] = (|d_i| - 1) / 2 | sign << 3,
+// digit 31 the remaining top in [1, 15] (u = sum d_i 16^i)
+__device__ __forceinline__ void recode_odd128(uint32_t (&kw)[4], uint32_t (&dg)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) dg[q] = 0;
+#pragma unroll
+    for (int i = 0; i < 31; i++) {
+        const int32_t d = (int32_t)(kw[0] & 31u) - 16;
+        if (d >= 0) {
+            uint64_t c = (uint64_t)kw[0] - (uint32_t)d;
+            kw[0] = (uint32_t)c;
+            uint32_t br = (uint32_t)(c >> 63);
+#pragma unroll
+            for (int q = 1; q < 4; q++) {
+                c = (uint64_t)kw[q] - br;
+                kw[q] = (uint32_t)c;
+                br = (uint32_t)(c >> 63);
+            }
+        } else {
+            uint64_t c = (uint64_t)kw[0] + (uint32_t)(-d);
+            kw[0] = (uint32_t)c;
+            uint32_t cy = (uint32_t)(c >> 32);
+#pragma unroll
+            for (int q = 1; q < 4; q++) {
+                c = (uint64_t)kw[q] + cy;
+                kw[q] = (uint32_t)c;
+                cy = (uint32_t)(c >> 32);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 3; q++) kw[q] = (kw[q] >> 4) | (kw[q + 1] << 28);
+        kw[3] >>= 4;
+        const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+        dg[i >> 3] |= (((mag - 1) >> 1) | (d < 0 ? 8u : 0u)) << (4 * (i & 7));
+    }
+    dg[3] |= ((kw[0] - 1) >> 1) << 28;
+}
+
 // H_j = z^(j-1) S_j, then its window table 2^(16 w) H_j, w < TW, by doublings: tmp[j TW + w]
-// (radix-2^32 XYZZ).  The scalar multiplication uses REGULAR signed 4-bit windows (no lane
-// divergence: every lane adds at every window): k = z^(j-1) made odd (k + 1 when even, S_j
-// subtracted at the end) is recoded into 64 odd digits in [-15, 15] (d = (k mod 32) - 16,
-// k <- (k - d) / 16), and the odd multiples S, 3S, .., 15S live in the thread's column of `mtab`
-// (MTAB raw accumulators per thread, coalesced across threads): 256 doublings + 64 additions,
-// against ~254 + ~254 (divergent) for double-and-add.
+// (radix-2^32 XYZZ).  The scalar multiplication is GLV + Straus: z^(j-1) = k1 + k2 lambda, and
+// k1 S + k2 phi(S) runs one doubling chain for both halves (~127 doublings instead of ~254).  Each
+// half is made odd (|k| + 1 when even, that S or phi(S) subtracted at the end) and recoded into 32
+// odd signed 4-bit digits, so every level adds one entry of each half: the odd multiples S, 3S, ..,
+// 15S live in the thread's column of `mtab` (MTAB raw accumulators per thread, coalesced across
+// threads) and phi of an entry is beta times its X.  128 doublings + 64 additions + 8 multiples,
+// against 252 + 64 + 8 for the plain signed windows.
 // rows j = lo + t, t < cnt; s and tmp are the slice's (rows >= n are the identity)
 constexpr uint32_t MTAB = 8;
 
@@ -263,9 +407,12 @@ __global__ void __launch_bounds__(64) k_open_finish29(const G1Affine* s_slice, u
     const G1Affine a = (j && j < n) ? ld_affine(s + j) : G1Affine{Fq::zero(), Fq::zero()};
     if (!is_inf(a)) {
         const F29 x = unpack29(to_fq261(a.x)), y = unpack29(to_fq261(a.y));
-        Fr k = to_canonical(pow_u64(z, j - 1));
-        const bool even = (k.v[0] & 1) == 0;
-        if (even) k.v[0] += 1;  // no carry: k even
+        uint32_t u1[4], u2[4];
+        bool neg1, neg2;
+        glv_split(to_canonical(pow_u64(z, j - 1)), u1, neg1, u2, neg2);
+        const bool even1 = (u1[0] & 1) == 0, even2 = (u2[0] & 1) == 0;
+        u1[0] |= 1u;  // + 1 when even (no carry)
+        u2[0] |= 1u;
         // the odd multiples (2m + 1) S, m < MTAB
         {
             G1X29 two = dbl29_affine(x, y), m;
@@ -280,62 +427,46 @@ __global__ void __launch_bounds__(64) k_open_finish29(const G1Affine* s_slice, u
                 st_raw29(mtab + (uint64_t)q * cnt + t, m);
             }
         }
-        // recoding: 64 odd digits, nibble i of dg[] = (|d_i| - 1) / 2 | sign << 3
-        uint32_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        uint32_t kw[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) kw[q] = k.v[q];
-#pragma unroll
-        for (int i = 0; i < 63; i++) {
-            const int32_t d = (int32_t)(kw[0] & 31u) - 16;
-            // k - d (|d| <= 15, odd), then >> 4 (exact)
-            if (d >= 0) {
-                uint64_t c = (uint64_t)kw[0] - (uint32_t)d;
-                kw[0] = (uint32_t)c;
-                uint32_t br = (uint32_t)(c >> 63);
-#pragma unroll
-                for (int q = 1; q < 8; q++) {
-                    c = (uint64_t)kw[q] - br;
-                    kw[q] = (uint32_t)c;
-                    br = (uint32_t)(c >> 63);
-                }
-            } else {
-                uint64_t c = (uint64_t)kw[0] + (uint32_t)(-d);
-                kw[0] = (uint32_t)c;
-                uint32_t cy = (uint32_t)(c >> 32);
-#pragma unroll
-                for (int q = 1; q < 8; q++) {
-                    c = (uint64_t)kw[q] + cy;
-                    kw[q] = (uint32_t)c;
-                    cy = (uint32_t)(c >> 32);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 7; q++) kw[q] = (kw[q] >> 4) | (kw[q + 1] << 28);
-            kw[7] >>= 4;
-            const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
-            dg[i >> 3] |= (((mag - 1) >> 1) | (d < 0 ? 8u : 0u)) << (4 * (i & 7));
-        }
-        // the top digit: the rest, odd, in [1, 15] (k < 2^254)
-        dg[7] |= ((kw[0] - 1) >> 1) << 28;
-        G1X29 e;
-        (void)ld_raw29(mtab + (uint64_t)((dg[7] >> 28) & 7u) * cnt + t, e);
-        acc = e;
-        inf = false;
-        for (int i = 62; i >= 0; i--) {
-            dbl29(acc);
-            dbl29(acc);
-            dbl29(acc);
-            dbl29(acc);
-            const uint32_t nib = (dg[i >> 3] >> (4 * (i & 7))) & 15u;
+        uint32_t dg1[4], dg2[4];
+        recode_odd128(u1, dg1);
+        recode_odd128(u2, dg2);
+        // the table entry of digit nibble `nib` of a half, times -1 when the half is negative
+        auto entry = [&](uint32_t nib, bool phi, bool neg) __attribute__((always_inline)) {
+            G1X29 e;
             (void)ld_raw29(mtab + (uint64_t)(nib & 7u) * cnt + t, e);
-            if (nib & 8u) e.Y = sub29<FqP, 4>(F29{}, e.Y);  // -(x, y): Y < 4p
-            acc29(acc, inf, e, false);
+            if (phi) e.X = mul29<FqP>(e.X, const29<FqP>(glv::BETA29));
+            if (((nib >> 3) & 1u) != (uint32_t)neg) e.Y = sub29<FqP, 4>(F29{}, e.Y);  // -(x, y): Y < 4p
+            return e;
+        };
+        // digits are consumed from the top: nibble 31 of each word stream, then the stream shifts
+        // left by 4 (no dynamically indexed digit array, which would live in scratch)
+        auto shl4 = [](uint32_t (&d)[4]) __attribute__((always_inline)) {
+            d[3] = (d[3] << 4) | (d[2] >> 28);
+            d[2] = (d[2] << 4) | (d[1] >> 28);
+            d[1] = (d[1] << 4) | (d[0] >> 28);
+            d[0] <<= 4;
+        };
+        acc = entry((dg1[3] >> 28) & 7u, false, neg1);
+        inf = false;
+        acc29(acc, inf, entry((dg2[3] >> 28) & 7u, true, neg2), false);
+        for (int i = 30; i >= 0; i--) {
+            shl4(dg1);
+            shl4(dg2);
+            if (!inf) {
+                dbl29(acc);
+                dbl29(acc);
+                dbl29(acc);
+                dbl29(acc);
+            }
+#pragma unroll 1
+            for (int h = 0; h < 2; h++) {  // one copy of the addition for both halves
+                const uint32_t nib = (h ? dg2[3] : dg1[3]) >> 28;
+                acc29(acc, inf, entry(nib, h == 1, h ? neg2 : neg1), false);
+            }
         }
-        if (even) {
-            const F29 ny = sub29<FqP, 1>(F29{}, y);  // y canonical < p
-            madd29_any(acc, inf, x, ny);
-        }
+        // the +1 of an even half: add the digit -1 of that half (its sign folded in)
+        if (even1) acc29(acc, inf, entry(8u, false, neg1), false);
+        if (even2) acc29(acc, inf, entry(8u, true, neg2), false);
     }
     G1Xyzz* dst = tmp + j * TW;
     for (uint32_t w = 0; w < TW; w++) {
@@ -361,16 +492,17 @@ __global__ void k_add_rank_offset(G1Xyzz* s, uint64_t cnt, const G1Affine* total
 
 unsigned grid_for(uint64_t threads, uint32_t block) { return (unsigned)((threads + block - 1) / block); }
 
-// exclusive prefix sum of a[0..len) in place; tmp holds >= len / SCAN + len / SCAN^2 + ... points
-void scan_exclusive(G1Xyzz* a, uint64_t len, G1Xyzz* tmp, hipStream_t st) {
-    if (len <= SCAN) {
+// exclusive prefix sum of a[0..len) in place; tmp holds scan_tmp_points(len) points
+void scan_exclusive(G1Xyzz* a, uint64_t len, G1Xyzz* tmp, hipStream_t st, uint32_t chunk = 0) {
+    if (!chunk) chunk = scan_chunk(len);
+    if (len <= chunk) {
         hipLaunchKernelGGL(k_scan_serial, dim3(1), dim3(1), 0, st, a, len);
         return;
     }
-    const uint64_t nt = (len + SCAN - 1) / SCAN;
-    hipLaunchKernelGGL(k_scan_totals, dim3(grid_for(nt, 64)), dim3(64), 0, st, a, len, tmp);
-    scan_exclusive(tmp, nt, tmp + nt, st);
-    hipLaunchKernelGGL(k_scan_apply, dim3(grid_for(nt, 64)), dim3(64), 0, st, a, len, tmp);
+    const uint64_t nt = (len + chunk - 1) / chunk;
+    hipLaunchKernelGGL(k_scan_totals, dim3(grid_for(nt, 64)), dim3(64), 0, st, a, len, chunk, tmp);
+    scan_exclusive(tmp, nt, tmp + nt, st, chunk);
+    hipLaunchKernelGGL(k_scan_apply, dim3(grid_for(nt, 64)), dim3(64), 0, st, a, len, chunk, tmp);
 }
 
 // one point's scratch, alive until its stream is synchronised
@@ -385,7 +517,7 @@ struct Scratch {
 Status opening_bases_async29(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, const Fr& z, hipStream_t st,
                              Scratch& sc, eon_msm_bases** out) {
     EON_HIP(sc.pts.ensure(n * sizeof(G1Xyzz)));
-    EON_HIP(sc.tmp.ensure((n / (SCAN - 1) + 64) * sizeof(G1Xyzz)));
+    EON_HIP(sc.tmp.ensure(scan_tmp_points(n) * sizeof(G1Xyzz)));
     EON_HIP(sc.aff.ensure(n * sizeof(G1Affine)));
     EON_HIP(sc.table_tmp.ensure(n * TW * sizeof(G1Xyzz)));
     eon_msm_bases* b = nullptr;
@@ -400,8 +532,8 @@ Status opening_bases_async29(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
     ctx->prof.end(st);
     scan_exclusive(sc.pts.as<G1Xyzz>(), n, sc.tmp.as<G1Xyzz>(), st);
     EON_HIP(launch_batch_to_affine(sc.pts.as<G1Xyzz>(), n, sc.aff.as<G1Affine>(), st));
-    // 256 dbl + 64 add (12M+2S) + 8 multiples, then 240 dbl for the window table
-    ctx->prof.begin("k_open_finish29", n * (64ull + TW * 128ull), st, n * 5300ull);
+    // GLV: 124 dbl + 64 add (12M+2S) + 8 multiples, then 240 dbl for the window table
+    ctx->prof.begin("k_open_finish29", n * (64ull + TW * 128ull), st, n * 4170ull);
     hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(n, 64)), dim3(64), 0, st, sc.aff.as<G1Affine>(), n, 0ull, n, z,
                        sc.mtab.as<G1Raw29>(), sc.table_tmp.as<G1Xyzz>());
     ctx->prof.end(st);
@@ -429,7 +561,7 @@ Status opening_bases_async(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, c
         EON_HIP(hipGetLastError());
     } else {
         EON_HIP(sc.pts.ensure(n * sizeof(G1Xyzz)));
-        EON_HIP(sc.tmp.ensure((n / (SCAN - 1) + 64) * sizeof(G1Xyzz)));
+        EON_HIP(sc.tmp.ensure(scan_tmp_points(n) * sizeof(G1Xyzz)));
         EON_HIP(sc.aff.ensure(n * sizeof(G1Affine)));
         // algorithmic cost: 2 scalar multiplications per point, ~254 dbl (6M+3S) + ~127 madd (8M+2S)
         ctx->prof.begin("k_open_scale", n * (64ull + 128ull), st, n * 3556ull);
@@ -485,7 +617,7 @@ Status opening_bases_sharded(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
     for (uint32_t t = 0; t < np; t++) {
         hipStream_t st = streams[t % 3];
         EON_HIP(sc[t].pts.ensure((m + 1) * sizeof(G1Xyzz)));
-        EON_HIP(sc[t].tmp.ensure(((m + 1) / (SCAN - 1) + 64) * sizeof(G1Xyzz)));
+        EON_HIP(sc[t].tmp.ensure(scan_tmp_points(m + 1) * sizeof(G1Xyzz)));
         EON_HIP(sc[t].aff.ensure(m * sizeof(G1Affine)));
         EON_HIP(sc[t].table_tmp.ensure(slice_entries * sizeof(G1Xyzz)));
         EON_HIP(sc[t].mtab.ensure(m * MTAB * sizeof(G1Raw29)));
@@ -515,7 +647,7 @@ Status opening_bases_sharded(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
             hipLaunchKernelGGL(k_add_rank_offset, dim3(grid_for(m, 64)), dim3(64), 0, st, sc[t].pts.as<G1Xyzz>(), m,
                                all_totals.as<G1Affine>(), np, t, rank);
         EON_HIP(launch_batch_to_affine(sc[t].pts.as<G1Xyzz>(), m, sc[t].aff.as<G1Affine>(), st));
-        ctx->prof.begin("k_open_finish29", m * (64ull + TW * 128ull), st, m * 5300ull);
+        ctx->prof.begin("k_open_finish29", m * (64ull + TW * 128ull), st, m * 4170ull);
         hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(m, 64)), dim3(64), 0, st, sc[t].aff.as<G1Affine>(), n, lo,
                            m, zs[t], sc[t].mtab.as<G1Raw29>(), sc[t].table_tmp.as<G1Xyzz>());
         ctx->prof.end(st);

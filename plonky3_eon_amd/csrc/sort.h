@@ -11,6 +11,18 @@ namespace eon {
 // Largest n radix_sort_pairs takes: u32 positions, the last tile's indices must not wrap.
 constexpr uint64_t RADIX_SORT_MAX_PAIRS = (1ull << 32) - 8192;
 
+// The LSD passes of a sort on `bits` low key bits: pass p sorts key bits [shift[p], shift[p] +
+// bits[p]) (<= 8 bits each).  A producer of the keys may count every pass's 256-bin histogram
+// itself (radix_sort_histograms: hist[p * 256 + digit], zeroed first) and then call
+// radix_sort_pairs with hist_ready, which skips the sort's own histogram read of the keys.
+constexpr uint32_t RADIX_SORT_MAX_PASSES = 4;
+struct RadixPasses {
+    uint32_t shift[RADIX_SORT_MAX_PASSES], bits[RADIX_SORT_MAX_PASSES];
+    uint32_t passes;
+};
+RadixPasses radix_sort_passes(uint32_t bits);
+uint32_t* radix_sort_histograms(void* temp, uint64_t n);
+
 // Scratch bytes of radix_sort_pairs for n pairs sorted on `bits` low key bits.
 size_t radix_sort_temp_bytes(uint64_t n, uint32_t bits);
 
@@ -21,12 +33,19 @@ size_t radix_sort_temp_bytes(uint64_t n, uint32_t bits);
 // global digit offsets by a decoupled look-back over the preceding tiles, after one histogram
 // kernel for every pass.  `temp` holds radix_sort_temp_bytes(n, bits) bytes.
 hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
-                            uint32_t* vals_out, uint64_t n, uint32_t bits, hipStream_t st);
+                            uint32_t* vals_out, uint64_t n, uint32_t bits, hipStream_t st, bool hist_ready = false);
 
 // Scratch bytes of exclusive_scan_u32 for n elements.
 size_t exclusive_scan_temp_bytes(uint64_t n);
 
 // out[i] = in[0] + ... + in[i-1] (out[0] = 0), n < 2^32, sums modulo 2^32; in != out.
 hipError_t exclusive_scan_u32(void* temp, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t st);
+
+// The MSM's piece offsets: the exclusive scan (nb + 1 outputs, exclusive_scan_temp_bytes(nb + 1)
+// scratch) of count[b] = the 2^log_chunk-aligned runs bucket b's pairs [start[b], start[b + 1])
+// touch (0 if empty; count[nb] = 0), computed from `start` on the fly -- no count array -- and
+// *max_out raised to the largest count when that exceeds 1 (max_out zeroed before).
+hipError_t exclusive_scan_chunk_counts(void* temp, const uint32_t* start, uint32_t nb, uint32_t log_chunk,
+                                       uint32_t* out, uint32_t* max_out, hipStream_t st);
 
 }  // namespace eon

@@ -30,13 +30,10 @@ constexpr uint32_t SORT_THREADS = 512, SORT_WAVES = SORT_THREADS / 64, SORT_ITEM
 constexpr uint32_t SORT_TILE = SORT_THREADS * SORT_ITEMS;
 constexpr uint64_t ST_AGG = 1ull << 62, ST_INC = 2ull << 62, ST_COUNT = (1ull << 62) - 1;
 static_assert(RADIX_SORT_MAX_PAIRS == (1ull << 32) - SORT_TILE, "sort.h's limit is this tile's");
-constexpr uint32_t MAX_PASSES = 4;
+constexpr uint32_t MAX_PASSES = RADIX_SORT_MAX_PASSES;
 constexpr size_t SORT_LDS = (size_t)SORT_TILE * 8 + SORT_WAVES * 256 * 4 + 2 * 256 * 4 + 64;
 
-struct PassBits {
-    uint32_t shift[MAX_PASSES], bits[MAX_PASSES];
-    uint32_t passes;
-};
+using PassBits = RadixPasses;
 
 PassBits split_bits(uint32_t bits) {
     PassBits pb{};
@@ -229,18 +226,41 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* wsu
     return scan256(v, wsum, tot);
 }
 
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce(const uint32_t* __restrict__ in, uint64_t n,
-                                                              uint32_t* __restrict__ bsum) {
+// the scanned values: a u32 array, or the MSM's piece counts computed from its bucket starts
+struct PlainIn {
+    const uint32_t* in;
+    __device__ __forceinline__ uint32_t operator()(uint64_t i) const { return in[i]; }
+};
+struct ChunkCountIn {
+    const uint32_t* start;  // nb + 1 entries
+    uint32_t nb, log_chunk;
+    __device__ __forceinline__ uint32_t operator()(uint64_t b) const {
+        if (b >= nb) return 0;
+        const uint32_t s = start[b], e = start[b + 1];
+        return s == e ? 0 : ((e - 1) >> log_chunk) - (s >> log_chunk) + 1;
+    }
+};
+
+// per-block sums; with max_out, also the largest value (atomicMax, only where it exceeds 1)
+template <class In>
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce(In in, uint64_t n, uint32_t* __restrict__ bsum,
+                                                              uint32_t* max_out) {
     __shared__ uint32_t wsum[4];
     const uint64_t t0 = (uint64_t)blockIdx.x * SCAN_TILE;
-    uint32_t s = 0;
+    uint32_t s = 0, mx = 0;
     for (uint32_t j = 0; j < SCAN_ITEMS; j++) {
         const uint64_t i = t0 + j * SCAN_THREADS + threadIdx.x;
-        s += i < n ? in[i] : 0u;
+        const uint32_t v = i < n ? in(i) : 0u;
+        s += v;
+        mx = max(mx, v);
     }
     uint32_t tot;
     (void)block_excl_scan256(s, wsum, tot);
     if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+    if (max_out) {
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
+        if ((threadIdx.x & 63) == 0 && mx > 1 && mx > __atomic_load_n(max_out, __ATOMIC_RELAXED)) atomicMax(max_out, mx);
+    }
 }
 
 // exclusive scan of the m block sums in place (one block)
@@ -257,15 +277,16 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_top(uint32_t* bsum, uint3
     }
 }
 
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(const uint32_t* __restrict__ in, uint64_t n,
-                                                             const uint32_t* __restrict__ bsum, uint32_t* __restrict__ out) {
+template <class In>
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(In in, uint64_t n, const uint32_t* __restrict__ bsum,
+                                                             uint32_t* __restrict__ out) {
     __shared__ uint32_t wsum[4];
     // blocked: thread t owns elements [t0 + t ITEMS, t0 + (t + 1) ITEMS)
     const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
     uint32_t v[SCAN_ITEMS], s = 0;
 #pragma unroll
     for (uint32_t j = 0; j < SCAN_ITEMS; j++) {
-        v[j] = i0 + j < n ? in[i0 + j] : 0u;
+        v[j] = i0 + j < n ? in(i0 + j) : 0u;
         s += v[j];
     }
     uint32_t tot;
@@ -277,7 +298,24 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(const uint32_t* __r
     }
 }
 
+template <class In>
+hipError_t scan_with(void* temp, In in, uint32_t* out, uint64_t n, uint32_t* max_out, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)((n + SCAN_TILE - 1) / SCAN_TILE);
+    uint32_t* bsum = static_cast<uint32_t*>(temp);
+    hipLaunchKernelGGL(k_scan_reduce<In>, dim3(blocks), dim3(SCAN_THREADS), 0, st, in, n, bsum, max_out);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_THREADS), 0, st, bsum, blocks);
+    hipLaunchKernelGGL(k_scan_apply<In>, dim3(blocks), dim3(SCAN_THREADS), 0, st, in, n, bsum, out);
+    return hipGetLastError();
+}
+
 }  // namespace
+
+RadixPasses radix_sort_passes(uint32_t bits) { return split_bits(bits); }
+
+uint32_t* radix_sort_histograms(void* temp, uint64_t n) {
+    return reinterpret_cast<uint32_t*>(static_cast<char*>(temp) + 2 * align256(n * 4));
+}
 
 size_t radix_sort_temp_bytes(uint64_t n, uint32_t bits) {
     const uint64_t tiles = (n + SORT_TILE - 1) / SORT_TILE;
@@ -286,7 +324,7 @@ size_t radix_sort_temp_bytes(uint64_t n, uint32_t bits) {
 }
 
 hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
-                            uint32_t* vals_out, uint64_t n, uint32_t bits, hipStream_t st) {
+                            uint32_t* vals_out, uint64_t n, uint32_t bits, hipStream_t st, bool hist_ready) {
     if (n == 0) return hipSuccess;
     if (n > RADIX_SORT_MAX_PAIRS || bits > 32) return hipErrorInvalidValue;
     if (bits == 0) {
@@ -309,10 +347,12 @@ hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_
     p += 256;
     uint64_t* status = reinterpret_cast<uint64_t*>(p);
 
-    hipError_t e = hipMemsetAsync(hist, 0, MAX_PASSES * 256 * 4, st);
-    if (e != hipSuccess) return e;
-    const uint32_t hblocks = (uint32_t)std::min<uint64_t>((n + 512ull * 16 - 1) / (512ull * 16), 2048);
-    hipLaunchKernelGGL(k_sort_hist, dim3(hblocks), dim3(512), 0, st, keys_in, (uint32_t)n, pb, hist);
+    hipError_t e = hipSuccess;
+    if (!hist_ready) {
+        if ((e = hipMemsetAsync(hist, 0, MAX_PASSES * 256 * 4, st)) != hipSuccess) return e;
+        const uint32_t hblocks = (uint32_t)std::min<uint64_t>((n + 512ull * 16 - 1) / (512ull * 16), 2048);
+        hipLaunchKernelGGL(k_sort_hist, dim3(hblocks), dim3(512), 0, st, keys_in, (uint32_t)n, pb, hist);
+    }
     hipLaunchKernelGGL(k_sort_base, dim3(1), dim3(256), 0, st, hist, pb.passes, base);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_sort_pass), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -339,13 +379,12 @@ hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_
 size_t exclusive_scan_temp_bytes(uint64_t n) { return align256(((n + SCAN_TILE - 1) / SCAN_TILE + 1) * 4); }
 
 hipError_t exclusive_scan_u32(void* temp, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t st) {
-    if (n == 0) return hipSuccess;
-    const uint32_t blocks = (uint32_t)((n + SCAN_TILE - 1) / SCAN_TILE);
-    uint32_t* bsum = static_cast<uint32_t*>(temp);
-    hipLaunchKernelGGL(k_scan_reduce, dim3(blocks), dim3(SCAN_THREADS), 0, st, in, n, bsum);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_THREADS), 0, st, bsum, blocks);
-    hipLaunchKernelGGL(k_scan_apply, dim3(blocks), dim3(SCAN_THREADS), 0, st, in, n, bsum, out);
-    return hipGetLastError();
+    return scan_with(temp, PlainIn{in}, out, n, nullptr, st);
+}
+
+hipError_t exclusive_scan_chunk_counts(void* temp, const uint32_t* start, uint32_t nb, uint32_t log_chunk,
+                                       uint32_t* out, uint32_t* max_out, hipStream_t st) {
+    return scan_with(temp, ChunkCountIn{start, nb, log_chunk}, out, (uint64_t)nb + 1, max_out, st);
 }
 
 }  // namespace eon

@@ -114,23 +114,25 @@ inline void mont_mul_lazy(const uint64_t a[4], const uint64_t b[4], uint64_t out
 
 // The same product with MULX and the two carry chains of ADCX / ADOX (BMI2 + ADX): ~2x lower
 // latency than the compiler's code for the u128 form above, which matters because the sponge's
-// partial rounds are one dependent chain of products.  Register roles rotate over the four rounds
-// (T0 of a round is zero after its reduction and becomes the next round's carry word), so no
-// moves between rounds.  Same bounds as mont_mul_lazy; the clang and gcc assemblers accept these
-// instructions without target flags, and kCpuAdx gates every use at run time.
-#define EON_FR_ADX_ROUND(BOFF, T0, T1, T2, T3, T4) \
-    "movq " BOFF "(%[b]), %%rdx\n\t"              \
+// partial rounds are one dependent chain of products.  `a` is passed in four registers (no store /
+// reload on the chain), `b` word by word into rdx from memory or registers.  Register roles rotate
+// over the four rounds (T0 of a round is zero after its reduction and becomes the next round's
+// carry word), so no moves between rounds.  Same bounds as mont_mul_lazy; the clang and gcc
+// assemblers accept these instructions without target flags, and kCpuAdx gates every use at run
+// time.
+#define EON_FR_ADX_ROUND(BSRC, T0, T1, T2, T3, T4) \
+    "movq " BSRC ", %%rdx\n\t"                     \
     "xorl %k[lo], %k[lo]\n\t"                     \
-    "mulxq 0(%[a]), %[lo], %[hi]\n\t"             \
+    "mulxq %[a0], %[lo], %[hi]\n\t"               \
     "adoxq %[lo], " T0 "\n\t"                     \
     "adcxq %[hi], " T1 "\n\t"                     \
-    "mulxq 8(%[a]), %[lo], %[hi]\n\t"             \
+    "mulxq %[a1], %[lo], %[hi]\n\t"               \
     "adoxq %[lo], " T1 "\n\t"                     \
     "adcxq %[hi], " T2 "\n\t"                     \
-    "mulxq 16(%[a]), %[lo], %[hi]\n\t"            \
+    "mulxq %[a2], %[lo], %[hi]\n\t"               \
     "adoxq %[lo], " T2 "\n\t"                     \
     "adcxq %[hi], " T3 "\n\t"                     \
-    "mulxq 24(%[a]), %[lo], %[hi]\n\t"            \
+    "mulxq %[a3], %[lo], %[hi]\n\t"               \
     "adoxq %[lo], " T3 "\n\t"                     \
     "adcxq %[hi], " T4 "\n\t"                     \
     "movl $0, %k[lo]\n\t"                         \
@@ -152,21 +154,40 @@ inline void mont_mul_lazy(const uint64_t a[4], const uint64_t b[4], uint64_t out
     "adoxq %[hi], " T4 "\n\t"                     \
     "movl $0, %k[lo]\n\t"                         \
     "adcxq %[lo], " T4 "\n\t"
+#define EON_FR_ADX_OUTS                                                                                 \
+    [r0] "+&r"(r0), [r1] "+&r"(r1), [r2] "+&r"(r2), [r3] "+&r"(r3), [r4] "+&r"(r4), [lo] "=&r"(lo), \
+        [hi] "=&r"(hi)
+#define EON_FR_ADX_CONSTS                                                                         \
+    [p0] "m"(Fr::P[0]), [p1] "m"(Fr::P[1]), [p2] "m"(Fr::P[2]), [p3] "m"(Fr::P[3]), [inv] "m"(Fr::INV)
 
 inline void mont_mul_adx(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]) {
     uint64_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0, lo, hi;
-    asm(EON_FR_ADX_ROUND("0", "%[r0]", "%[r1]", "%[r2]", "%[r3]", "%[r4]")
-        EON_FR_ADX_ROUND("8", "%[r1]", "%[r2]", "%[r3]", "%[r4]", "%[r0]")
-        EON_FR_ADX_ROUND("16", "%[r2]", "%[r3]", "%[r4]", "%[r0]", "%[r1]")
-        EON_FR_ADX_ROUND("24", "%[r3]", "%[r4]", "%[r0]", "%[r1]", "%[r2]")
-        : [r0] "+&r"(r0), [r1] "+&r"(r1), [r2] "+&r"(r2), [r3] "+&r"(r3), [r4] "+&r"(r4), [lo] "=&r"(lo),
-          [hi] "=&r"(hi)
-        : [a] "r"(a), [b] "r"(b), "m"(*(const uint64_t(*)[4])a), "m"(*(const uint64_t(*)[4])b),
-          [p0] "m"(Fr::P[0]), [p1] "m"(Fr::P[1]), [p2] "m"(Fr::P[2]), [p3] "m"(Fr::P[3]), [inv] "m"(Fr::INV)
+    asm(EON_FR_ADX_ROUND("0(%[b])", "%[r0]", "%[r1]", "%[r2]", "%[r3]", "%[r4]")
+        EON_FR_ADX_ROUND("8(%[b])", "%[r1]", "%[r2]", "%[r3]", "%[r4]", "%[r0]")
+        EON_FR_ADX_ROUND("16(%[b])", "%[r2]", "%[r3]", "%[r4]", "%[r0]", "%[r1]")
+        EON_FR_ADX_ROUND("24(%[b])", "%[r3]", "%[r4]", "%[r0]", "%[r1]", "%[r2]")
+        : EON_FR_ADX_OUTS
+        : [a0] "r"(a[0]), [a1] "r"(a[1]), [a2] "r"(a[2]), [a3] "r"(a[3]), [b] "r"(b),
+          "m"(*(const uint64_t(*)[4])b), EON_FR_ADX_CONSTS
+        : "rdx", "cc");
+    out[0] = r4, out[1] = r0, out[2] = r1, out[3] = r2;
+}
+
+// a * a: both operands in registers
+inline void mont_sqr_adx(const uint64_t a[4], uint64_t out[4]) {
+    uint64_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0, lo, hi;
+    asm(EON_FR_ADX_ROUND("%[a0]", "%[r0]", "%[r1]", "%[r2]", "%[r3]", "%[r4]")
+        EON_FR_ADX_ROUND("%[a1]", "%[r1]", "%[r2]", "%[r3]", "%[r4]", "%[r0]")
+        EON_FR_ADX_ROUND("%[a2]", "%[r2]", "%[r3]", "%[r4]", "%[r0]", "%[r1]")
+        EON_FR_ADX_ROUND("%[a3]", "%[r3]", "%[r4]", "%[r0]", "%[r1]", "%[r2]")
+        : EON_FR_ADX_OUTS
+        : [a0] "r"(a[0]), [a1] "r"(a[1]), [a2] "r"(a[2]), [a3] "r"(a[3]), EON_FR_ADX_CONSTS
         : "rdx", "cc");
     out[0] = r4, out[1] = r0, out[2] = r1, out[3] = r2;
 }
 #undef EON_FR_ADX_ROUND
+#undef EON_FR_ADX_OUTS
+#undef EON_FR_ADX_CONSTS
 
 // BMI2 (CPUID.7.0:EBX bit 8) and ADX (bit 19); EON_HOST_NO_ADX=1 forces the portable product
 inline bool detect_adx() {
@@ -217,6 +238,15 @@ inline FrLazy lz_mul(const FrLazy& a, const FrLazy& b) {
         detail::mont_mul_adx(a.l, b.l, r.l);
     else
         detail::mont_mul_lazy(a.l, b.l, r.l);
+    return r;
+}
+template <bool ADX = false>
+inline FrLazy lz_sqr(const FrLazy& a) {
+    FrLazy r;
+    if (ADX)
+        detail::mont_sqr_adx(a.l, r.l);
+    else
+        detail::mont_mul_lazy(a.l, a.l, r.l);
     return r;
 }
 inline FrLazy lz_add(const FrLazy& a, const FrLazy& b) {

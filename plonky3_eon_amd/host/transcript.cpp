@@ -53,8 +53,8 @@ void fq_from_mont(const uint64_t a[4], uint64_t out[4]) {
 
 template <bool ADX>
 FrLazy sbox(const FrLazy& x) {  // x^5
-    const FrLazy x2 = lz_mul<ADX>(x, x);
-    return lz_mul<ADX>(lz_mul<ADX>(x2, x2), x);
+    const FrLazy x2 = lz_sqr<ADX>(x);
+    return lz_mul<ADX>(lz_sqr<ADX>(x2), x);
 }
 
 void mds_light(FrLazy s[3]) {  // external.rs:128-133
@@ -115,8 +115,8 @@ void Poseidon2Bn254::permute_impl(Fr st[3]) const {
         FrLazy x = lz_add(s[0], partial_[0]);
         for (size_t r = 0; r < partial_.size(); r++) {
             const FrLazy p = lz_add(s[1], s[2]);
-            const FrLazy x2 = lz_mul<ADX>(x, x), xd = lz_add(x, x);
-            const FrLazy x4 = lz_mul<ADX>(x2, x2);
+            const FrLazy x2 = lz_sqr<ADX>(x), xd = lz_add(x, x);
+            const FrLazy x4 = lz_sqr<ADX>(x2);
             const FrLazy v2 = lz_mul<ADX>(x4, xd), v = lz_half(v2);
             const FrLazy t = lz_add(v, p);
             s[1] = lz_add(s[1], t);

@@ -60,6 +60,8 @@ int main(int argc, char** argv) {
         if (adx) {
             detail::mont_mul_adx(a, b, r);
             put("mul", a, b, r);
+            detail::mont_sqr_adx(a, r);
+            put("mul", a, a, r);
         }
         detail::add_lazy(a, b, r);
         put("add", a, b, r);

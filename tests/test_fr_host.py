@@ -59,7 +59,7 @@ def test_host_fr_default(exe):
     counts, err = _check(exe, {})
     assert counts["add"] == counts["half"] == 3064
     if "adx=1" in err:  # both products checked
-        assert counts["mul"] == 2 * 3064
+        assert counts["mul"] == 3 * 3064
 
 
 def test_host_fr_portable(exe):

@@ -1,12 +1,12 @@
 #!/bin/bash
 # Issue/LDS/VALU PMC passes (each alone, kernel-trace only, within the gfx950 slot limits) for one
 # kernel of one bench.py workload (serialized) -> gpurun_out/pmc_<name>.json via tools/pmc_table.py.
-# usage: tools/gpu_pmc_kernel.sh <workload> <kernel-regex> <name>
+# usage: [BENCH_EXTRA="--air generic"] tools/gpu_pmc_kernel.sh <workload> <kernel-regex> <name>
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 W=${1:?workload}; K=${2:?kernel regex}; N=${3:?name}
-B="python3 bench.py --workload $W --serial --steps 1 --warmup 0 --no-cpu-baseline"
+B="python3 bench.py --workload $W --serial --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_EXTRA}"
 pass() {  # pass-name counters...
   local n=$1; shift
   rm -rf gpurun_out/pmc_${N}_$n

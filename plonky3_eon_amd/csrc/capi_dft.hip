@@ -354,6 +354,7 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     ctx->fs_b.release();
     ctx->shard_send.release();
     ctx->shard_recv.release();
+    ctx->pool.release_all();
     ctx->scratch.release();
     ctx->stage_in.release();
     ctx->stage_out.release();

@@ -38,6 +38,57 @@ struct DevBuf {
     }
 };
 
+// Exact-size cache of large transient device buffers (the KZG opening bases' tables and their
+// scratch): a proof builds the same-sized buffers again, so they go back here instead of
+// hipFree (which synchronises the device and costs host time) and come back instead of hipMalloc.
+// Trimmed past CAP bytes; emptied with the context.
+struct DevPool {
+    static constexpr size_t CAP = size_t(8) << 30;
+    std::multimap<size_t, void*> free_;
+    size_t bytes = 0;
+    // `b` (empty or holding a smaller buffer, which returns to the pool) gets `need` bytes
+    hipError_t take(DevBuf& b, size_t need) {
+        if (b.p && b.bytes >= need) return hipSuccess;
+        give(b);
+        auto it = free_.find(need);
+        if (it != free_.end()) {
+            b.p = it->second;
+            b.bytes = need;
+            bytes -= need;
+            free_.erase(it);
+            return hipSuccess;
+        }
+        hipError_t e = hipMalloc(&b.p, need);
+        if (e == hipErrorOutOfMemory) {
+            (void)hipGetLastError();
+            release_all();
+            e = hipMalloc(&b.p, need);
+        }
+        if (e == hipSuccess)
+            b.bytes = need;
+        else
+            b.p = nullptr;
+        return e;
+    }
+    // work still queued on b must be finished (the caller synchronises first)
+    void give(DevBuf& b) {
+        if (!b.p) return;
+        if (bytes + b.bytes <= CAP) {
+            free_.emplace(b.bytes, b.p);
+            bytes += b.bytes;
+        } else {
+            (void)hipFree(b.p);
+        }
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    void release_all() {
+        for (auto& kv : free_) (void)hipFree(kv.second);
+        free_.clear();
+        bytes = 0;
+    }
+};
+
 struct Status {
     int code = EON_OK;
     std::string msg;
@@ -145,8 +196,13 @@ struct eon_ctx {
     // four-step DFT working blocks; the sharded MSM's partials (sharded.hip)
     eon::DevBuf fs_a, fs_b, shard_send, shard_recv;
 
-    // quotient: vanishing-polynomial table; KZG opening scan workspace
+    // quotient: vanishing-polynomial table (kept while its domains repeat); KZG opening scan workspace
     eon::DevBuf sel_tab, kzg_tmp;
+    bool van_valid = false;
+    uint32_t van_log_n = 0, van_log_q = 0;
+    eon::Fr van_shift{};
+    // opening bases' tables and scratch, reused across proofs (opening.hip, msm.hip)
+    eon::DevPool pool;
 
     // scratch: NTT intermediates, host-API staging
     eon::DevBuf scratch, stage_in, stage_out;

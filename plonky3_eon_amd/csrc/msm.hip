@@ -60,6 +60,8 @@ struct eon_msm_bases {
     // 3 * table (29-form affine, same layout), built on first use by the KZG opening bases'
     // radix-4 fixed-base multiplications (bases_table3_29)
     DevBuf table3;
+    // points / table come from (and return to) the context's DevPool (the opening bases)
+    bool pooled = false;
     const G1Affine* piece_source() const {
         return precomputed ? table.as<G1Affine>() : points29.as<G1Affine>();
     }
@@ -1253,8 +1255,9 @@ Status bases_alloc_table(eon_ctx* ctx, uint64_t n, uint32_t c, eon_msm_bases** o
     b->precomputed = true;
     b->c = c;
     b->windows = (255 + c - 1) / c;
-    if (b->points.ensure(n * sizeof(G1Affine)) != hipSuccess ||
-        b->table.ensure(n * b->windows * sizeof(G1Affine)) != hipSuccess) {
+    b->pooled = true;
+    if (ctx->pool.take(b->points, n * sizeof(G1Affine)) != hipSuccess ||
+        ctx->pool.take(b->table, n * b->windows * sizeof(G1Affine)) != hipSuccess) {
         bases_free(b);
         return Status::err(EON_E_OOM, "bases allocation failed");
     }
@@ -1275,6 +1278,10 @@ Status bases_seal_table(eon_msm_bases* b, hipStream_t st) {
 }
 
 void bases_free(eon_msm_bases* b) {
+    if (b->pooled) {  // the caller has synchronised the context's streams
+        b->ctx->pool.give(b->points);
+        b->ctx->pool.give(b->table);
+    }
     b->points.release();
     b->table.release();
     b->table3.release();

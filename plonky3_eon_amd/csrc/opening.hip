@@ -149,22 +149,30 @@ __device__ __forceinline__ void madd29_any(G1X29& acc, bool& inf, const F29& x, 
 // {-3, -1, 1, 3} (bit pairs of (d_w + 2^16 - 1) / 2, every bit read as +-1), so that every level
 // adds every window's entry +-T or +-3T (no lane divergence): 14 doublings + 128 mixed
 // additions, against 15 + 256 with +-1 digits (tab3 == null keeps that radix-2 form).
-// rows i = lo + t, t < cnt (a rank's slice; rows >= n - 1 are the identity)
+// rows i = lo + t, t < cnt (a rank's slice; rows >= n - 1 are the identity).  SPLIT (a short
+// slice, where a thread per row leaves SIMDs idle and the time is one row's chain): two adjacent
+// lanes per row, each adding 8 of the 16 windows at every level (both double), and the odd lane's
+// sum is passed to the even one by DPP and added there -- half the additions on the chain for 9 %
+// more work in total.
+template <bool SPLIT>
 __global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, const G1Affine* tab3, uint64_t n,
                                                      uint64_t lo, uint64_t cnt, Fr zinv, G1Xyzz* out_slice) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t t = SPLIT ? gt >> 1 : gt;
+    const uint32_t half = SPLIT ? (uint32_t)(gt & 1) : 0u;
+    const uint32_t w_lo = SPLIT ? half * (TW / 2) : 0u, w_hi = SPLIT ? w_lo + TW / 2 : TW;
     if (t >= cnt) return;
     const uint64_t i = lo + t;
     G1Xyzz* out = out_slice - lo;
     if (i + 1 >= n) {
-        st_xyzz(out + i, xyzz_inf());
+        if (half == 0) st_xyzz(out + i, xyzz_inf());
         return;
     }
     const G1Affine* row = tab + i * TW;
     {
         const G1Affine g = ld_affine(row);
         if (is_inf(g)) {  // the identity's table row is all identity
-            st_xyzz(out + i, xyzz_inf());
+            if (half == 0) st_xyzz(out + i, xyzz_inf());
             return;
         }
     }
@@ -223,7 +231,7 @@ __global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, const 
                 dbl29(acc);
                 dbl29(acc);
             }
-            for (uint32_t w = 0; w < TW; w++) {
+            for (uint32_t w = w_lo; w < w_hi; w++) {
                 // bit pair (hi, lo) of u_w: f = 2 e_hi + e_lo, e = +-1: 3 -> +3, 2 -> +1, 1 -> -1, 0 -> -3
                 const uint32_t two = (u[w] >> (2 * b)) & 3u;
                 const bool three = two == 3u || two == 0u;
@@ -234,17 +242,43 @@ __global__ void __launch_bounds__(64) k_open_scale29(const G1Affine* tab, const 
     } else {
         for (int b = (int)TC - 1; b >= 0; b--) {
             if (!inf) dbl29(acc);
-            for (uint32_t w = 0; w < TW; w++) {
+            for (uint32_t w = w_lo; w < w_hi; w++) {
                 ld_affine29(row + w, ((u[w] >> b) & 1) == 0, x, y);
                 madd29_any(acc, inf, x, y);
             }
         }
     }
-    if (even) {
+    if (even && half == 0) {
         ld_affine29(row, true, x, y);
         madd29_any(acc, inf, x, y);
     }
+    if (SPLIT) {
+        // the partner lane's (odd -> even) accumulator, word by word over DPP quad_perm(1, 0, 3, 2)
+        G1X29 o;
+        F29* dst[4] = {&o.X, &o.Y, &o.ZZ, &o.ZZZ};
+        const F29* src[4] = {&acc.X, &acc.Y, &acc.ZZ, &acc.ZZZ};
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int l = 0; l < 9; l++)
+                dst[c]->l[l] = (uint32_t)__builtin_amdgcn_mov_dpp((int)src[c]->l[l], 0xB1, 0xf, 0xf, false);
+        const bool o_inf = __builtin_amdgcn_mov_dpp((int)inf, 0xB1, 0xf, 0xf, false) != 0;
+        if (half) return;
+        acc29(acc, inf, o, o_inf);
+    }
     st_xyzz(out + i, x29_to_xyzz(acc, inf));
+}
+
+// short slices (a sharded rank's rows) split each row over two lanes
+inline bool scale_split(uint64_t rows) { return rows <= (1ull << 15); }
+void launch_open_scale29(uint64_t rows, const G1Affine* tab, const G1Affine* tab3, uint64_t n, uint64_t lo, Fr zinv,
+                         G1Xyzz* out, hipStream_t st) {
+    if (scale_split(rows))
+        hipLaunchKernelGGL(k_open_scale29<true>, dim3((unsigned)((2 * rows + 63) / 64)), dim3(64), 0, st, tab, tab3, n,
+                           lo, rows, zinv, out);
+    else
+        hipLaunchKernelGGL(k_open_scale29<false>, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, tab, tab3, n, lo,
+                           rows, zinv, out);
 }
 
 // GLV for BN254 G1: phi(x, y) = (beta x, y) = lambda (x, y) with lambda^2 + lambda + 1 = 0 mod r
@@ -395,18 +429,18 @@ __device__ __forceinline__ void recode_odd128(uint32_t (&kw)[4], uint32_t (&dg)[
 // rows j = lo + t, t < cnt; s and tmp are the slice's (rows >= n are the identity)
 constexpr uint32_t MTAB = 8;
 
-__global__ void __launch_bounds__(64) k_open_finish29(const G1Affine* s_slice, uint64_t n, uint64_t lo, uint64_t cnt,
+// S_j arrives as the scan left it (radix-2^32 XYZZ, no affine conversion pass)
+__global__ void __launch_bounds__(64) k_open_finish29(const G1Xyzz* s_slice, uint64_t n, uint64_t lo, uint64_t cnt,
                                                       Fr z, G1Raw29* mtab, G1Xyzz* tmp_slice) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     const uint64_t j = lo + t;
-    const G1Affine* s = s_slice - lo;
+    const G1Xyzz* s = s_slice - lo;
     G1Xyzz* tmp = tmp_slice - lo * TW;
     G1X29 acc;
     bool inf = true;
-    const G1Affine a = (j && j < n) ? ld_affine(s + j) : G1Affine{Fq::zero(), Fq::zero()};
+    const G1Xyzz a = (j && j < n) ? ld_xyzz(s + j) : xyzz_inf();
     if (!is_inf(a)) {
-        const F29 x = unpack29(to_fq261(a.x)), y = unpack29(to_fq261(a.y));
         uint32_t u1[4], u2[4];
         bool neg1, neg2;
         glv_split(to_canonical(pow_u64(z, j - 1)), u1, neg1, u2, neg2);
@@ -415,11 +449,13 @@ __global__ void __launch_bounds__(64) k_open_finish29(const G1Affine* s_slice, u
         u2[0] |= 1u;
         // the odd multiples (2m + 1) S, m < MTAB
         {
-            G1X29 two = dbl29_affine(x, y), m;
-            m.X = x;
-            m.Y = y;
-            m.ZZ = const29<FqP>(R29<FqP>::ONE);
-            m.ZZZ = m.ZZ;
+            G1X29 m;
+            m.X = unpack29(to_fq261(a.X));
+            m.Y = unpack29(to_fq261(a.Y));
+            m.ZZ = unpack29(to_fq261(a.ZZ));
+            m.ZZZ = unpack29(to_fq261(a.ZZZ));
+            G1X29 two = m;
+            dbl29(two);
             bool m_inf = false;
             st_raw29(mtab + t, m);
             for (uint32_t q = 1; q < MTAB; q++) {
@@ -505,36 +541,38 @@ void scan_exclusive(G1Xyzz* a, uint64_t len, G1Xyzz* tmp, hipStream_t st, uint32
     hipLaunchKernelGGL(k_scan_apply, dim3(grid_for(nt, 64)), dim3(64), 0, st, a, len, chunk, tmp);
 }
 
-// one point's scratch, alive until its stream is synchronised
+// one point's scratch, alive until its stream is synchronised; taken from and given back to the
+// context's DevPool (the next proof builds the same sizes)
 struct Scratch {
     DevBuf h_aff, pts, tmp, aff, table_tmp, mtab;
+    DevPool* pool = nullptr;
+    hipError_t take(DevBuf& b, size_t need) { return pool ? pool->take(b, need) : b.ensure(need); }
     void release() {
-        for (DevBuf* b : {&h_aff, &pts, &tmp, &aff, &table_tmp, &mtab}) b->release();
+        for (DevBuf* b : {&h_aff, &pts, &tmp, &aff, &table_tmp, &mtab}) {
+            if (pool) pool->give(*b);
+            b->release();
+        }
     }
 };
 
 // radix-2^29 fast path: P_i from the SRS table, one kernel for H_j and its window table
 Status opening_bases_async29(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, const Fr& z, hipStream_t st,
                              Scratch& sc, eon_msm_bases** out) {
-    EON_HIP(sc.pts.ensure(n * sizeof(G1Xyzz)));
-    EON_HIP(sc.tmp.ensure(scan_tmp_points(n) * sizeof(G1Xyzz)));
-    EON_HIP(sc.aff.ensure(n * sizeof(G1Affine)));
-    EON_HIP(sc.table_tmp.ensure(n * TW * sizeof(G1Xyzz)));
+    EON_HIP(sc.take(sc.pts, n * sizeof(G1Xyzz)));
+    EON_HIP(sc.take(sc.tmp, scan_tmp_points(n) * sizeof(G1Xyzz)));
+    EON_HIP(sc.take(sc.table_tmp, n * TW * sizeof(G1Xyzz)));
     eon_msm_bases* b = nullptr;
     EON_TRY(bases_alloc_table(ctx, n, TC, &b));
-    // ~15 dbl (6M+3S) + 257 madd (8M+2S) and ~254 dbl + ~127 madd + 240 dbl per point
-    EON_HIP(sc.mtab.ensure(n * MTAB * sizeof(G1Raw29)));
+    EON_HIP(sc.take(sc.mtab, n * MTAB * sizeof(G1Raw29)));
     const G1Affine* tab3 = bases_table3_29(srs, st);  // null (radix 2) if it cannot be built
     // radix 4: 14 dbl (6M+3S) + 129 madd (8M+2S); radix 2: 15 dbl + 257 madd
     ctx->prof.begin("k_open_scale29", n * (TW * 64ull + 128ull), st, n * (tab3 ? 1416ull : 2705ull));
-    hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(n, 64)), dim3(64), 0, st, bases_table29(srs), tab3, n, 0ull,
-                       n, inverse(z), sc.pts.as<G1Xyzz>());
+    launch_open_scale29(n, bases_table29(srs), tab3, n, 0ull, inverse(z), sc.pts.as<G1Xyzz>(), st);
     ctx->prof.end(st);
     scan_exclusive(sc.pts.as<G1Xyzz>(), n, sc.tmp.as<G1Xyzz>(), st);
-    EON_HIP(launch_batch_to_affine(sc.pts.as<G1Xyzz>(), n, sc.aff.as<G1Affine>(), st));
     // GLV: 124 dbl + 64 add (12M+2S) + 8 multiples, then 240 dbl for the window table
-    ctx->prof.begin("k_open_finish29", n * (64ull + TW * 128ull), st, n * 4170ull);
-    hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(n, 64)), dim3(64), 0, st, sc.aff.as<G1Affine>(), n, 0ull, n, z,
+    ctx->prof.begin("k_open_finish29", n * (128ull + TW * 128ull), st, n * 4170ull);
+    hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(n, 64)), dim3(64), 0, st, sc.pts.as<G1Xyzz>(), n, 0ull, n, z,
                        sc.mtab.as<G1Raw29>(), sc.table_tmp.as<G1Xyzz>());
     ctx->prof.end(st);
     hipError_t e = launch_batch_to_affine(sc.table_tmp.as<G1Xyzz>(), n * TW, bases_table_mut(b), st);
@@ -555,14 +593,14 @@ Status opening_bases_async(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, c
         n >= 2)
         return opening_bases_async29(ctx, srs, n, z, st, sc, out);
     const G1Affine* g = bases_points(srs);
-    EON_HIP(sc.h_aff.ensure(n * sizeof(G1Affine)));
+    EON_HIP(sc.take(sc.h_aff, n * sizeof(G1Affine)));
     if (z.is_zero()) {
         hipLaunchKernelGGL(k_open_shift, dim3(grid_for(n, 256)), dim3(256), 0, st, g, n, sc.h_aff.as<G1Affine>());
         EON_HIP(hipGetLastError());
     } else {
-        EON_HIP(sc.pts.ensure(n * sizeof(G1Xyzz)));
-        EON_HIP(sc.tmp.ensure(scan_tmp_points(n) * sizeof(G1Xyzz)));
-        EON_HIP(sc.aff.ensure(n * sizeof(G1Affine)));
+        EON_HIP(sc.take(sc.pts, n * sizeof(G1Xyzz)));
+        EON_HIP(sc.take(sc.tmp, scan_tmp_points(n) * sizeof(G1Xyzz)));
+        EON_HIP(sc.take(sc.aff, n * sizeof(G1Affine)));
         // algorithmic cost: 2 scalar multiplications per point, ~254 dbl (6M+3S) + ~127 madd (8M+2S)
         ctx->prof.begin("k_open_scale", n * (64ull + 128ull), st, n * 3556ull);
         hipLaunchKernelGGL(k_open_scale, dim3(grid_for(n, 64)), dim3(64), 0, st, g, n, inverse(z),
@@ -595,36 +633,38 @@ Status opening_bases_sharded(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
     hipStream_t streams[3] = {ctx->stream, ctx->side(ctx->msm_side), ctx->side(ctx->msm_side2)};
     // per point: slice points (+1 for the total), scan scratch, affine slice, table slice
     std::vector<Scratch> sc(np);
+    for (auto& x : sc) x.pool = &ctx->pool;
     DevBuf totals_x, totals_a, all_totals, send, recv;
-    struct Release {
+    struct Release {  // every exit: drain the streams, then the buffers go back to the pool
         std::vector<Scratch>& sc;
         DevBuf* b[5];
+        DevPool& pool;
+        hipStream_t* streams;
         ~Release() {
+            for (int i = 0; i < 3; i++) (void)hipStreamSynchronize(streams[i]);
             for (auto& x : sc) x.release();
-            for (DevBuf* x : b) x->release();
+            for (DevBuf* x : b) pool.give(*x);
         }
-    } release{sc, {&totals_x, &totals_a, &all_totals, &send, &recv}};
-    EON_HIP(totals_x.ensure(np * sizeof(G1Xyzz)));
-    EON_HIP(totals_a.ensure(np * sizeof(G1Affine)));
-    EON_HIP(all_totals.ensure((uint64_t)world * np * sizeof(G1Affine)));
+    } release{sc, {&totals_x, &totals_a, &all_totals, &send, &recv}, ctx->pool, streams};
+    EON_HIP(ctx->pool.take(totals_x, np * sizeof(G1Xyzz)));
+    EON_HIP(ctx->pool.take(totals_a, np * sizeof(G1Affine)));
+    EON_HIP(ctx->pool.take(all_totals, (uint64_t)world * np * sizeof(G1Affine)));
     const uint64_t slice_entries = m * TW;  // per point
-    EON_HIP(send.ensure(np * slice_entries * sizeof(G1Affine)));
-    EON_HIP(recv.ensure((uint64_t)world * np * slice_entries * sizeof(G1Affine)));
+    EON_HIP(ctx->pool.take(send, np * slice_entries * sizeof(G1Affine)));
+    EON_HIP(ctx->pool.take(recv, (uint64_t)world * np * slice_entries * sizeof(G1Affine)));
     EON_HIP(hipEventRecord(ctx->msm_ev[0], ctx->stream));
     EON_HIP(hipStreamWaitEvent(ctx->msm_side, ctx->msm_ev[0], 0));
     EON_HIP(hipStreamWaitEvent(ctx->msm_side2, ctx->msm_ev[0], 0));
     // phase 1: P_i of the slice and its exclusive prefix sums; the total lands at index m
     for (uint32_t t = 0; t < np; t++) {
         hipStream_t st = streams[t % 3];
-        EON_HIP(sc[t].pts.ensure((m + 1) * sizeof(G1Xyzz)));
-        EON_HIP(sc[t].tmp.ensure(scan_tmp_points(m + 1) * sizeof(G1Xyzz)));
-        EON_HIP(sc[t].aff.ensure(m * sizeof(G1Affine)));
-        EON_HIP(sc[t].table_tmp.ensure(slice_entries * sizeof(G1Xyzz)));
-        EON_HIP(sc[t].mtab.ensure(m * MTAB * sizeof(G1Raw29)));
+        EON_HIP(sc[t].take(sc[t].pts, (m + 1) * sizeof(G1Xyzz)));
+        EON_HIP(sc[t].take(sc[t].tmp, scan_tmp_points(m + 1) * sizeof(G1Xyzz)));
+        EON_HIP(sc[t].take(sc[t].table_tmp, slice_entries * sizeof(G1Xyzz)));
+        EON_HIP(sc[t].take(sc[t].mtab, m * MTAB * sizeof(G1Raw29)));
         const G1Affine* tab3 = bases_table3_29(srs, st);  // null (radix 2) if it cannot be built
         ctx->prof.begin("k_open_scale29", m * (TW * 64ull + 128ull), st, m * (tab3 ? 1416ull : 2705ull));
-        hipLaunchKernelGGL(k_open_scale29, dim3(grid_for(m, 64)), dim3(64), 0, st, bases_table29(srs), tab3, n, lo, m,
-                           inverse(zs[t]), sc[t].pts.as<G1Xyzz>());
+        launch_open_scale29(m, bases_table29(srs), tab3, n, lo, inverse(zs[t]), sc[t].pts.as<G1Xyzz>(), st);
         ctx->prof.end(st);
         // one identity past the slice: the exclusive scan leaves the slice total there
         hipLaunchKernelGGL(k_set_inf, dim3(1), dim3(1), 0, st, sc[t].pts.as<G1Xyzz>() + m);
@@ -646,9 +686,8 @@ Status opening_bases_sharded(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n,
         if (rank)
             hipLaunchKernelGGL(k_add_rank_offset, dim3(grid_for(m, 64)), dim3(64), 0, st, sc[t].pts.as<G1Xyzz>(), m,
                                all_totals.as<G1Affine>(), np, t, rank);
-        EON_HIP(launch_batch_to_affine(sc[t].pts.as<G1Xyzz>(), m, sc[t].aff.as<G1Affine>(), st));
-        ctx->prof.begin("k_open_finish29", m * (64ull + TW * 128ull), st, m * 4170ull);
-        hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(m, 64)), dim3(64), 0, st, sc[t].aff.as<G1Affine>(), n, lo,
+        ctx->prof.begin("k_open_finish29", m * (128ull + TW * 128ull), st, m * 4170ull);
+        hipLaunchKernelGGL(k_open_finish29, dim3(grid_for(m, 64)), dim3(64), 0, st, sc[t].pts.as<G1Xyzz>(), n, lo,
                            m, zs[t], sc[t].mtab.as<G1Raw29>(), sc[t].table_tmp.as<G1Xyzz>());
         ctx->prof.end(st);
         EON_HIP(launch_batch_to_affine(sc[t].table_tmp.as<G1Xyzz>(), slice_entries,
@@ -708,6 +747,7 @@ Status opening_bases_many(eon_ctx* ctx, const eon_msm_bases* srs, uint64_t n, co
     EON_HIP(hipStreamWaitEvent(ctx->msm_side, ctx->msm_ev[0], 0));
     EON_HIP(hipStreamWaitEvent(ctx->msm_side2, ctx->msm_ev[0], 0));
     std::vector<Scratch> sc(npoints);
+    for (auto& x : sc) x.pool = &ctx->pool;
     Status s = Status::ok();
     for (uint32_t t = 0; t < npoints && !s.bad(); t++)
         s = opening_bases_async(ctx, srs, n, zs[t], streams[t % 3], sc[t], outs + t);

@@ -11,6 +11,8 @@
 // acc = acc * alpha + C_k in constraint order, so no alpha-power table is read.  One thread owns
 // one (row, vector lane) pair; the VECTOR_LEN lanes of a row are adjacent threads and are
 // combined as sum_v P_v * alpha^(160 * (VL - 1 - v)) through LDS.
+#include <cstring>
+
 #include "quotient.h"
 #include <vector>
 
@@ -231,13 +233,23 @@ Status vanishing_table(eon_ctx* ctx, uint32_t log_n, uint32_t log_q, const Fr& s
     const uint32_t rate = log_q - log_n;
     const uint32_t nr = 1u << rate;
     EON_HIP(ctx->sel_tab.ensure(2ull * nr * sizeof(Fr)));
-    Fr s_pow_n = shift;
-    for (uint32_t i = 0; i < log_n; i++) s_pow_n = sqr(s_pow_n);
     *zh = ctx->sel_tab.as<Fr>();
     *zh_inv = *zh + nr;
+    // the same domains every proof: the table is kept (a single-thread inversion per entry is a
+    // ~0.5 ms latency-bound launch otherwise)
+    if (ctx->van_valid && ctx->van_log_n == log_n && ctx->van_log_q == log_q &&
+        std::memcmp(&ctx->van_shift, &shift, sizeof(Fr)) == 0)
+        return Status::ok();
+    ctx->van_valid = false;
+    Fr s_pow_n = shift;
+    for (uint32_t i = 0; i < log_n; i++) s_pow_n = sqr(s_pow_n);
     hipLaunchKernelGGL(k_vanishing_table, dim3((nr + 63) / 64), dim3(64), 0, ctx->stream, s_pow_n,
                        fr_two_adic_generator(rate), nr, *zh, *zh_inv);
     EON_HIP(hipGetLastError());
+    ctx->van_valid = true;
+    ctx->van_log_n = log_n;
+    ctx->van_log_q = log_q;
+    ctx->van_shift = shift;
     return Status::ok();
 }
 

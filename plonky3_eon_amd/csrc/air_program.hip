@@ -33,7 +33,7 @@ using namespace eon;
 
 namespace {
 
-enum : uint32_t { OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_NEG = 3, OP_ASSERT = 4 };
+enum : uint32_t { OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_NEG = 3, OP_ASSERT = 4, OP_NOP = 5 };
 // operand = mode << 29 | index
 enum : uint32_t { M_REG = 0, M_LOCAL = 1, M_NEXT = 2, M_CONST = 3, M_FIRST = 4, M_LAST = 5, M_TRANS = 6, M_PREV = 7 };
 constexpr uint32_t IDX_MASK = (1u << 29) - 1;
@@ -85,41 +85,63 @@ __device__ __forceinline__ Fr fetch(uint32_t opnd, const RF& rf, const Fr& prev,
     }
 }
 
+// The program is fetched in blocks of CODE_BLOCK instructions (one 64-byte scalar load each; the
+// device copy is padded with OP_NOP to a whole block), the next block's load issued before the
+// current block runs: the program (~130 KB for the Poseidon2-AIR) does not fit the scalar cache, so
+// every fetch is an L2 round trip that an instruction-at-a-time loop waits on.
+constexpr uint32_t CODE_BLOCK = 4;
+struct CodeBlock {
+    Instr i[CODE_BLOCK];
+};
+
 template <class RF>
-__device__ __forceinline__ void run_program(const Instr* __restrict__ code, uint32_t n_code, RF& rf, const Window& w,
-                                            const Fr& alpha, Fr& acc) {
+__device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, const Fr& alpha, Fr& acc, Fr& prev) {
+    if (in.op == OP_NOP) return;
+    const Fr x = fetch(in.a, rf, prev, w);
+    if (in.op == OP_ASSERT) {
+        acc = add(mul(acc, alpha), x);  // folder.rs:81-85, alpha powers reversed
+        return;
+    }
+    Fr r;
+    if (in.op == OP_NEG) {
+        r = neg(x);
+    } else {
+        const Fr y = fetch(in.b, rf, prev, w);
+        if (in.op == OP_MUL)
+            r = mul(x, y);
+        else if (in.op == OP_ADD)
+            r = add(x, y);
+        else
+            r = sub(x, y);
+    }
+    prev = r;
+    if (in.dst != NO_DST) rf.set(in.dst, r);
+}
+
+template <class RF>
+__device__ __forceinline__ void run_program(const CodeBlock* __restrict__ code, uint32_t n_blocks, RF& rf,
+                                            const Window& w, const Fr& alpha, Fr& acc) {
+    if (n_blocks == 0) return;
     Fr prev = Fr::zero();
-    Instr nx = n_code ? code[0] : Instr{OP_ASSERT, NO_DST, M_PREV << 29, 0};
-    for (uint32_t pc = 0; pc < n_code; pc++) {
-        // uniform: every lane runs the same instruction, so the operand switch is scalar
-        const Instr in{(uint32_t)__builtin_amdgcn_readfirstlane(nx.op), (uint32_t)__builtin_amdgcn_readfirstlane(nx.dst),
-                       (uint32_t)__builtin_amdgcn_readfirstlane(nx.a), (uint32_t)__builtin_amdgcn_readfirstlane(nx.b)};
-        if (pc + 1 < n_code) nx = code[pc + 1];  // in flight while this instruction computes
-        const Fr x = fetch(in.a, rf, prev, w);
-        if (in.op == OP_ASSERT) {
-            acc = add(mul(acc, alpha), x);  // folder.rs:81-85, alpha powers reversed
-            continue;
+    CodeBlock nx = code[0];
+    for (uint32_t bk = 0; bk < n_blocks; bk++) {
+        const CodeBlock cur = nx;
+        if (bk + 1 < n_blocks) nx = code[bk + 1];  // in flight while this block runs
+#pragma unroll
+        for (uint32_t u = 0; u < CODE_BLOCK; u++) {
+            // uniform: every lane runs the same instruction, so the operand switch is scalar
+            const Instr in{(uint32_t)__builtin_amdgcn_readfirstlane(cur.i[u].op),
+                           (uint32_t)__builtin_amdgcn_readfirstlane(cur.i[u].dst),
+                           (uint32_t)__builtin_amdgcn_readfirstlane(cur.i[u].a),
+                           (uint32_t)__builtin_amdgcn_readfirstlane(cur.i[u].b)};
+            exec1(in, rf, w, alpha, acc, prev);
         }
-        Fr r;
-        if (in.op == OP_NEG) {
-            r = neg(x);
-        } else {
-            const Fr y = fetch(in.b, rf, prev, w);
-            if (in.op == OP_MUL)
-                r = mul(x, y);
-            else if (in.op == OP_ADD)
-                r = add(x, y);
-            else
-                r = sub(x, y);
-        }
-        prev = r;
-        if (in.dst != NO_DST) rf.set(in.dst, r);
     }
 }
 
 // MODE 0: registers in LDS; 1: in the global buffer `gregs`
 template <int MODE>
-__global__ void __launch_bounds__(256) k_air_quotient(const Instr* __restrict__ code, uint32_t n_code,
+__global__ void __launch_bounds__(256) k_air_quotient(const CodeBlock* __restrict__ code, uint32_t n_blocks,
                                                       const Fr* __restrict__ lde, uint32_t width, uint64_t q,
                                                       uint64_t next_step, const Fr* __restrict__ table,
                                                       const Fr* __restrict__ sels, const Fr* __restrict__ inv_van,
@@ -138,7 +160,7 @@ __global__ void __launch_bounds__(256) k_air_quotient(const Instr* __restrict__ 
         rf.base = gregs + row;
         rf.stride = q;
     }
-    run_program(code, n_code, rf, w, alpha, acc);
+    run_program(code, n_blocks, rf, w, alpha, acc);
     st_vec(out + row, mul(acc, ld(inv_van + (row & nr_mask))));  // prover.rs:699
 }
 
@@ -421,9 +443,12 @@ int eon_air_program_create(eon_ctx* ctx, const eon_sym_node* nodes, uint32_t n_n
             delete p;
             return c;
         }
-        hipError_t e = p->d_code.ensure(std::max<size_t>(1, p->code.size()) * sizeof(Instr));
-        if (e == hipSuccess && !p->code.empty())
-            e = hipMemcpy(p->d_code.p, p->code.data(), p->code.size() * sizeof(Instr), hipMemcpyHostToDevice);
+        // device copy padded with OP_NOP to whole CODE_BLOCKs
+        std::vector<Instr> padded(p->code);
+        while (padded.size() % CODE_BLOCK) padded.push_back({OP_NOP, NO_DST, M_PREV << 29, 0});
+        hipError_t e = p->d_code.ensure(std::max<size_t>(1, padded.size()) * sizeof(Instr));
+        if (e == hipSuccess && !padded.empty())
+            e = hipMemcpy(p->d_code.p, padded.data(), padded.size() * sizeof(Instr), hipMemcpyHostToDevice);
         if (e == hipSuccess) e = p->d_table.ensure(std::max<size_t>(1, p->n_consts + n_public) * sizeof(Fr));
         if (e != hipSuccess) {
             p->d_code.release();
@@ -530,8 +555,8 @@ int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const e
         uint64_t products = 1;
         for (const Instr& in : prog->code) products += (in.op == OP_MUL || in.op == OP_ASSERT) ? 1 : 0;
         ctx->prof.begin("k_air_quotient", q * (uint64_t)prog->width * 32 + q * 32, ctx->stream, q * products);
-        const Instr* code = prog->d_code.as<Instr>();
-        const uint32_t n_code = (uint32_t)prog->code.size();
+        const CodeBlock* code = prog->d_code.as<CodeBlock>();
+        const uint32_t n_blocks = (uint32_t)((prog->code.size() + CODE_BLOCK - 1) / CODE_BLOCK);
         const Fr* lde_f = reinterpret_cast<const Fr*>(lde);
         const Fr* sel = prog->uses_sels ? prog->d_sels.as<Fr>() : nullptr;
         Fr* out_f = reinterpret_cast<Fr*>(out);
@@ -540,11 +565,11 @@ int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const e
             // the one another context set it on
             EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_air_quotient<0>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            hipLaunchKernelGGL(k_air_quotient<0>, dim3(grid), dim3(block), shmem, ctx->stream, code, n_code, lde_f,
+            hipLaunchKernelGGL(k_air_quotient<0>, dim3(grid), dim3(block), shmem, ctx->stream, code, n_blocks, lde_f,
                                prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(), sel, inv_van, nr_mask, al, out_f,
                                nullptr);
         } else {
-            hipLaunchKernelGGL(k_air_quotient<1>, dim3(grid), dim3(block), 0, ctx->stream, code, n_code, lde_f,
+            hipLaunchKernelGGL(k_air_quotient<1>, dim3(grid), dim3(block), 0, ctx->stream, code, n_blocks, lde_f,
                                prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(), sel, inv_van, nr_mask, al, out_f,
                                prog->d_regs.as<uint4>());
         }

@@ -268,6 +268,26 @@ EON_NI G2Jac g2j_add_affine(const G2Jac& p, const G2Affine& a) {
     return r;
 }
 
+// P + Q (both Jacobian), add-2007-bl with the doubling / inverse / identity cases
+EON_NI G2Jac g2j_add(const G2Jac& p, const G2Jac& q) {
+    if (f2_is_zero(p.Z)) return q;
+    if (f2_is_zero(q.Z)) return p;
+    const Fq2 Z1Z1 = f2_sqr(p.Z), Z2Z2 = f2_sqr(q.Z);
+    const Fq2 U1 = f2_mul(p.X, Z2Z2), U2 = f2_mul(q.X, Z1Z1);
+    const Fq2 S1 = f2_mul(f2_mul(p.Y, q.Z), Z2Z2), S2 = f2_mul(f2_mul(q.Y, p.Z), Z1Z1);
+    const Fq2 H = f2_sub(U2, U1), rr = f2_dbl(f2_sub(S2, S1));
+    if (f2_is_zero(H)) {
+        if (f2_is_zero(rr)) return g2j_dbl(p);
+        return {f2_one(), f2_one(), f2_zero()};
+    }
+    const Fq2 I = f2_sqr(f2_dbl(H)), J = f2_mul(H, I), V = f2_mul(U1, I);
+    G2Jac r;
+    r.X = f2_sub(f2_sub(f2_sqr(rr), J), f2_dbl(V));
+    r.Y = f2_sub(f2_mul(rr, f2_sub(V, r.X)), f2_dbl(f2_mul(S1, J)));
+    r.Z = f2_mul(f2_sub(f2_sub(f2_sqr(f2_add(p.Z, q.Z)), Z1Z1), Z2Z2), H);
+    return r;
+}
+
 EON_NI G2Affine g2j_to_affine(const G2Jac& p) {
     if (f2_is_zero(p.Z)) return {f2_zero(), f2_zero()};
     const Fq2 zi = f2_inv(p.Z), zi2 = f2_sqr(zi);

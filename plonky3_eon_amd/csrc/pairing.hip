@@ -13,7 +13,8 @@
 //   k_vb_sums     one block per distinct point: -sum W_i over its openings; one more block for
 //                 sum C_i and sum v_i (XYZZ partial sums per thread, LDS tree)
 //   k_vb_pairs    the merged pairs: P_0 = sum C - (sum v) G1 with Q_0 = G2, P_z = -sum W with
-//                 Q_z = [alpha]G2 - z G2 (Jacobian double-and-add over Fq2, then affine)
+//                 Q_z = [alpha]G2 - z G2 (fixed-generator multiples as sums of 2^i tables, 64
+//                 lanes and an LDS tree per pair, then affine)
 //   k_miller      one thread per pair: f_{6x+2,Q}(P) and the two Frobenius-twisted lines, T in
 //                 projective coordinates (no inversions; lines scaled by Fq2 factors)
 //   k_final_exp   product of the Miller values, easy part f^((q^6-1)(q^2+1)), hard part
@@ -210,45 +211,55 @@ __global__ void __launch_bounds__(VB_THREADS) k_vb_sums(const G1Affine* __restri
 }
 
 
-// k G2 for the fixed generator: the sum of the table entries 2^i G2 of k's set bits (additions
-// only -- a double-and-add pays 256 doublings on top)
-__device__ __noinline__ G2Jac g2_gen_mul_words(const uint32_t (&k)[8]) {
-    G2Jac acc = {f2_one(), f2_one(), f2_zero()};
-    for (int i = 0; i < 256; i++)
-        if ((k[i >> 5] >> (i & 31)) & 1) acc = g2j_add_affine(acc, {f2_c(pc::G2_POW2[i][0]), f2_c(pc::G2_POW2[i][1])});
-    return acc;
-}
+// One block of VBP_THREADS per merged pair.  [k] of a fixed generator is the sum of the table
+// entries 2^i G of k's set bits: thread i sums the entries of bits [4i, 4i + 4), then an LDS tree
+// adds the 64 partial sums -- 4 + 6 dependent additions instead of one thread's ~128.
+constexpr uint32_t VBP_THREADS = 64;
 
-// k G1 for the generator (1, 2), likewise from the table 2^i G1
-__device__ __noinline__ G1Xyzz g1_gen_mul_words(const uint32_t (&k)[8]) {
-    G1Xyzz acc = xyzz_inf();
-    for (int i = 0; i < 256; i++)
-        if ((k[i >> 5] >> (i & 31)) & 1) acc = xyzz_add_affine(acc, {fq_c(pc::G1_POW2[i][0]), fq_c(pc::G1_POW2[i][1])});
-    return acc;
-}
-
-__global__ void __launch_bounds__(64) k_vb_pairs(const G1Xyzz* __restrict__ sums, const Fr* __restrict__ vsum,
-                                                 const Fr* __restrict__ zs, uint32_t G, G2Affine g2_alpha,
-                                                 G1Affine* __restrict__ P, G2Affine* __restrict__ Q) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(VBP_THREADS) k_vb_pairs(const G1Xyzz* __restrict__ sums, const Fr* __restrict__ vsum,
+                                                          const Fr* __restrict__ zs, uint32_t G, G2Affine g2_alpha,
+                                                          G1Affine* __restrict__ P, G2Affine* __restrict__ Q) {
+    __shared__ G1Xyzz p1[VBP_THREADS];
+    __shared__ G2Jac p2[VBP_THREADS];
+    const uint32_t t = blockIdx.x, i = threadIdx.x;
     if (t > G) return;
+    const Fr k = to_canonical(t == 0 ? *vsum : zs[t - 1]);
+    const uint32_t word = k.v[i >> 3], b0 = 4 * i, sh = b0 & 31;
     if (t == 0) {
         // P_0 = sum C - (sum v) G1, Q_0 = G2
-        const Fr v = to_canonical(*vsum);
-        uint32_t k[8];
-        for (int i = 0; i < 8; i++) k[i] = v.v[i];
-        G1Affine vg = xyzz_to_affine(g1_gen_mul_words(k));
-        P[0] = xyzz_to_affine(xyzz_add_affine(sums[G], affine_neg(vg)));
-        Q[0] = g2_generator();
+        G1Xyzz acc = xyzz_inf();
+        for (uint32_t b = 0; b < 4; b++)
+            if ((word >> (sh + b)) & 1)
+                acc = xyzz_add_affine(acc, {fq_c(pc::G1_POW2[b0 + b][0]), fq_c(pc::G1_POW2[b0 + b][1])});
+        p1[i] = acc;
+        __syncthreads();
+        for (uint32_t s = VBP_THREADS / 2; s > 0; s >>= 1) {
+            if (i < s) p1[i] = xyzz_add(p1[i], p1[i + s]);
+            __syncthreads();
+        }
+        if (i == 0) {
+            const G1Affine vg = xyzz_to_affine(p1[0]);
+            P[0] = xyzz_to_affine(xyzz_add_affine(sums[G], affine_neg(vg)));
+            Q[0] = g2_generator();
+        }
     } else {
         // P_z = -sum W, Q_z = [alpha]G2 - z G2
-        const Fr z = to_canonical(zs[t - 1]);
-        uint32_t k[8];
-        for (int i = 0; i < 8; i++) k[i] = z.v[i];
-        G2Jac zg = g2_gen_mul_words(k);
-        if (!f2_is_zero(zg.Z)) zg.Y = f2_neg(zg.Y);
-        P[t] = xyzz_to_affine(sums[t - 1]);
-        Q[t] = g2j_to_affine(g2j_add_affine(zg, g2_alpha));
+        G2Jac acc = {f2_one(), f2_one(), f2_zero()};
+        for (uint32_t b = 0; b < 4; b++)
+            if ((word >> (sh + b)) & 1)
+                acc = g2j_add_affine(acc, {f2_c(pc::G2_POW2[b0 + b][0]), f2_c(pc::G2_POW2[b0 + b][1])});
+        p2[i] = acc;
+        __syncthreads();
+        for (uint32_t s = VBP_THREADS / 2; s > 0; s >>= 1) {
+            if (i < s) p2[i] = g2j_add(p2[i], p2[i + s]);
+            __syncthreads();
+        }
+        if (i == 0) {
+            G2Jac zg = p2[0];
+            if (!f2_is_zero(zg.Z)) zg.Y = f2_neg(zg.Y);
+            P[t] = xyzz_to_affine(sums[t - 1]);
+            Q[t] = g2j_to_affine(g2j_add_affine(zg, g2_alpha));
+        }
     }
 }
 
@@ -476,7 +487,7 @@ int eon_kzg_verify_batch(eon_ctx* ctx, const eon_g1_affine* commitments, const e
                            dvsum.as<Fr>());
         ctx->prof.end(st);
         ctx->prof.begin("k_vb_pairs", (uint64_t)(G + 1) * (96 + 192), st);
-        hipLaunchKernelGGL(k_vb_pairs, dim3((G + 1 + 63) / 64), dim3(64), 0, st, dsums.as<G1Xyzz>(), dvsum.as<Fr>(),
+        hipLaunchKernelGGL(k_vb_pairs, dim3(G + 1), dim3(VBP_THREADS), 0, st, dsums.as<G1Xyzz>(), dvsum.as<Fr>(),
                            dz.as<Fr>(), G, ga, dP.as<G1Affine>(), dQ.as<G2Affine>());
         ctx->prof.end(st);
         EON_HIP(hipGetLastError());

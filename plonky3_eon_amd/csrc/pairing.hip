@@ -15,17 +15,19 @@
 //   k_vb_pairs    the merged pairs: P_0 = sum C - (sum v) G1 with Q_0 = G2, P_z = -sum W with
 //                 Q_z = [alpha]G2 - z G2 (fixed-generator multiples as sums of 2^i tables, 64
 //                 lanes and an LDS tree per pair, then affine)
-//   k_miller      one thread per pair: f_{6x+2,Q}(P) and the two Frobenius-twisted lines, T in
-//                 projective coordinates (no inversions; lines scaled by Fq2 factors)
-//   k_final_exp   product of the Miller values, easy part f^((q^6-1)(q^2+1)), hard part
-//                 f^((q^4-q^2+1)/r) from f^x, f^(x^2), f^(x^3) and Frobenius maps, and the test
-//                 against 1
+//   k_miller_team one 6-lane team per pair (pairing_team.h: lane k holds the coefficient of w^k):
+//                 f_{6x+2,Q}(P) by the signed digits of 6x + 2 and the two Frobenius-twisted lines,
+//                 T in projective coordinates (no inversions; lines scaled by Fq2 factors), the
+//                 line and point formulas spread over the lanes
+//   k_final_exp_team  one team: product of the Miller values, easy part f^((q^6-1)(q^2+1)), hard
+//                 part f^((q^4-q^2+1)/r) from f^x, f^(x^2), f^(x^3) and Frobenius maps, and the
+//                 test against 1
 #include <algorithm>
 #include <map>
 #include <vector>
 
 #include "context.h"
-#include "pairing.h"
+#include "pairing_team.h"
 
 using namespace eon;
 
@@ -92,81 +94,277 @@ __device__ __noinline__ Fq12 add_line(G2Proj& T, const G2Affine& A, const Fq& xp
     return l;
 }
 
-// f times a line of dbl_line / add_line: sparse (l0 + l1 w + l3 w^3) except the vertical line
-__device__ __forceinline__ Fq12 mul_line(const Fq12& f, const Fq12& l) {
-    if (f2_is_zero(l.c1.c0) && f2_is_zero(l.c1.c1)) return f12_mul(f, l);  // vertical: l0 + l2 w^2
-    return f12_mul_line(f, l.c0.c0, l.c1.c0, l.c1.c1);
+// ---- team-parallel Miller loop and final exponentiation (pairing_team.h) -----------------------
+//
+// Lane k of a team holds the coefficient of w^k of the running Fq12; lanes 6 and 7 of the 8-lane
+// team compute as copies of lane 5 and publish nothing.  Every barrier sits in control flow that is
+// uniform over the block (the loop bits are constants; per-team data decides only selects), and
+// the blocks are one wave, so a barrier costs a few cycles next to an Fq2 product's hundreds.
+
+constexpr uint32_t TEAM = 8;
+
+struct TeamLane {
+    int k;     // coefficient index this lane computes (0..5)
+    bool pub;  // lanes 0..5 publish
+};
+
+__device__ __forceinline__ TeamLane team_lane() {
+    const uint32_t l = threadIdx.x & (TEAM - 1);
+    return {l < 6 ? (int)l : 5, l < 6};
 }
 
-__device__ __noinline__ Fq12 miller_loop(const G1Affine& p, const G2Affine& q) {
-    if (is_inf(p) || g2_is_inf(q)) return f12_one();
-    Fq12 f = f12_one();
-    G2Proj T = {q.x, q.y, f2_one()};
-    for (int b = 63; b >= 0; b--) {  // 6x + 2 below its top bit, MSB first
-        f = mul_line(f12_sqr(f), dbl_line(T, p.x, p.y));
-        if ((pc::ATE_LOOP_LOW >> b) & 1) f = mul_line(f, add_line(T, q, p.x, p.y));
+// per team: the published Fq12 operands (v, xi v) and the doubling's exchanged products
+struct MillerLds {
+    Fq2 f[TEAM], fx[TEAM], d[TEAM], s[TEAM], sx[TEAM], e[TEAM];
+};
+
+// f times an add_line line (sparse l0 + l1 w + l3 w^3, or the vertical l0 + l2 w^2)
+__device__ __forceinline__ Fq2 team_mul_add_line(MillerLds& L, const TeamLane& tl, const Fq2& f, const Fq12& l) {
+    const bool vert = f2_is_zero(l.c1.c0) && f2_is_zero(l.c1.c1);
+    if (tl.pub) {
+        L.f[tl.k] = f;
+        L.fx[tl.k] = f2_mul_xi(f);
     }
-    // Q1 = pi(Q), -Q2 = -pi^2(Q) on the twist: pi(x, y) = (conj(x) g_x, conj(y) g_y),
-    // pi^2(x, y) = (x g2_x, -y)
+    __syncthreads();
+    const int j[3] = {0, vert ? 2 : 1, 3};
+    const Fq2 v[3] = {l.c0.c0, vert ? l.c0.c1 : l.c1.c0, vert ? f2_zero() : l.c1.c1};
+    const Fq2 r = tm_sparse(L.f, L.fx, j, v, tl.k);
+    __syncthreads();
+    return r;
+}
+
+// chord step T <- T + A with f <- f l, add_line's formulas spread over the lanes in four exchanges:
+//   1  publish f, and lane 0 y_A Z, 1 x_A Z;
+//   2  theta = Y - y_A Z, lambda = X - x_A Z; lane 0 theta^2, 1 lambda^2, 2 -lambda yp,
+//      3 theta xp, 4 lambda y_A, 5 theta x_A;
+//   3  f l (3 products); lane 0 E = lambda D, 1 F = Z C, 2 G = X D;
+//   4  H = E + F - 2G; lane 0 lambda H, 1 theta (G - H), 2 E Y, 3 Z E; then T.
+// Returns whether lambda = 0 (T = +-A: add_line's doubling or vertical case, which this step
+// does not compute; the caller redoes the step with add_line).
+__device__ __noinline__ bool team_add_step(MillerLds& L, const TeamLane& tl, Fq2& f, G2Proj& T, const G2Affine& A,
+                                           const Fq& xp, const Fq& yp) {
+    const int k = tl.k;
+    {
+        const Fq2 d = f2_mul(k == 0 ? A.y : A.x, T.Z);
+        if (tl.pub) {
+            L.f[k] = f;
+            L.fx[k] = f2_mul_xi(f);
+            L.d[k] = d;
+        }
+    }
+    __syncthreads();
+    const Fq2 theta = f2_sub(T.Y, L.d[0]), lam = f2_sub(T.X, L.d[1]);
+    {
+        const Fq2 yp2 = {yp, Fq::zero()}, xp2 = {xp, Fq::zero()};
+        const Fq2 u = k == 0 ? theta : k == 1 ? lam : k == 2 ? f2_neg(lam) : k == 3 ? theta : k == 4 ? lam : theta;
+        const Fq2 v = k == 0 ? theta : k == 1 ? lam : k == 2 ? yp2 : k == 3 ? xp2 : k == 4 ? A.y : A.x;
+        const Fq2 e = f2_mul(u, v);
+        if (tl.pub) L.e[k] = e;
+    }
+    __syncthreads();
+    {
+        const int j[3] = {0, 1, 3};
+        const Fq2 l[3] = {L.e[2], L.e[3], f2_sub(L.e[4], L.e[5])};
+        f = tm_sparse(L.f, L.fx, j, l, k);
+        const Fq2 C = L.e[0], D = L.e[1];
+        const Fq2 g = f2_mul(k == 0 ? lam : k == 1 ? T.Z : T.X, k == 1 ? C : D);
+        if (tl.pub) L.s[k] = g;
+    }
+    __syncthreads();
+    {
+        const Fq2 E = L.s[0], F = L.s[1], G = L.s[2];
+        const Fq2 H = f2_sub(f2_add(E, F), f2_dbl(G));
+        const Fq2 u = k == 0 ? lam : k == 1 ? theta : k == 2 ? E : T.Z;
+        const Fq2 v = k == 0 ? H : k == 1 ? f2_sub(G, H) : k == 2 ? T.Y : E;
+        const Fq2 e = f2_mul(u, v);
+        if (tl.pub) L.e[k] = e;
+    }
+    __syncthreads();
+    T = {L.e[0], f2_sub(L.e[1], L.e[2]), L.e[3]};
+    return f2_is_zero(lam);
+}
+
+// team_add_step, and add_line on every lane for the teams where it met T = +-A (a barrier-uniform
+// branch: every team of the block takes it when any team needs it, and keeps its result only then)
+__device__ __forceinline__ void team_add(MillerLds& L, const TeamLane& tl, Fq2& f, G2Proj& T, const G2Affine& A,
+                                         const Fq& xp, const Fq& yp) {
+    const Fq2 f0 = f;
+    G2Proj T0 = T;
+    const bool special = team_add_step(L, tl, f, T, A, xp, yp);
+    if (__syncthreads_or(special)) {
+        const Fq2 fs = team_mul_add_line(L, tl, f0, add_line(T0, A, xp, yp));
+        if (special) {
+            f = fs;
+            T = T0;
+        }
+    }
+}
+
+// One pair per team, 8 teams per block; 6x + 2 by its non-adjacent form (65 doublings, 21 chord
+// steps, -Q = (x, -y)).  A doubling step is two exchanges:
+//   A  publish f and the tangent's first-level products (lane 0 XY, 1 Y^2, 2 Z^2, 3 X^2,
+//      4 (Y + Z)^2);
+//   B  f^2's coefficient (6 products), E = 3 b' Z^2, and the second level (lane 0 E^2, 1 G^2,
+//      2 A (B - F), 3 B H, 4 -H yp, 5 3 J xp) -- dbl_line's formulas, spread over the lanes;
+//   C  T from the second level, f^2 times the line (3 products).
+// Lines and T are dbl_line's / add_line's exactly; the value after the final exponentiation is the
+// definition's (the signed chain changes f only by vertical lines, which lie in Fq6).
+__global__ void __launch_bounds__(64) k_miller_team(const G1Affine* __restrict__ P, const G2Affine* __restrict__ Q,
+                                                    uint32_t m, Fq12* __restrict__ out) {
+    __shared__ MillerLds lds[64 / TEAM];
+    const TeamLane tl = team_lane();
+    const int k = tl.k;
+    const uint32_t pi = blockIdx.x * (64 / TEAM) + threadIdx.x / TEAM;
+    MillerLds& L = lds[threadIdx.x / TEAM];
+    const G1Affine p = P[min(pi, m - 1)];
+    const G2Affine q = Q[min(pi, m - 1)];
+    const G2Affine nq = {q.x, f2_neg(q.y)};
+    const Fq &xp = p.x, &yp = p.y;
+    Fq2 f = k == 0 ? f2_one() : f2_zero();
+    G2Proj T = {q.x, q.y, f2_one()};
+    for (int b = 64; b >= 0; b--) {
+        {
+            const Fq2 yz = f2_add(T.Y, T.Z);
+            const Fq2 u = k == 0 ? T.X : k == 1 ? T.Y : k == 2 ? T.Z : k == 3 ? T.X : yz;
+            const Fq2 v = k == 0 ? T.Y : k == 1 ? T.Y : k == 2 ? T.Z : k == 3 ? T.X : yz;
+            const Fq2 d = f2_mul(u, v);
+            if (tl.pub) {
+                L.f[k] = f;
+                L.fx[k] = f2_mul_xi(f);
+                L.d[k] = d;
+            }
+        }
+        __syncthreads();
+        const Fq2 B = L.d[1], C = L.d[2];
+        const Fq2 E = f2_mul(f2_add(f2_dbl(C), C), f2_c(pc::TWIST_B));
+        {
+            const Fq2 fs = tm_mul(L.f, L.f, L.fx, k);
+            const Fq2 A = f2_dbl(L.d[0]), J = L.d[3];
+            const Fq2 H = f2_sub(L.d[4], f2_add(B, C));
+            const Fq2 F = f2_add(f2_dbl(E), E), G = f2_add(B, F);
+            const Fq2 yp2 = {yp, Fq::zero()}, xp2 = {xp, Fq::zero()};
+            const Fq2 u = k == 0 ? E : k == 1 ? G : k == 2 ? A : k == 3 ? B : k == 4 ? f2_neg(H) : f2_add(f2_dbl(J), J);
+            const Fq2 v = k == 0 ? E : k == 1 ? G : k == 2 ? f2_sub(B, F) : k == 3 ? H : k == 4 ? yp2 : xp2;
+            const Fq2 e = f2_mul(u, v);
+            if (tl.pub) {
+                L.s[k] = fs;
+                L.sx[k] = f2_mul_xi(fs);
+                L.e[k] = e;
+            }
+        }
+        __syncthreads();
+        {
+            const Fq2 E2 = L.e[0];
+            T.X = L.e[2];
+            T.Y = f2_sub(L.e[1], f2_dbl(f2_dbl(f2_add(f2_dbl(E2), E2))));
+            T.Z = f2_dbl(f2_dbl(L.e[3]));
+            const int j[3] = {0, 1, 3};
+            const Fq2 v[3] = {L.e[4], L.e[5], f2_sub(E, B)};
+            f = tm_sparse(L.s, L.sx, j, v, k);
+        }
+        if (b < 64) {
+            if ((pc::ATE_NAF_POS >> b) & 1) team_add(L, tl, f, T, q, xp, yp);
+            if ((pc::ATE_NAF_NEG >> b) & 1) team_add(L, tl, f, T, nq, xp, yp);
+        }
+    }
     const G2Affine q1 = {f2_mul(f2_conj(q.x), f2_c(pc::TWIST_FROB_X)), f2_mul(f2_conj(q.y), f2_c(pc::TWIST_FROB_Y))};
     const G2Affine nq2 = {f2_mul_fq(q.x, fq_c(pc::TWIST_FROB2_X)), q.y};
-    f = mul_line(f, add_line(T, q1, p.x, p.y));
-    f = mul_line(f, add_line(T, nq2, p.x, p.y));
-    return f;
+    team_add(L, tl, f, T, q1, xp, yp);
+    team_add(L, tl, f, T, nq2, xp, yp);
+    if (is_inf(p) || g2_is_inf(q)) f = k == 0 ? f2_one() : f2_zero();
+    if (pi < m && tl.pub) set_w_coef(out[pi], k, f);
 }
 
-__global__ void __launch_bounds__(64) k_miller(const G1Affine* __restrict__ P, const G2Affine* __restrict__ Q, uint32_t m,
-                                               Fq12* __restrict__ out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    out[i] = miller_loop(P[i], Q[i]);
+struct ExpLds {
+    Fq2 a[TEAM], b[TEAM], bx[TEAM];
+    uint32_t flag[TEAM];
+};
+
+// coefficient k of a b
+__device__ __noinline__ Fq2 team_mul(ExpLds& L, const TeamLane& tl, const Fq2& a, const Fq2& b) {
+    if (tl.pub) {
+        L.a[tl.k] = a;
+        L.b[tl.k] = b;
+        L.bx[tl.k] = f2_mul_xi(b);
+    }
+    __syncthreads();
+    const Fq2 r = tm_mul(L.a, L.b, L.bx, tl.k);
+    __syncthreads();
+    return r;
 }
 
-// a^x for a unitary a (x = pc::BN_X, 63 bits): cyclotomic squarings and x's non-adjacent form,
-// MSB first, a^-1 being conj(a) (23 multiplications instead of 27)
-__device__ __noinline__ Fq12 f12_pow_x(const Fq12& a) {
-    const Fq12 ai = f12_conj(a);
-    Fq12 r = a;
+// coefficient k of a^2 for a unitary a
+__device__ __noinline__ Fq2 team_cyc_sqr(ExpLds& L, const TeamLane& tl, const Fq2& a) {
+    if (tl.pub) L.a[tl.k] = a;
+    __syncthreads();
+    const Fq2 r = tm_cyc_sqr(L.a, tl.k);
+    __syncthreads();
+    return r;
+}
+
+// coefficient k of a^x (x = pc::BN_X by its non-adjacent form, a^-1 = conj(a))
+__device__ __noinline__ Fq2 team_pow_x(ExpLds& L, const TeamLane& tl, const Fq2& a) {
+    const Fq2 ai = tm_conj(a, tl.k);
+    Fq2 r = a;
     for (int b = 61; b >= 0; b--) {
-        r = f12_cyc_sqr(r);
-        if ((pc::BN_X_NAF_POS >> b) & 1) r = f12_mul(r, a);
-        if ((pc::BN_X_NAF_NEG >> b) & 1) r = f12_mul(r, ai);
+        r = team_cyc_sqr(L, tl, r);
+        if ((pc::BN_X_NAF_POS >> b) & 1) r = team_mul(L, tl, r, a);
+        if ((pc::BN_X_NAF_NEG >> b) & 1) r = team_mul(L, tl, r, ai);
     }
     return r;
 }
 
-__device__ __noinline__ Fq12 final_exponentiation(const Fq12& f) {
-    // easy part: f^((q^6 - 1)(q^2 + 1)); t is unitary from here on (its inverse is its conjugate)
-    Fq12 t = f12_mul(f12_conj(f), f12_inv(f));
-    t = f12_mul(f12_frob<2>(t), t);
-    // hard part: t^((q^4 - q^2 + 1) / r) = t^(l0 + l1 q + l2 q^2 + l3 q^3) exactly, the l_i
-    // polynomials in x (Scott et al. 2009; identity asserted in tools/pairing_consts.py):
-    //   y0 = t^(q + q^2 + q^3), y1 = t^-1, y2 = t^(x^2 q^2), y3 = t^(-x q), y4 = t^(-x - x^2 q),
-    //   y5 = t^(-x^2), y6 = t^(-x^3 - x^3 q), and y0 y1^2 y2^6 y3^12 y4^18 y5^30 y6^36 by the chain
-    const Fq12 fx = f12_pow_x(t), fx2 = f12_pow_x(fx), fx3 = f12_pow_x(fx2);
-    const Fq12 y0 = f12_mul(f12_mul(f12_frob<1>(t), f12_frob<2>(t)), f12_frob<3>(t));
-    const Fq12 y1 = f12_conj(t);
-    const Fq12 y2 = f12_frob<2>(fx2);
-    const Fq12 y3 = f12_conj(f12_frob<1>(fx));
-    const Fq12 y4 = f12_conj(f12_mul(fx, f12_frob<1>(fx2)));
-    const Fq12 y5 = f12_conj(fx2);
-    const Fq12 y6 = f12_conj(f12_mul(fx3, f12_frob<1>(fx3)));
-    Fq12 t0 = f12_mul(f12_mul(f12_cyc_sqr(y6), y4), y5);
-    Fq12 t1 = f12_mul(f12_mul(y3, y5), t0);
-    t0 = f12_mul(t0, y2);
-    t1 = f12_cyc_sqr(f12_mul(f12_cyc_sqr(t1), t0));
-    t0 = f12_cyc_sqr(f12_mul(t1, y1));
-    t1 = f12_mul(t1, y0);
-    return f12_mul(t0, t1);
-}
-
-__global__ void k_final_exp(const Fq12* __restrict__ f, uint32_t m, Fq12* __restrict__ out, uint32_t* __restrict__ is_one) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    Fq12 acc = f12_one();
-    for (uint32_t i = 0; i < m; i++) acc = f12_mul(acc, f[i]);
-    const Fq12 r = final_exponentiation(acc);
-    *out = r;
-    *is_one = f12_is_one(r) ? 1u : 0u;
+// One team: the product of the m Miller values, the final exponentiation (easy part
+// f^((q^6 - 1)(q^2 + 1)); hard part t^((q^4 - q^2 + 1) / r) = t^(l0 + l1 q + l2 q^2 + l3 q^3)
+// exactly, the l_i polynomials in x (Scott et al. 2009; identity asserted in
+// tools/pairing_consts.py): y0 = t^(q + q^2 + q^3), y1 = t^-1, y2 = t^(x^2 q^2), y3 = t^(-x q),
+// y4 = t^(-x - x^2 q), y5 = t^(-x^2), y6 = t^(-x^3 - x^3 q), and y0 y1^2 y2^6 y3^12 y4^18 y5^30
+// y6^36 by the addition chain), and the test against 1.  The one inversion gathers the element
+// on every lane.
+__global__ void __launch_bounds__(TEAM) k_final_exp_team(const Fq12* __restrict__ f, uint32_t m,
+                                                         Fq12* __restrict__ out, uint32_t* __restrict__ is_one) {
+    __shared__ ExpLds L;
+    const TeamLane tl = team_lane();
+    const int k = tl.k;
+    Fq2 acc = m ? w_coef(f[0], k) : (k == 0 ? f2_one() : f2_zero());
+    for (uint32_t i = 1; i < m; i++) acc = team_mul(L, tl, acc, w_coef(f[i], k));
+    // easy part; t is unitary from here on (its inverse is its conjugate)
+    if (tl.pub) L.a[k] = acc;
+    __syncthreads();
+    Fq12 whole;
+    for (int j = 0; j < 6; j++) set_w_coef(whole, j, L.a[j]);
+    __syncthreads();
+    const Fq12 inv = f12_inv(whole);
+    Fq2 t = team_mul(L, tl, tm_conj(acc, k), w_coef(inv, k));
+    t = team_mul(L, tl, tm_frob<2>(t, k), t);
+    // hard part
+    const Fq2 fx = team_pow_x(L, tl, t);
+    const Fq2 fx2 = team_pow_x(L, tl, fx);
+    const Fq2 fx3 = team_pow_x(L, tl, fx2);
+    const Fq2 y0 = team_mul(L, tl, team_mul(L, tl, tm_frob<1>(t, k), tm_frob<2>(t, k)), tm_frob<3>(t, k));
+    const Fq2 y1 = tm_conj(t, k);
+    const Fq2 y2 = tm_frob<2>(fx2, k);
+    const Fq2 y3 = tm_conj(tm_frob<1>(fx, k), k);
+    const Fq2 y4 = tm_conj(team_mul(L, tl, fx, tm_frob<1>(fx2, k)), k);
+    const Fq2 y5 = tm_conj(fx2, k);
+    const Fq2 y6 = tm_conj(team_mul(L, tl, fx3, tm_frob<1>(fx3, k)), k);
+    Fq2 t0 = team_mul(L, tl, team_mul(L, tl, team_cyc_sqr(L, tl, y6), y4), y5);
+    Fq2 t1 = team_mul(L, tl, team_mul(L, tl, y3, y5), t0);
+    t0 = team_mul(L, tl, t0, y2);
+    t1 = team_cyc_sqr(L, tl, team_mul(L, tl, team_cyc_sqr(L, tl, t1), t0));
+    t0 = team_cyc_sqr(L, tl, team_mul(L, tl, t1, y1));
+    t1 = team_mul(L, tl, t1, y0);
+    const Fq2 r = team_mul(L, tl, t0, t1);
+    if (tl.pub) {
+        set_w_coef(*out, k, r);
+        L.flag[k] = f2_eq(r, k == 0 ? f2_one() : f2_zero()) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t all = 1;
+        for (int j = 0; j < 6; j++) all &= L.flag[j];
+        *is_one = all;
+    }
 }
 
 // ---- verify_batch: merged pairs -----------------------------------------------------------------
@@ -337,11 +535,12 @@ Status pair_product(eon_ctx* ctx, const G1Affine* P, const G2Affine* Q, uint32_t
     DevBuf f, res;
     EON_HIP(f.ensure((size_t)std::max<uint32_t>(m, 1) * sizeof(Fq12)));
     EON_HIP(res.ensure(sizeof(Fq12) + 16));
-    ctx->prof.begin("k_miller", (uint64_t)m * (64 + 128 + 384), ctx->stream);
-    if (m) hipLaunchKernelGGL(k_miller, dim3((m + 63) / 64), dim3(64), 0, ctx->stream, P, Q, m, f.as<Fq12>());
+    ctx->prof.begin("k_miller_team", (uint64_t)m * (64 + 128 + 384), ctx->stream);
+    if (m) hipLaunchKernelGGL(k_miller_team, dim3((m + 64 / TEAM - 1) / (64 / TEAM)), dim3(64), 0, ctx->stream, P, Q, m,
+                              f.as<Fq12>());
     ctx->prof.end(ctx->stream);
-    ctx->prof.begin("k_final_exp", (uint64_t)m * 384 + 384, ctx->stream);
-    hipLaunchKernelGGL(k_final_exp, dim3(1), dim3(64), 0, ctx->stream, f.as<Fq12>(), m, res.as<Fq12>(),
+    ctx->prof.begin("k_final_exp_team", (uint64_t)m * 384 + 384, ctx->stream);
+    hipLaunchKernelGGL(k_final_exp_team, dim3(1), dim3(TEAM), 0, ctx->stream, f.as<Fq12>(), m, res.as<Fq12>(),
                        reinterpret_cast<uint32_t*>(res.as<char>() + sizeof(Fq12)));
     ctx->prof.end(ctx->stream);
     EON_HIP(hipGetLastError());

@@ -144,6 +144,24 @@ def main():
     ate = 6 * X_BN + 2
     assert ate.bit_length() == 65
     out.append(f"constexpr uint64_t ATE_LOOP_LOW = 0x{ate & ((1 << 64) - 1):x}ull;  // 6x + 2 below its top bit (bit 64)")
+    # 6x + 2 in non-adjacent form for the Miller loop: 22 nonzero digits against 37 set bits; the
+    # top digit is 65 and digit 64 is zero, so the loop runs bits 64..0 from the masks
+    pos = neg = 0
+    k, i = ate, 0
+    while k:
+        if k & 1:
+            d = 2 - (k % 4)
+            k -= d
+            if d == 1:
+                pos |= 1 << i
+            else:
+                neg |= 1 << i
+        k //= 2
+        i += 1
+    assert pos - neg == ate and pos >> 65 == 1 and (pos | neg) >> 64 == 2
+    low = (1 << 64) - 1
+    out.append(f"constexpr uint64_t ATE_NAF_POS = 0x{pos & low:x}ull, ATE_NAF_NEG = 0x{neg & low:x}ull;"
+               "  // 6x + 2 = 2^65 + POS - NEG")
     print("\n".join(out))
 
 

@@ -89,6 +89,25 @@ struct DevPool {
     }
 };
 
+// The buffers local to one call, taken from a DevPool and given back when the scope ends -- on
+// every path, early error returns included -- after the stream that used them has drained.
+struct PoolScope {
+    DevPool& pool;
+    hipStream_t st;
+    std::vector<DevBuf*> bufs;
+    PoolScope(DevPool& p, hipStream_t s) : pool(p), st(s) {}
+    PoolScope(const PoolScope&) = delete;
+    PoolScope& operator=(const PoolScope&) = delete;
+    hipError_t take(DevBuf& b, size_t need) {
+        bufs.push_back(&b);
+        return pool.take(b, need);
+    }
+    ~PoolScope() {
+        (void)hipStreamSynchronize(st);
+        for (DevBuf* b : bufs) pool.give(*b);
+    }
+};
+
 struct Status {
     int code = EON_OK;
     std::string msg;

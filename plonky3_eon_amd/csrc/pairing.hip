@@ -532,9 +532,10 @@ void fq12_to_abi(const Fq12& a, eon_fq12& out) {
 
 // product of the pairings of m device pairs -> Gt element and the is-one flag (host)
 Status pair_product(eon_ctx* ctx, const G1Affine* P, const G2Affine* Q, uint32_t m, Fq12* gt, bool* one) {
+    PoolScope ps(ctx->pool, ctx->stream);
     DevBuf f, res;
-    EON_HIP(f.ensure((size_t)std::max<uint32_t>(m, 1) * sizeof(Fq12)));
-    EON_HIP(res.ensure(sizeof(Fq12) + 16));
+    EON_HIP(ps.take(f, (size_t)std::max<uint32_t>(m, 1) * sizeof(Fq12)));
+    EON_HIP(ps.take(res, sizeof(Fq12) + 16));
     ctx->prof.begin("k_miller_team", (uint64_t)m * (64 + 128 + 384), ctx->stream);
     if (m) hipLaunchKernelGGL(k_miller_team, dim3((m + 64 / TEAM - 1) / (64 / TEAM)), dim3(64), 0, ctx->stream, P, Q, m,
                               f.as<Fq12>());
@@ -575,8 +576,9 @@ int eon_g2_mul(eon_ctx* ctx, const eon_g2_affine* base, const eon_fr* k, eon_g2_
         if (base) EON_TRY(g2_from_abi(*base, b));
         const Fr kk = fr_from_abi(k);
         if (!fr_is_canonical(kk)) return Status::err(EON_E_ARG, "scalar is not a canonical Fr");
+        PoolScope ps(ctx->pool, ctx->stream);
         DevBuf d;
-        EON_HIP(d.ensure(sizeof(G2Affine)));
+        EON_HIP(ps.take(d, sizeof(G2Affine)));
         hipLaunchKernelGGL(k_g2_mul, dim3(1), dim3(64), 0, ctx->stream, b, kk, d.as<G2Affine>());
         EON_HIP(hipGetLastError());
         G2Affine r;
@@ -601,9 +603,10 @@ int eon_multi_pairing(eon_ctx* ctx, const eon_g1_affine* p, const eon_g2_affine*
             EON_TRY(g1_from_abi(p[i], hp[i]));
             EON_TRY(g2_from_abi(q[i], hq[i]));
         }
+        PoolScope ps(ctx->pool, ctx->stream);
         DevBuf dp, dq;
-        EON_HIP(dp.ensure(std::max<uint64_t>(n, 1) * sizeof(G1Affine)));
-        EON_HIP(dq.ensure(std::max<uint64_t>(n, 1) * sizeof(G2Affine)));
+        EON_HIP(ps.take(dp, std::max<uint64_t>(n, 1) * sizeof(G1Affine)));
+        EON_HIP(ps.take(dq, std::max<uint64_t>(n, 1) * sizeof(G2Affine)));
         if (n) {
             EON_HIP(hipMemcpyAsync(dp.p, hp.data(), n * sizeof(G1Affine), hipMemcpyHostToDevice, ctx->stream));
             EON_HIP(hipMemcpyAsync(dq.p, hq.data(), n * sizeof(G2Affine), hipMemcpyHostToDevice, ctx->stream));
@@ -661,17 +664,18 @@ int eon_kzg_verify_batch(eon_ctx* ctx, const eon_g1_affine* commitments, const e
             std::vector<uint32_t> fill(gs.begin(), gs.end() - 1);
             for (uint64_t i = 0; i < n; i++) ord[fill[grp[i]]++] = (uint32_t)i;
         }
+        PoolScope ps(ctx->pool, ctx->stream);
         DevBuf dc, dw, dv, dord, dgs, dz, dsums, dvsum, dP, dQ;
-        EON_HIP(dc.ensure(n * sizeof(G1Affine)));
-        EON_HIP(dw.ensure(n * sizeof(G1Affine)));
-        EON_HIP(dv.ensure(n * sizeof(Fr)));
-        EON_HIP(dord.ensure(n * 4));
-        EON_HIP(dgs.ensure((G + 1) * 4));
-        EON_HIP(dz.ensure(G * sizeof(Fr)));
-        EON_HIP(dsums.ensure((G + 1) * sizeof(G1Xyzz)));
-        EON_HIP(dvsum.ensure(sizeof(Fr)));
-        EON_HIP(dP.ensure((G + 1) * sizeof(G1Affine)));
-        EON_HIP(dQ.ensure((G + 1) * sizeof(G2Affine)));
+        EON_HIP(ps.take(dc, n * sizeof(G1Affine)));
+        EON_HIP(ps.take(dw, n * sizeof(G1Affine)));
+        EON_HIP(ps.take(dv, n * sizeof(Fr)));
+        EON_HIP(ps.take(dord, n * 4));
+        EON_HIP(ps.take(dgs, (G + 1) * 4));
+        EON_HIP(ps.take(dz, G * sizeof(Fr)));
+        EON_HIP(ps.take(dsums, (G + 1) * sizeof(G1Xyzz)));
+        EON_HIP(ps.take(dvsum, sizeof(Fr)));
+        EON_HIP(ps.take(dP, (G + 1) * sizeof(G1Affine)));
+        EON_HIP(ps.take(dQ, (G + 1) * sizeof(G2Affine)));
         hipStream_t st = ctx->stream;
         EON_HIP(hipMemcpyAsync(dc.p, hc.data(), n * sizeof(G1Affine), hipMemcpyHostToDevice, st));
         EON_HIP(hipMemcpyAsync(dw.p, hw.data(), n * sizeof(G1Affine), hipMemcpyHostToDevice, st));

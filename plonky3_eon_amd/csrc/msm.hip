@@ -100,7 +100,11 @@ constexpr uint32_t DIGIT_COLS = 4;  // widest scalar tile of one 256-thread bloc
 
 // The digit sort's per-pass histograms of the keys (radix_sort_histograms) are counted here, in
 // LDS per block and added to the global bins once per block, so the sort never re-reads the keys
-// for them.
+// for them.  Blocks walk row tiles grid-stride (the grid is capped near DIGIT_BLOCKS): every block
+// adds its bins to the same few hundred global counters, so one block per tile would put
+// ~E / 8 atomics on those addresses.
+constexpr uint32_t DIGIT_BLOCKS = 4096;
+
 __global__ void __launch_bounds__(256) k_msm_digits(const Fr* scalars, uint64_t n, uint64_t ld,
                                                     uint32_t cols, uint32_t c, uint32_t windows,
                                                     uint32_t ref_windows, uint32_t precomputed,
@@ -109,14 +113,15 @@ __global__ void __launch_bounds__(256) k_msm_digits(const Fr* scalars, uint64_t 
     __shared__ uint32_t h[RADIX_SORT_MAX_PASSES][256];
     for (uint32_t j = threadIdx.x; j < RADIX_SORT_MAX_PASSES * 256; j += 256) (&h[0][0])[j] = 0;
     __syncthreads();
-    // a block reads 256 / tile_cols row segments of tile_cols adjacent columns (up to 128
-    // contiguous bytes), so the group-major writes stay in runs of consecutive rows
+    // a tile is 256 / tile_cols row segments of tile_cols adjacent columns (up to 128 contiguous
+    // bytes), so the group-major writes stay in runs of consecutive rows
     const uint32_t col = blockIdx.y * tile_cols + threadIdx.x % tile_cols;
-    const uint64_t i = (uint64_t)blockIdx.x * (256 / tile_cols) + threadIdx.x / tile_cols;
-    if (col < cols && i < n) {
+    const uint32_t rows = 256 / tile_cols;
+    const uint32_t B = 1u << (c - 1);
+    for (uint64_t i = (uint64_t)blockIdx.x * rows + threadIdx.x / tile_cols; col < cols && i < n;
+         i += (uint64_t)gridDim.x * rows) {
         Fr s = to_canonical(ld_pinned(scalars + i * ld + col));
         pin(s);
-        const uint32_t B = 1u << (c - 1);
         uint32_t carry = 0;
         for (uint32_t w = 0; w < windows; w++) {
             const uint32_t raw = window_bits(s.v, w * c, c) + carry;
@@ -906,8 +911,10 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     prof->begin("k_msm_digits", n * bt.cols * 32 + E * 8, st);
     const uint32_t tile_cols = bt.cols >= DIGIT_COLS ? DIGIT_COLS : (bt.cols >= 2 ? 2 : 1);
     const uint32_t tile_rows = 256 / tile_cols;
-    hipLaunchKernelGGL(k_msm_digits, dim3((unsigned)((n + tile_rows - 1) / tile_rows),
-                                          (bt.cols + tile_cols - 1) / tile_cols),
+    const uint32_t grid_y = (bt.cols + tile_cols - 1) / tile_cols;
+    const uint64_t tiles = (n + tile_rows - 1) / tile_rows;
+    const uint32_t grid_x = (uint32_t)std::min<uint64_t>(tiles, std::max<uint32_t>(1, DIGIT_BLOCKS / grid_y));
+    hipLaunchKernelGGL(k_msm_digits, dim3(grid_x, grid_y),
                        dim3(256), 0, st, bt.scalars, n, ld, bt.cols, bt.c, bt.W, L.W, (uint32_t)L.precomputed,
                        tile_cols, wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>(), radix_sort_passes(bt.key_bits),
                        hist);

@@ -49,12 +49,16 @@ EON_HD Fq2 f2_dbl(const Fq2& a) { return {dbl(a.c0), dbl(a.c1)}; }
 EON_HD Fq2 f2_conj(const Fq2& a) { return {a.c0, neg(a.c1)}; }
 EON_HD Fq2 f2_mul_fq(const Fq2& a, const Fq& b) { return {mul(a.c0, b), mul(a.c1, b)}; }
 
-// (a0 + a1 u)(b0 + b1 u), u^2 = -1 (Karatsuba: 3 products)
-EON_NI Fq2 f2_mul(const Fq2& a, const Fq2& b) {
+// (a0 + a1 u)(b0 + b1 u), u^2 = -1 (Karatsuba: 3 products).  f2_mul_inl is the inlined body for
+// the latency-bound team kernels (pairing_team.h): a call passes its Fq2 operands through scratch
+// (the calling convention takes at most 16 registers of aggregate arguments).
+EON_HD Fq2 f2_mul_inl(const Fq2& a, const Fq2& b) {
     const Fq t0 = mul(a.c0, b.c0), t1 = mul(a.c1, b.c1);
     const Fq t2 = mul(add(a.c0, a.c1), add(b.c0, b.c1));
     return {sub(t0, t1), sub(sub(t2, t0), t1)};
 }
+
+EON_NI Fq2 f2_mul(const Fq2& a, const Fq2& b) { return f2_mul_inl(a, b); }
 
 EON_NI Fq2 f2_sqr(const Fq2& a) {
     const Fq t = mul(a.c0, a.c1);

@@ -141,11 +141,11 @@ __device__ __forceinline__ Fq2 team_mul_add_line(MillerLds& L, const TeamLane& t
 //   4  H = E + F - 2G; lane 0 lambda H, 1 theta (G - H), 2 E Y, 3 Z E; then T.
 // Returns whether lambda = 0 (T = +-A: add_line's doubling or vertical case, which this step
 // does not compute; the caller redoes the step with add_line).
-__device__ __noinline__ bool team_add_step(MillerLds& L, const TeamLane& tl, Fq2& f, G2Proj& T, const G2Affine& A,
-                                           const Fq& xp, const Fq& yp) {
+__device__ __forceinline__ bool team_add_step(MillerLds& L, const TeamLane& tl, Fq2& f, G2Proj& T, const G2Affine& A,
+                                              const Fq& xp, const Fq& yp) {
     const int k = tl.k;
     {
-        const Fq2 d = f2_mul(k == 0 ? A.y : A.x, T.Z);
+        const Fq2 d = f2_mul_inl(k == 0 ? A.y : A.x, T.Z);
         if (tl.pub) {
             L.f[k] = f;
             L.fx[k] = f2_mul_xi(f);
@@ -158,7 +158,7 @@ __device__ __noinline__ bool team_add_step(MillerLds& L, const TeamLane& tl, Fq2
         const Fq2 yp2 = {yp, Fq::zero()}, xp2 = {xp, Fq::zero()};
         const Fq2 u = k == 0 ? theta : k == 1 ? lam : k == 2 ? f2_neg(lam) : k == 3 ? theta : k == 4 ? lam : theta;
         const Fq2 v = k == 0 ? theta : k == 1 ? lam : k == 2 ? yp2 : k == 3 ? xp2 : k == 4 ? A.y : A.x;
-        const Fq2 e = f2_mul(u, v);
+        const Fq2 e = f2_mul_inl(u, v);
         if (tl.pub) L.e[k] = e;
     }
     __syncthreads();
@@ -167,7 +167,7 @@ __device__ __noinline__ bool team_add_step(MillerLds& L, const TeamLane& tl, Fq2
         const Fq2 l[3] = {L.e[2], L.e[3], f2_sub(L.e[4], L.e[5])};
         f = tm_sparse(L.f, L.fx, j, l, k);
         const Fq2 C = L.e[0], D = L.e[1];
-        const Fq2 g = f2_mul(k == 0 ? lam : k == 1 ? T.Z : T.X, k == 1 ? C : D);
+        const Fq2 g = f2_mul_inl(k == 0 ? lam : k == 1 ? T.Z : T.X, k == 1 ? C : D);
         if (tl.pub) L.s[k] = g;
     }
     __syncthreads();
@@ -176,7 +176,7 @@ __device__ __noinline__ bool team_add_step(MillerLds& L, const TeamLane& tl, Fq2
         const Fq2 H = f2_sub(f2_add(E, F), f2_dbl(G));
         const Fq2 u = k == 0 ? lam : k == 1 ? theta : k == 2 ? E : T.Z;
         const Fq2 v = k == 0 ? H : k == 1 ? f2_sub(G, H) : k == 2 ? T.Y : E;
-        const Fq2 e = f2_mul(u, v);
+        const Fq2 e = f2_mul_inl(u, v);
         if (tl.pub) L.e[k] = e;
     }
     __syncthreads();
@@ -192,7 +192,10 @@ __device__ __forceinline__ void team_add(MillerLds& L, const TeamLane& tl, Fq2& 
     G2Proj T0 = T;
     const bool special = team_add_step(L, tl, f, T, A, xp, yp);
     if (__syncthreads_or(special)) {
-        const Fq2 fs = team_mul_add_line(L, tl, f0, add_line(T0, A, xp, yp));
+        // copies made here, so that no operand of the hot path has its address taken by the call
+        G2Affine a_c = A;
+        Fq xp_c = xp, yp_c = yp;
+        const Fq2 fs = team_mul_add_line(L, tl, f0, add_line(T0, a_c, xp_c, yp_c));
         if (special) {
             f = fs;
             T = T0;
@@ -218,59 +221,69 @@ __global__ void __launch_bounds__(64) k_miller_team(const G1Affine* __restrict__
     MillerLds& L = lds[threadIdx.x / TEAM];
     const G1Affine p = P[min(pi, m - 1)];
     const G2Affine q = Q[min(pi, m - 1)];
-    const G2Affine nq = {q.x, f2_neg(q.y)};
     const Fq &xp = p.x, &yp = p.y;
     Fq2 f = k == 0 ? f2_one() : f2_zero();
     G2Proj T = {q.x, q.y, f2_one()};
-    for (int b = 64; b >= 0; b--) {
-        {
-            const Fq2 yz = f2_add(T.Y, T.Z);
-            const Fq2 u = k == 0 ? T.X : k == 1 ? T.Y : k == 2 ? T.Z : k == 3 ? T.X : yz;
-            const Fq2 v = k == 0 ? T.Y : k == 1 ? T.Y : k == 2 ? T.Z : k == 3 ? T.X : yz;
-            const Fq2 d = f2_mul(u, v);
-            if (tl.pub) {
-                L.f[k] = f;
-                L.fx[k] = f2_mul_xi(f);
-                L.d[k] = d;
+    // b = 64 .. 0: the doubling and the digit's chord; b = -1, -2: the chords through pi(Q) and
+    // -pi^2(Q).  One inlined copy of each step (calls would pass T and f through scratch).
+    for (int b = 64; b >= -2; b--) {
+        if (b >= 0) {
+            {
+                const Fq2 yz = f2_add(T.Y, T.Z);
+                const Fq2 u = k == 0 ? T.X : k == 1 ? T.Y : k == 2 ? T.Z : k == 3 ? T.X : yz;
+                const Fq2 v = k == 0 ? T.Y : k == 1 ? T.Y : k == 2 ? T.Z : k == 3 ? T.X : yz;
+                const Fq2 d = f2_mul_inl(u, v);
+                if (tl.pub) {
+                    L.f[k] = f;
+                    L.fx[k] = f2_mul_xi(f);
+                    L.d[k] = d;
+                }
+            }
+            __syncthreads();
+            const Fq2 B = L.d[1], C = L.d[2];
+            const Fq2 E = f2_mul_inl(f2_add(f2_dbl(C), C), f2_c(pc::TWIST_B));
+            {
+                const Fq2 fs = tm_mul(L.f, L.f, L.fx, k);
+                const Fq2 A = f2_dbl(L.d[0]), J = L.d[3];
+                const Fq2 H = f2_sub(L.d[4], f2_add(B, C));
+                const Fq2 F = f2_add(f2_dbl(E), E), G = f2_add(B, F);
+                const Fq2 yp2 = {yp, Fq::zero()}, xp2 = {xp, Fq::zero()};
+                const Fq2 u = k == 0 ? E : k == 1 ? G : k == 2 ? A : k == 3 ? B : k == 4 ? f2_neg(H) : f2_add(f2_dbl(J), J);
+                const Fq2 v = k == 0 ? E : k == 1 ? G : k == 2 ? f2_sub(B, F) : k == 3 ? H : k == 4 ? yp2 : xp2;
+                const Fq2 e = f2_mul_inl(u, v);
+                if (tl.pub) {
+                    L.s[k] = fs;
+                    L.sx[k] = f2_mul_xi(fs);
+                    L.e[k] = e;
+                }
+            }
+            __syncthreads();
+            {
+                const Fq2 E2 = L.e[0];
+                T.X = L.e[2];
+                T.Y = f2_sub(L.e[1], f2_dbl(f2_dbl(f2_add(f2_dbl(E2), E2))));
+                T.Z = f2_dbl(f2_dbl(L.e[3]));
+                const int j[3] = {0, 1, 3};
+                const Fq2 v[3] = {L.e[4], L.e[5], f2_sub(E, B)};
+                f = tm_sparse(L.s, L.sx, j, v, k);
             }
         }
-        __syncthreads();
-        const Fq2 B = L.d[1], C = L.d[2];
-        const Fq2 E = f2_mul(f2_add(f2_dbl(C), C), f2_c(pc::TWIST_B));
-        {
-            const Fq2 fs = tm_mul(L.f, L.f, L.fx, k);
-            const Fq2 A = f2_dbl(L.d[0]), J = L.d[3];
-            const Fq2 H = f2_sub(L.d[4], f2_add(B, C));
-            const Fq2 F = f2_add(f2_dbl(E), E), G = f2_add(B, F);
-            const Fq2 yp2 = {yp, Fq::zero()}, xp2 = {xp, Fq::zero()};
-            const Fq2 u = k == 0 ? E : k == 1 ? G : k == 2 ? A : k == 3 ? B : k == 4 ? f2_neg(H) : f2_add(f2_dbl(J), J);
-            const Fq2 v = k == 0 ? E : k == 1 ? G : k == 2 ? f2_sub(B, F) : k == 3 ? H : k == 4 ? yp2 : xp2;
-            const Fq2 e = f2_mul(u, v);
-            if (tl.pub) {
-                L.s[k] = fs;
-                L.sx[k] = f2_mul_xi(fs);
-                L.e[k] = e;
+        const bool pos = b >= 0 && b < 64 && ((pc::ATE_NAF_POS >> b) & 1);
+        const bool neg = b >= 0 && b < 64 && ((pc::ATE_NAF_NEG >> b) & 1);
+        if (pos || neg || b < 0) {
+            // the chord's point, formed here (uniform branches) rather than kept live across the
+            // loop: -Q = (x, -y), pi(Q) = (conj(x) g_x, conj(y) g_y), -pi^2(Q) = (x g2_x, y)
+            G2Affine A = q;
+            if (neg) {
+                A.y = f2_neg(q.y);
+            } else if (b == -1) {
+                A = {f2_mul_inl(f2_conj(q.x), f2_c(pc::TWIST_FROB_X)), f2_mul_inl(f2_conj(q.y), f2_c(pc::TWIST_FROB_Y))};
+            } else if (b == -2) {
+                A.x = f2_mul_fq(q.x, fq_c(pc::TWIST_FROB2_X));
             }
-        }
-        __syncthreads();
-        {
-            const Fq2 E2 = L.e[0];
-            T.X = L.e[2];
-            T.Y = f2_sub(L.e[1], f2_dbl(f2_dbl(f2_add(f2_dbl(E2), E2))));
-            T.Z = f2_dbl(f2_dbl(L.e[3]));
-            const int j[3] = {0, 1, 3};
-            const Fq2 v[3] = {L.e[4], L.e[5], f2_sub(E, B)};
-            f = tm_sparse(L.s, L.sx, j, v, k);
-        }
-        if (b < 64) {
-            if ((pc::ATE_NAF_POS >> b) & 1) team_add(L, tl, f, T, q, xp, yp);
-            if ((pc::ATE_NAF_NEG >> b) & 1) team_add(L, tl, f, T, nq, xp, yp);
+            team_add(L, tl, f, T, A, xp, yp);
         }
     }
-    const G2Affine q1 = {f2_mul(f2_conj(q.x), f2_c(pc::TWIST_FROB_X)), f2_mul(f2_conj(q.y), f2_c(pc::TWIST_FROB_Y))};
-    const G2Affine nq2 = {f2_mul_fq(q.x, fq_c(pc::TWIST_FROB2_X)), q.y};
-    team_add(L, tl, f, T, q1, xp, yp);
-    team_add(L, tl, f, T, nq2, xp, yp);
     if (is_inf(p) || g2_is_inf(q)) f = k == 0 ? f2_one() : f2_zero();
     if (pi < m && tl.pub) set_w_coef(out[pi], k, f);
 }
@@ -280,36 +293,50 @@ struct ExpLds {
     uint32_t flag[TEAM];
 };
 
+// the final exponentiation's exchange slots (one team per launch).  Namespace scope, so that the
+// called helpers below address it as LDS directly; their operands go by value (registers), not by
+// reference (scratch)
+__shared__ ExpLds g_exp;
+
+// The exchanges inline (publish, barrier, compute, barrier); the products of the compute half are
+// one called function per kind reading the slots, so the ~20 products of the chain share a copy of
+// the code and no operand passes through a call (an Fq2 pair exceeds the 16 registers the calling
+// convention gives aggregate arguments, and the rest would go through scratch).
+__device__ __noinline__ Fq2 team_mul_compute() { return tm_mul(g_exp.a, g_exp.b, g_exp.bx, team_lane().k); }
+__device__ __noinline__ Fq2 team_cyc_sqr_compute() { return tm_cyc_sqr(g_exp.a, team_lane().k); }
+
 // coefficient k of a b
-__device__ __noinline__ Fq2 team_mul(ExpLds& L, const TeamLane& tl, const Fq2& a, const Fq2& b) {
+__device__ __forceinline__ Fq2 team_mul(const Fq2& a, const Fq2& b) {
+    const TeamLane tl = team_lane();
     if (tl.pub) {
-        L.a[tl.k] = a;
-        L.b[tl.k] = b;
-        L.bx[tl.k] = f2_mul_xi(b);
+        g_exp.a[tl.k] = a;
+        g_exp.b[tl.k] = b;
+        g_exp.bx[tl.k] = f2_mul_xi(b);
     }
     __syncthreads();
-    const Fq2 r = tm_mul(L.a, L.b, L.bx, tl.k);
+    const Fq2 r = team_mul_compute();
     __syncthreads();
     return r;
 }
 
 // coefficient k of a^2 for a unitary a
-__device__ __noinline__ Fq2 team_cyc_sqr(ExpLds& L, const TeamLane& tl, const Fq2& a) {
-    if (tl.pub) L.a[tl.k] = a;
+__device__ __forceinline__ Fq2 team_cyc_sqr(const Fq2& a) {
+    const TeamLane tl = team_lane();
+    if (tl.pub) g_exp.a[tl.k] = a;
     __syncthreads();
-    const Fq2 r = tm_cyc_sqr(L.a, tl.k);
+    const Fq2 r = team_cyc_sqr_compute();
     __syncthreads();
     return r;
 }
 
 // coefficient k of a^x (x = pc::BN_X by its non-adjacent form, a^-1 = conj(a))
-__device__ __noinline__ Fq2 team_pow_x(ExpLds& L, const TeamLane& tl, const Fq2& a) {
-    const Fq2 ai = tm_conj(a, tl.k);
+__device__ __noinline__ Fq2 team_pow_x(Fq2 a) {
+    const Fq2 ai = tm_conj(a, team_lane().k);
     Fq2 r = a;
     for (int b = 61; b >= 0; b--) {
-        r = team_cyc_sqr(L, tl, r);
-        if ((pc::BN_X_NAF_POS >> b) & 1) r = team_mul(L, tl, r, a);
-        if ((pc::BN_X_NAF_NEG >> b) & 1) r = team_mul(L, tl, r, ai);
+        r = team_cyc_sqr(r);
+        if ((pc::BN_X_NAF_POS >> b) & 1) r = team_mul(r, a);
+        if ((pc::BN_X_NAF_NEG >> b) & 1) r = team_mul(r, ai);
     }
     return r;
 }
@@ -323,11 +350,11 @@ __device__ __noinline__ Fq2 team_pow_x(ExpLds& L, const TeamLane& tl, const Fq2&
 // on every lane.
 __global__ void __launch_bounds__(TEAM) k_final_exp_team(const Fq12* __restrict__ f, uint32_t m,
                                                          Fq12* __restrict__ out, uint32_t* __restrict__ is_one) {
-    __shared__ ExpLds L;
+    ExpLds& L = g_exp;
     const TeamLane tl = team_lane();
     const int k = tl.k;
     Fq2 acc = m ? w_coef(f[0], k) : (k == 0 ? f2_one() : f2_zero());
-    for (uint32_t i = 1; i < m; i++) acc = team_mul(L, tl, acc, w_coef(f[i], k));
+    for (uint32_t i = 1; i < m; i++) acc = team_mul(acc, w_coef(f[i], k));
     // easy part; t is unitary from here on (its inverse is its conjugate)
     if (tl.pub) L.a[k] = acc;
     __syncthreads();
@@ -335,26 +362,26 @@ __global__ void __launch_bounds__(TEAM) k_final_exp_team(const Fq12* __restrict_
     for (int j = 0; j < 6; j++) set_w_coef(whole, j, L.a[j]);
     __syncthreads();
     const Fq12 inv = f12_inv(whole);
-    Fq2 t = team_mul(L, tl, tm_conj(acc, k), w_coef(inv, k));
-    t = team_mul(L, tl, tm_frob<2>(t, k), t);
+    Fq2 t = team_mul(tm_conj(acc, k), w_coef(inv, k));
+    t = team_mul(tm_frob<2>(t, k), t);
     // hard part
-    const Fq2 fx = team_pow_x(L, tl, t);
-    const Fq2 fx2 = team_pow_x(L, tl, fx);
-    const Fq2 fx3 = team_pow_x(L, tl, fx2);
-    const Fq2 y0 = team_mul(L, tl, team_mul(L, tl, tm_frob<1>(t, k), tm_frob<2>(t, k)), tm_frob<3>(t, k));
+    const Fq2 fx = team_pow_x(t);
+    const Fq2 fx2 = team_pow_x(fx);
+    const Fq2 fx3 = team_pow_x(fx2);
+    const Fq2 y0 = team_mul(team_mul(tm_frob<1>(t, k), tm_frob<2>(t, k)), tm_frob<3>(t, k));
     const Fq2 y1 = tm_conj(t, k);
     const Fq2 y2 = tm_frob<2>(fx2, k);
     const Fq2 y3 = tm_conj(tm_frob<1>(fx, k), k);
-    const Fq2 y4 = tm_conj(team_mul(L, tl, fx, tm_frob<1>(fx2, k)), k);
+    const Fq2 y4 = tm_conj(team_mul(fx, tm_frob<1>(fx2, k)), k);
     const Fq2 y5 = tm_conj(fx2, k);
-    const Fq2 y6 = tm_conj(team_mul(L, tl, fx3, tm_frob<1>(fx3, k)), k);
-    Fq2 t0 = team_mul(L, tl, team_mul(L, tl, team_cyc_sqr(L, tl, y6), y4), y5);
-    Fq2 t1 = team_mul(L, tl, team_mul(L, tl, y3, y5), t0);
-    t0 = team_mul(L, tl, t0, y2);
-    t1 = team_cyc_sqr(L, tl, team_mul(L, tl, team_cyc_sqr(L, tl, t1), t0));
-    t0 = team_cyc_sqr(L, tl, team_mul(L, tl, t1, y1));
-    t1 = team_mul(L, tl, t1, y0);
-    const Fq2 r = team_mul(L, tl, t0, t1);
+    const Fq2 y6 = tm_conj(team_mul(fx3, tm_frob<1>(fx3, k)), k);
+    Fq2 t0 = team_mul(team_mul(team_cyc_sqr(y6), y4), y5);
+    Fq2 t1 = team_mul(team_mul(y3, y5), t0);
+    t0 = team_mul(t0, y2);
+    t1 = team_cyc_sqr(team_mul(team_cyc_sqr(t1), t0));
+    t0 = team_cyc_sqr(team_mul(t1, y1));
+    t1 = team_mul(t1, y0);
+    const Fq2 r = team_mul(t0, t1);
     if (tl.pub) {
         set_w_coef(*out, k, r);
         L.flag[k] = f2_eq(r, k == 0 ? f2_one() : f2_zero()) ? 1u : 0u;

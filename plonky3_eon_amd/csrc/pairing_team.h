@@ -46,7 +46,7 @@ EON_HD Fq2 tm_mul(const Fq2* a, const Fq2* b, const Fq2* bx, int k) {
     for (int i = 0; i < 6; i++) {
         const int j = k - i;
         const Fq2* src = j < 0 ? bx : b;
-        acc = f2_add(acc, f2_mul(a[i], src[j < 0 ? j + 6 : j]));
+        acc = f2_add(acc, f2_mul_inl(a[i], src[j < 0 ? j + 6 : j]));
     }
     return acc;
 }
@@ -60,7 +60,7 @@ EON_HD Fq2 tm_sparse(const Fq2* a, const Fq2* ax, const int (&j)[N], const Fq2 (
     for (int t = 0; t < N; t++) {
         const int i = k - j[t];
         const Fq2* src = i < 0 ? ax : a;
-        acc = f2_add(acc, f2_mul(src[i < 0 ? i + 6 : i], l[t]));
+        acc = f2_add(acc, f2_mul_inl(src[i < 0 ? i + 6 : i], l[t]));
     }
     return acc;
 }
@@ -72,8 +72,8 @@ EON_HD Fq2 tm_sparse(const Fq2* a, const Fq2* ax, const int (&j)[N], const Fq2 (
 EON_HD Fq2 tm_cyc_sqr(const Fq2* a, int k) {
     const int m = (k == 0 || k == 3) ? 0 : (k == 2 || k == 5) ? 1 : 2;
     const Fq2 x = a[m], y = a[m + 3], z = a[k];
-    const Fq2 t = f2_mul(x, y);
-    const Fq2 u = f2_mul(f2_add(x, y), f2_add(x, f2_mul_xi(y)));
+    const Fq2 t = f2_mul_inl(x, y);
+    const Fq2 u = f2_mul_inl(f2_add(x, y), f2_add(x, f2_mul_xi(y)));
     const Fq2 s0 = f2_sub(f2_sub(u, t), f2_mul_xi(t));
     const Fq2 t2 = f2_dbl(t);
     const Fq2 s1 = k == 1 ? f2_mul_xi(t2) : t2;
@@ -88,7 +88,7 @@ template <int J>
 EON_HD Fq2 tm_frob(const Fq2& a, int k) {
     const Fq2 c = (J & 1) ? f2_conj(a) : a;
     const auto& tab = J == 1 ? pc::FROB1 : J == 2 ? pc::FROB2 : pc::FROB3;
-    return f2_mul(c, f2_c(tab[k]));
+    return f2_mul_inl(c, f2_c(tab[k]));
 }
 
 // coefficient k of a^(q^6): w -> -w

@@ -94,7 +94,9 @@ struct CodeBlock {
     Instr i[CODE_BLOCK];
 };
 
-#ifdef EON_AIR_OLD_BODY  // A/B of round 4: the four slots unrolled, a product per op kind
+// The four slots of a block are unrolled, each with its own product per op kind.  One shared body
+// (the slot's words picked by scalar selects, one product for MUL and ASSERT) measured slower,
+// 15.8 vs 14.8 ms for the Poseidon2-AIR at 2^18 rows (round 4, profiles/r04/s7): not kept.
 template <class RF>
 __device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, const Fr& alpha, Fr& acc, Fr& prev) {
     if (in.op == OP_NOP) return;
@@ -118,36 +120,6 @@ __device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, 
     prev = r;
     if (in.dst != NO_DST) rf.set(in.dst, r);
 }
-#else
-// One Montgomery product per instruction slot, shared by OP_MUL (x y) and OP_ASSERT (acc alpha,
-// the folder's Horner step): a slot with a product per op kind nearly doubles the kernel's code,
-// which the four unrolled slots of a block then push past the instruction cache.
-template <class RF>
-__device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, const Fr& alpha, Fr& acc, Fr& prev) {
-    if (in.op == OP_NOP) return;
-    const Fr x = fetch(in.a, rf, prev, w);
-    const bool is_assert = in.op == OP_ASSERT;
-    const bool binary = in.op == OP_MUL || in.op == OP_ADD || in.op == OP_SUB;
-    const Fr y = binary ? fetch(in.b, rf, prev, w) : Fr::zero();
-    Fr r;
-    if (in.op == OP_MUL || is_assert) {
-        r = mul(is_assert ? acc : x, is_assert ? alpha : y);
-        if (is_assert) {
-            acc = add(r, x);  // folder.rs:81-85, alpha powers reversed
-            return;
-        }
-    } else if (in.op == OP_ADD) {
-        r = add(x, y);
-    } else if (in.op == OP_SUB) {
-        r = sub(x, y);
-    } else {
-        r = neg(x);
-    }
-    prev = r;
-    if (in.dst != NO_DST) rf.set(in.dst, r);
-}
-
-#endif
 
 template <class RF>
 __device__ __forceinline__ void run_program(const CodeBlock* __restrict__ code, uint32_t n_blocks, RF& rf,
@@ -158,7 +130,6 @@ __device__ __forceinline__ void run_program(const CodeBlock* __restrict__ code, 
     for (uint32_t bk = 0; bk < n_blocks; bk++) {
         const CodeBlock cur = nx;
         if (bk + 1 < n_blocks) nx = code[bk + 1];  // in flight while this block runs
-#ifdef EON_AIR_OLD_BODY
 #pragma unroll
         for (uint32_t u = 0; u < CODE_BLOCK; u++) {
             const Instr in{(uint32_t)__builtin_amdgcn_readfirstlane(cur.i[u].op),
@@ -167,22 +138,6 @@ __device__ __forceinline__ void run_program(const CodeBlock* __restrict__ code, 
                            (uint32_t)__builtin_amdgcn_readfirstlane(cur.i[u].b)};
             exec1(in, rf, w, alpha, acc, prev);
         }
-#else
-        // one copy of the instruction body: the slot's words are picked from the block by scalar
-        // selects (a body per slot would quadruple the code past the instruction cache)
-#pragma unroll 1
-        for (uint32_t u = 0; u < CODE_BLOCK; u++) {
-            auto pick = [&](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-                return (uint32_t)__builtin_amdgcn_readfirstlane(u == 0 ? w0 : u == 1 ? w1 : u == 2 ? w2 : w3);
-            };
-            // uniform: every lane runs the same instruction, so the operand switch is scalar
-            const Instr in{pick(cur.i[0].op, cur.i[1].op, cur.i[2].op, cur.i[3].op),
-                           pick(cur.i[0].dst, cur.i[1].dst, cur.i[2].dst, cur.i[3].dst),
-                           pick(cur.i[0].a, cur.i[1].a, cur.i[2].a, cur.i[3].a),
-                           pick(cur.i[0].b, cur.i[1].b, cur.i[2].b, cur.i[3].b)};
-            exec1(in, rf, w, alpha, acc, prev);
-        }
-#endif
     }
 }
 

@@ -27,6 +27,7 @@
 #include <tuple>
 #include <vector>
 
+#include "field29.h"
 #include "quotient.h"
 
 using namespace eon;
@@ -34,6 +35,16 @@ using namespace eon;
 namespace {
 
 enum : uint32_t { OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_NEG = 3, OP_ASSERT = 4, OP_NOP = 5 };
+// op word: opcode (bits 0-3) | OP_RED (the result is brought below 2p by reduce_top29) | K << K_SHIFT
+// (OP_SUB / OP_NEG: the multiple of p added, at least the subtrahend's bound)
+constexpr uint32_t OP_MASK = 0xf, OP_RED = 0x10, K_SHIFT = 8;
+// Value bounds.  Every value is held in radix 2^29 as x 2^261 ("29-Montgomery", field29.h) with
+// normalised limbs and a value below B p, B tracked per value by the compiler: loaded leaves and
+// products B = 2, a sum B_a + B_b, a difference B_a + K.  A result whose bound would exceed B_MAX
+// is reduced in the same instruction (OP_RED: reduce_top29, B = 2), so every operand is below
+// B_MAX p and every product below B_MAX^2 = 144 p^2, inside mul29's 167 p^2; a reduced input is
+// below 2 B_MAX p = 24 p < 2^261.  The folder's accumulator stays below (2 + B_MAX) p.
+constexpr uint32_t B_MAX = 12;
 // operand = mode << 29 | index
 enum : uint32_t { M_REG = 0, M_LOCAL = 1, M_NEXT = 2, M_CONST = 3, M_FIRST = 4, M_LAST = 5, M_TRANS = 6, M_PREV = 7 };
 constexpr uint32_t IDX_MASK = (1u << 29) - 1;
@@ -43,22 +54,58 @@ struct Instr {
     uint32_t op, dst, a, b;
 };
 
-__device__ __forceinline__ Fr ld(const Fr* p) { return ld_pinned(p); }
+// K p in normalised 29-bit limbs for K <= B_MAX (OP_SUB / OP_NEG); K is uniform, so its row is
+// read with scalar loads
+struct KpTable {
+    uint32_t l[B_MAX + 1][9];
+    constexpr KpTable() : l{} {
+        for (uint32_t k = 0; k <= B_MAX; k++) {
+            uint64_t c = 0;
+            for (int i = 0; i < 9; i++) {
+                c += (uint64_t)R29<FrP>::P[i] * k;
+                l[k][i] = (uint32_t)(c & M29);
+                c >>= 29;
+            }
+        }
+    }
+};
+__device__ constexpr KpTable KP_TABLE{};
 
-// register file in LDS (LDS = true) or in a global buffer: two 16-byte planes per register
+// a - b + K p, normalised (b < K p; a, b normalised: the signed column sums stay inside int32)
+__device__ __forceinline__ F29 sub29_k(const F29& a, const F29& b, uint32_t k) {
+    const uint32_t* kp = KP_TABLE.l[k];
+    F29 r;
+    int32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        const int32_t t = (int32_t)(a.l[i] + kp[i]) - (int32_t)b.l[i] + c;
+        r.l[i] = (uint32_t)t & M29;
+        c = t >> 29;  // arithmetic: -1, 0 or 1
+    }
+    return r;
+}
+
+// a trace cell, constant or selector (canonical, x 2^256) as x 2^261 below 2p
+__device__ __forceinline__ F29 ld29(const Fr* p) { return shl5_to261<FrP>(ld_pinned(p)); }
+
+// register file in LDS or in a global buffer: 36 bytes per register in three planes (limbs 0-3
+// and 4-7 as 16-byte planes, limb 8 as a 4-byte one), conflict-free b128 / b32 accesses
 struct MemRegs {
-    uint4* base;
-    uint64_t stride;  // uint4 units between planes
-    __device__ __forceinline__ Fr get(uint32_t r) const {
+    uint4* base;     // plane j of register r at (2 r + j) stride
+    uint32_t* top;   // limb 8 of register r at r stride
+    uint64_t stride;
+    __device__ __forceinline__ F29 get(uint32_t r) const {
         const uint4 a = base[(uint64_t)(2 * r) * stride], b = base[(uint64_t)(2 * r + 1) * stride];
-        Fr x;
-        x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
-        x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+        F29 x;
+        x.l[0] = a.x; x.l[1] = a.y; x.l[2] = a.z; x.l[3] = a.w;
+        x.l[4] = b.x; x.l[5] = b.y; x.l[6] = b.z; x.l[7] = b.w;
+        x.l[8] = top[(uint64_t)r * stride];
         return x;
     }
-    __device__ __forceinline__ void set(uint32_t r, const Fr& x) {
-        base[(uint64_t)(2 * r) * stride] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
-        base[(uint64_t)(2 * r + 1) * stride] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+    __device__ __forceinline__ void set(uint32_t r, const F29& x) {
+        base[(uint64_t)(2 * r) * stride] = make_uint4(x.l[0], x.l[1], x.l[2], x.l[3]);
+        base[(uint64_t)(2 * r + 1) * stride] = make_uint4(x.l[4], x.l[5], x.l[6], x.l[7]);
+        top[(uint64_t)r * stride] = x.l[8];
     }
 };
 
@@ -71,16 +118,16 @@ struct Window {
 };
 
 template <class RF>
-__device__ __forceinline__ Fr fetch(uint32_t opnd, const RF& rf, const Fr& prev, const Window& w) {
+__device__ __forceinline__ F29 fetch(uint32_t opnd, const RF& rf, const F29& prev, const Window& w) {
     const uint32_t i = opnd & IDX_MASK;
     switch (opnd >> 29) {
         case M_REG: return rf.get(i);
-        case M_LOCAL: return ld(w.local + i);
-        case M_NEXT: return ld(w.next + i);
-        case M_CONST: return ld(w.table + i);
-        case M_FIRST: return ld(w.sels + w.row);
-        case M_LAST: return ld(w.sels + w.q + w.row);
-        case M_TRANS: return ld(w.sels + 2 * w.q + w.row);
+        case M_LOCAL: return ld29(w.local + i);
+        case M_NEXT: return ld29(w.next + i);
+        case M_CONST: return ld29(w.table + i);
+        case M_FIRST: return ld29(w.sels + w.row);
+        case M_LAST: return ld29(w.sels + w.q + w.row);
+        case M_TRANS: return ld29(w.sels + 2 * w.q + w.row);
         default: return prev;
     }
 }
@@ -98,24 +145,30 @@ struct CodeBlock {
 // (the slot's words picked by scalar selects, one product for MUL and ASSERT) measured slower,
 // 15.8 vs 14.8 ms for the Poseidon2-AIR at 2^18 rows (round 4, profiles/r04/s7): not kept.
 template <class RF>
-__device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, const Fr& alpha, Fr& acc, Fr& prev) {
-    if (in.op == OP_NOP) return;
-    const Fr x = fetch(in.a, rf, prev, w);
-    if (in.op == OP_ASSERT) {
-        acc = add(mul(acc, alpha), x);
+__device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, const F29& alpha, F29& acc,
+                                      F29& prev) {
+    const uint32_t opc = in.op & OP_MASK;
+    if (opc == OP_NOP) return;
+    const F29 x = fetch(in.a, rf, prev, w);
+    if (opc == OP_ASSERT) {
+        acc = add29_norm(mul29<FrP>(acc, alpha), x);  // folder.rs:81-85, alpha powers reversed
         return;
     }
-    Fr r;
-    if (in.op == OP_NEG) {
-        r = neg(x);
+    F29 r;
+    if (opc == OP_MUL) {
+        r = mul29<FrP>(x, fetch(in.b, rf, prev, w));
     } else {
-        const Fr y = fetch(in.b, rf, prev, w);
-        if (in.op == OP_MUL)
-            r = mul(x, y);
-        else if (in.op == OP_ADD)
-            r = add(x, y);
-        else
-            r = sub(x, y);
+        if (opc == OP_ADD) {
+            r = add29_norm(x, fetch(in.b, rf, prev, w));
+        } else if (opc == OP_SUB) {
+            r = sub29_k(x, fetch(in.b, rf, prev, w), in.op >> K_SHIFT);
+        } else {  // OP_NEG
+            F29 z;
+#pragma unroll
+            for (int i = 0; i < 9; i++) z.l[i] = 0;
+            r = sub29_k(z, x, in.op >> K_SHIFT);
+        }
+        if (in.op & OP_RED) r = reduce_top29<FrP>(r);
     }
     prev = r;
     if (in.dst != NO_DST) rf.set(in.dst, r);
@@ -123,29 +176,37 @@ __device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, 
 
 template <class RF>
 __device__ __forceinline__ void run_program(const CodeBlock* __restrict__ code, uint32_t n_blocks, RF& rf,
-                                            const Window& w, const Fr& alpha, Fr& acc) {
+                                            const Window& w, const F29& alpha, F29& acc) {
     if (n_blocks == 0) return;
-    Fr prev = Fr::zero();
+    F29 prev;
+#pragma unroll
+    for (int i = 0; i < 9; i++) prev.l[i] = 0;
     CodeBlock nx = code[0];
     for (uint32_t bk = 0; bk < n_blocks; bk++) {
         const CodeBlock cur = nx;
         if (bk + 1 < n_blocks) nx = code[bk + 1];  // in flight while this block runs
-#pragma unroll
-        for (uint32_t u = 0; u < CODE_BLOCK; u++) {
-            const Instr in{(uint32_t)__builtin_amdgcn_readfirstlane(cur.i[u].op),
-                           (uint32_t)__builtin_amdgcn_readfirstlane(cur.i[u].dst),
-                           (uint32_t)__builtin_amdgcn_readfirstlane(cur.i[u].a),
-                           (uint32_t)__builtin_amdgcn_readfirstlane(cur.i[u].b)};
+        // the four slots written out: a loop over them is left rolled by the compiler at this body
+        // size, and the block then goes through scratch to be indexed
+        auto slot = [&](const Instr& raw) __attribute__((always_inline)) {
+            const Instr in{(uint32_t)__builtin_amdgcn_readfirstlane(raw.op),
+                           (uint32_t)__builtin_amdgcn_readfirstlane(raw.dst),
+                           (uint32_t)__builtin_amdgcn_readfirstlane(raw.a),
+                           (uint32_t)__builtin_amdgcn_readfirstlane(raw.b)};
             exec1(in, rf, w, alpha, acc, prev);
-        }
+        };
+        static_assert(CODE_BLOCK == 4, "four slots below");
+        slot(cur.i[0]);
+        slot(cur.i[1]);
+        slot(cur.i[2]);
+        slot(cur.i[3]);
     }
 }
 
-// MODE 0: registers in LDS; 1: in the global buffer `gregs`
+// MODE 0: registers in LDS; 1: in the global buffer `gregs` (n_regs 36-byte registers per row)
 template <int MODE>
 __global__ void __launch_bounds__(256) k_air_quotient(const CodeBlock* __restrict__ code, uint32_t n_blocks,
-                                                      const Fr* __restrict__ lde, uint32_t width, uint64_t q,
-                                                      uint64_t next_step, const Fr* __restrict__ table,
+                                                      uint32_t n_regs, const Fr* __restrict__ lde, uint32_t width,
+                                                      uint64_t q, uint64_t next_step, const Fr* __restrict__ table,
                                                       const Fr* __restrict__ sels, const Fr* __restrict__ inv_van,
                                                       uint32_t nr_mask, Fr alpha, Fr* __restrict__ out,
                                                       uint4* __restrict__ gregs) {
@@ -153,17 +214,24 @@ __global__ void __launch_bounds__(256) k_air_quotient(const CodeBlock* __restric
     const uint64_t row = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= q) return;
     Window w{lde + row * width, lde + ((row + next_step) & (q - 1)) * width, table, sels, row, q};
-    Fr acc = Fr::zero();
+    F29 acc;
+#pragma unroll
+    for (int i = 0; i < 9; i++) acc.l[i] = 0;
     MemRegs rf;
     if (MODE == 0) {
         rf.base = lds_regs + threadIdx.x;
+        rf.top = reinterpret_cast<uint32_t*>(lds_regs + 2ull * n_regs * blockDim.x) + threadIdx.x;
         rf.stride = blockDim.x;
     } else {
         rf.base = gregs + row;
+        rf.top = reinterpret_cast<uint32_t*>(gregs + 2ull * n_regs * q) + row;
         rf.stride = q;
     }
-    run_program(code, n_blocks, rf, w, alpha, acc);
-    st_vec(out + row, mul(acc, ld(inv_van + (row & nr_mask))));  // prover.rs:699
+    run_program(code, n_blocks, rf, w, shl5_to261<FrP>(alpha), acc);
+    // acc (x 2^261, < (2 + B_MAX) p) times inv_vanishing in the ABI form: x 2^261 y 2^256 2^-261
+    // = x y 2^256 (prover.rs:699)
+    const F29 r = mul29<FrP>(acc, unpack29(ld_pinned(inv_van + (row & nr_mask))));
+    st_vec(out + row, pack29<FrP>(canon29<FrP>(r)));
 }
 
 }  // namespace
@@ -390,6 +458,9 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
             std::sort(free_regs.begin(), free_regs.end(), std::greater<uint32_t>());
         }
     };
+    // value bounds in multiples of p (see B_MAX): leaves and products 2, sums and differences
+    // add up, a result above B_MAX is reduced by its own instruction
+    std::vector<uint32_t> bound(nv, 2);
     for (size_t t = 0; t < items.size(); t++) {
         const Item& it = items[t];
         if (it.assert_) {
@@ -398,7 +469,22 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
             continue;
         }
         const Val& x = vals[it.v];
-        Instr in{x.op, 0, opnd(x.a), x.op == OP_NEG ? 0u : opnd(x.b)};
+        uint32_t op = x.op, b = 2;
+        if (x.op == OP_ADD) {
+            b = bound[x.a] + bound[x.b];
+        } else if (x.op == OP_SUB) {
+            op |= bound[x.b] << K_SHIFT;  // + K p with K = the subtrahend's bound
+            b = bound[x.a] + bound[x.b];
+        } else if (x.op == OP_NEG) {
+            op |= bound[x.a] << K_SHIFT;
+            b = bound[x.a];
+        }
+        if (b > B_MAX) {
+            op |= OP_RED;
+            b = 2;
+        }
+        bound[it.v] = b;
+        Instr in{op, 0, opnd(x.a), x.op == OP_NEG ? 0u : opnd(x.b)};
         release(x.a, t);
         if (x.op != OP_NEG && x.b != x.a) release(x.b, t);
         if (last[it.v] < 0) continue;  // never read (cannot happen for reachable values)
@@ -543,7 +629,7 @@ int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const e
             const char* e = getenv("EON_AIR_REGS");
             return e && std::string(e) == "global";
         }();
-        const uint64_t per_thread = (uint64_t)prog->n_regs * sizeof(Fr);
+        const uint64_t per_thread = (uint64_t)prog->n_regs * 36;  // MemRegs: 36 bytes per register
         uint32_t block = 256;
         while (block > 64 && block * per_thread > 64 * 1024) block /= 2;
         const int mode = !force_global && block * per_thread <= 160 * 1024 ? 0 : 1;
@@ -555,26 +641,26 @@ int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const e
         // constraint (ASSERT) and the final inv_vanishing product (additions, subtractions and
         // negations are not products)
         uint64_t products = 1;
-        for (const Instr& in : prog->code) products += (in.op == OP_MUL || in.op == OP_ASSERT) ? 1 : 0;
+        for (const Instr& in : prog->code) {
+            const uint32_t opc = in.op & OP_MASK;
+            products += (opc == OP_MUL || opc == OP_ASSERT) ? 1 : 0;
+        }
         ctx->prof.begin("k_air_quotient", q * (uint64_t)prog->width * 32 + q * 32, ctx->stream, q * products);
         const CodeBlock* code = prog->d_code.as<CodeBlock>();
         const uint32_t n_blocks = (uint32_t)((prog->code.size() + CODE_BLOCK - 1) / CODE_BLOCK);
         const Fr* lde_f = reinterpret_cast<const Fr*>(lde);
         const Fr* sel = prog->uses_sels ? prog->d_sels.as<Fr>() : nullptr;
         Fr* out_f = reinterpret_cast<Fr*>(out);
-        if (mode == 0) {
-            // per launch: the attribute is per device, and this context's device may differ from
-            // the one another context set it on
-            EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_air_quotient<0>),
+        using KernelFn = void (*)(const CodeBlock*, uint32_t, uint32_t, const Fr*, uint32_t, uint64_t, uint64_t,
+                                  const Fr*, const Fr*, const Fr*, uint32_t, Fr, Fr*, uint4*);
+        const KernelFn kern = mode == 0 ? k_air_quotient<0> : k_air_quotient<1>;
+        if (mode == 0)  // per launch: the attribute is per device, and this context's device may
+                        // differ from the one another context set it on
+            EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            hipLaunchKernelGGL(k_air_quotient<0>, dim3(grid), dim3(block), shmem, ctx->stream, code, n_blocks, lde_f,
-                               prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(), sel, inv_van, nr_mask, al, out_f,
-                               nullptr);
-        } else {
-            hipLaunchKernelGGL(k_air_quotient<1>, dim3(grid), dim3(block), 0, ctx->stream, code, n_blocks, lde_f,
-                               prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(), sel, inv_van, nr_mask, al, out_f,
-                               prog->d_regs.as<uint4>());
-        }
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(block), shmem, ctx->stream, code, n_blocks, prog->n_regs, lde_f,
+                           prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(), sel, inv_van, nr_mask, al, out_f,
+                           mode == 1 ? prog->d_regs.as<uint4>() : nullptr);
         ctx->prof.end(ctx->stream);
         EON_HIP(hipGetLastError());
         return Status::ok();

@@ -418,6 +418,23 @@ EON_HD F29 reduce_top29(const F29& a) {
     return r;
 }
 
+// canonical x 2^256 (the radix-2^32 ABI form, < p) -> x 2^261 in 29-bit limbs, < 2p: the bits of
+// 32 (x 2^256) (an integer < 2^259) re-split at offset -5, then one reduce_top29 step -- about a
+// quarter of the Montgomery product by 2^266 that to261 costs
+template <class M>
+EON_HD F29 shl5_to261(const Fe<M>& a) {
+    F29 r;
+    r.l[0] = (a.v[0] << 5) & M29;
+#pragma unroll
+    for (int i = 1; i < 9; i++) {
+        const int bit = 29 * i - 5, w = bit >> 5, s = bit & 31;
+        uint64_t v = a.v[w];
+        if (w + 1 < 8) v |= (uint64_t)a.v[w + 1] << 32;
+        r.l[i] = (uint32_t)(v >> s) & M29;
+    }
+    return reduce_top29<M>(r);
+}
+
 // a^2 2^-261 mod p (limbs < 2^30, a^2 < 0.99 p 2^261, as mul29): each column's cross products
 // once, summed apart and doubled by a shift (45 instead of 81 limb products; cross sums < 2^62)
 template <class M, int U = 8>

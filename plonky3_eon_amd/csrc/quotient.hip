@@ -13,6 +13,7 @@
 // combined as sum_v P_v * alpha^(160 * (VL - 1 - v)) through LDS.
 #include <cstring>
 
+#include "field29.h"
 #include "quotient.h"
 #include <vector>
 
@@ -99,39 +100,68 @@ __global__ void k_p2_trace(const Fr* inputs, uint64_t n, P2Args a, Fr* trace) {
     }
 }
 
-// Horner fold of one permutation's 160 constraints, in air.rs assert order
-__device__ Fr p2_fold(const Fr* c, const P2Args& a, const Fr& alpha) {
-    Fr acc = Fr::zero();
-    Fr s[3] = {ldg(c + 1), ldg(c + 2), ldg(c + 3)};
+// Horner fold of one permutation's 160 constraints, in air.rs assert order, in radix-2^29
+// arithmetic (field29.h: 162-multiply-add carry-free products instead of the radix-2^32 product's
+// multiply-adds with carry captures).  Values are held as x 2^261 ("29-Montgomery"): trace cells
+// and round constants are converted on load (shl5_to261, < 2p), alpha arrives converted.  Bounds
+// (multiples of p; mul29 takes any a b < 167 p^2 and returns < 2p): loaded values and products
+// < 2p; an external layer takes inputs < 2p to outputs < 8p; S-box input s + rc < 9p (or < 11p at
+// the partial round after an internal layer); a constraint value x3 - x^3 + 2p, y - post + 2p < 4p
+// and s - post + 2p < 10p; so acc = acc alpha + C < 12p and acc alpha is a < 24 p^2 product.  The
+// internal layer's s1, s2 are reduced (reduce_top29) every round: they are never reloaded.
+__device__ __forceinline__ F29 ld29(const Fr* p) { return shl5_to261<FrP>(ldg(p)); }
+
+__device__ __forceinline__ void p2_ext29(F29* s) {
+    const F29 t = add29_norm(add29_norm(s[0], s[1]), s[2]);
+    s[0] = add29_norm(s[0], t);
+    s[1] = add29_norm(s[1], t);
+    s[2] = add29_norm(s[2], t);
+}
+
+__device__ __forceinline__ void p2_int29(F29* s) {
+    const F29 t = add29_norm(s[0], add29_norm(s[1], s[2]));
+    s[0] = add29_norm(s[0], t);
+    s[1] = reduce_top29<FrP>(add29_norm(s[1], t));
+    s[2] = reduce_top29<FrP>(add29_norm(add29_norm(s[2], s[2]), t));
+}
+
+__device__ __forceinline__ void horner29(F29& acc, const F29& alpha, const F29& c) {
+    acc = add29_norm(mul29<FrP>(acc, alpha), c);
+}
+
+__device__ F29 p2_fold29(const Fr* c, const P2Args& a, const F29& alpha) {
+    F29 acc;
+#pragma unroll
+    for (int i = 0; i < 9; i++) acc.l[i] = 0;
+    F29 s[3] = {ld29(c + 1), ld29(c + 2), ld29(c + 3)};
     uint32_t k = 4;
-    p2_ext(s);
+    p2_ext29(s);
     for (uint32_t half = 0; half < 2; half++) {
         if (half == 1) {
             for (uint32_t r = 0; r < a.pr; r++) {
-                s[0] = add(s[0], ldg(a.partial + r));
-                const Fr x3 = ldg(c + k), post = ldg(c + k + 1);
+                const F29 x = add29_norm(s[0], ld29(a.partial + r));
+                const F29 x3 = ld29(c + k), post = ld29(c + k + 1);
                 k += 2;
-                const Fr x2 = sqr(s[0]);
-                acc = add(mul(acc, alpha), sub(x3, mul(x2, s[0])));  // assert_eq(x3, x2 * x)
-                s[0] = mul(x3, x2);
-                acc = add(mul(acc, alpha), sub(s[0], post));  // assert_eq(state[0], post_sbox)
+                const F29 x2 = sqr29<FrP>(x);
+                horner29(acc, alpha, sub29<FrP, 2>(x3, mul29<FrP>(x2, x)));  // assert_eq(x3, x2 * x)
+                horner29(acc, alpha, sub29<FrP, 2>(mul29<FrP>(x3, x2), post));  // assert_eq(state[0], post_sbox)
                 s[0] = post;
-                p2_int(s);
+                p2_int29(s);
             }
         }
         const Fr* rc = half == 0 ? a.begin : a.end;
         for (uint32_t r = 0; r < a.hf; r++) {
             for (int i = 0; i < 3; i++) {
-                s[i] = add(s[i], ldg(rc + 3 * r + i));
-                const Fr x3 = ldg(c + k + i);
-                const Fr x2 = sqr(s[i]);
-                acc = add(mul(acc, alpha), sub(x3, mul(x2, s[i])));
-                s[i] = mul(x3, x2);
+                const F29 x = add29_norm(s[i], ld29(rc + 3 * r + i));
+                const F29 x3 = ld29(c + k + i);
+                const F29 x2 = sqr29<FrP>(x);
+                horner29(acc, alpha, sub29<FrP, 2>(x3, mul29<FrP>(x2, x)));
+                s[i] = mul29<FrP>(x3, x2);
             }
-            p2_ext(s);
+            p2_ext29(s);
             for (int i = 0; i < 3; i++) {
-                const Fr post = ldg(c + k + 3 + i);
-                acc = add(mul(acc, alpha), sub(s[i], post));  // assert_eq(state_i, post_i)
+                const F29 post = ld29(c + k + 3 + i);
+                horner29(acc, alpha, sub29<FrP, 2>(s[i], post));  // assert_eq(state_i, post_i)
                 s[i] = post;
             }
             k += 6;
@@ -155,15 +185,19 @@ __global__ void __launch_bounds__(256) k_p2_quotient(const Fr* lde, uint64_t q, 
     Fr p = Fr::zero();
     if (row < q) {
         const Fr* c = lde + row * (uint64_t)a.ncols * a.vl + (uint64_t)v * a.ncols;
-        p = p2_fold(c, a, alpha);
-        if (a.vl > 1) p = mul(p, lane_pow.v[v]);
+        F29 acc = p2_fold29(c, a, shl5_to261<FrP>(alpha));
+        // the lane's share times its alpha power (29-Montgomery), then times inv_vanishing in the
+        // ABI form: mul29 of x 2^261 and y 2^256 is x y 2^256 (prover.rs:699)
+        if (a.vl > 1) acc = mul29<FrP>(acc, shl5_to261<FrP>(lane_pow.v[v]));
+        const F29 iv = unpack29(ldg(inv_van + (row & nr_mask)));
+        p = pack29<FrP>(canon29<FrP>(mul29<FrP>(acc, iv)));
     }
     part[threadIdx.x] = p;
     __syncthreads();
     if (v == 0 && row < q) {
         Fr acc = part[threadIdx.x];
         for (uint32_t u = 1; u < a.vl; u++) acc = add(acc, part[threadIdx.x + u]);
-        stg(out + row, mul(acc, ldg(inv_van + (row & nr_mask))));
+        stg(out + row, acc);
     }
 }
 
@@ -417,7 +451,12 @@ int eon_p2air_quotient_values_dev(eon_ctx* ctx, const eon_p2air* air, const eon_
         }
         const uint64_t q = 1ull << log_q;
         const uint64_t threads = q * a.vl;
-        ctx->prof.begin("k_p2_quotient", q * (uint64_t)a.ncols * a.vl * 32 + q * 32, ctx->stream);
+        // algorithmic 256-bit products per (row, lane): per partial round x^2, x^2 x, x3 x^2 and two
+        // Horner steps; per full-round S-box x^2, x^2 x, x3 x^2 and one Horner step, plus one per
+        // post-state constraint; the lane power and inv_vanishing
+        const uint64_t lane_products = 5ull * a.pr + 2ull * a.hf * 3 * 4 + 2ull * a.hf * 3 + 2;
+        ctx->prof.begin("k_p2_quotient", q * (uint64_t)a.ncols * a.vl * 32 + q * 32, ctx->stream,
+                        q * a.vl * lane_products);
         hipLaunchKernelGGL(k_p2_quotient, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                            ctx->stream, reinterpret_cast<const Fr*>(lde), q, a, al, lp, zh_inv,
                            (1u << log_qd) - 1,

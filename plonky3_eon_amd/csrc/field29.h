@@ -418,11 +418,12 @@ EON_HD F29 reduce_top29(const F29& a) {
     return r;
 }
 
-// canonical x 2^256 (the radix-2^32 ABI form, < p) -> x 2^261 in 29-bit limbs, < 2p: the bits of
-// 32 (x 2^256) (an integer < 2^259) re-split at offset -5, then one reduce_top29 step -- about a
-// quarter of the Montgomery product by 2^266 that to261 costs
+// canonical x 2^256 (the radix-2^32 ABI form, < p) -> x 2^261 in 29-bit limbs: the bits of
+// 32 (x 2^256) re-split at offset -5, an integer < 2^259 < 32p (shl5_raw, normalised limbs), or
+// brought below 2p by one reduce_top29 step (shl5_to261) -- about a quarter of the Montgomery
+// product by 2^266 that to261 costs
 template <class M>
-EON_HD F29 shl5_to261(const Fe<M>& a) {
+EON_HD F29 shl5_raw(const Fe<M>& a) {
     F29 r;
     r.l[0] = (a.v[0] << 5) & M29;
 #pragma unroll
@@ -432,7 +433,12 @@ EON_HD F29 shl5_to261(const Fe<M>& a) {
         if (w + 1 < 8) v |= (uint64_t)a.v[w + 1] << 32;
         r.l[i] = (uint32_t)(v >> s) & M29;
     }
-    return reduce_top29<M>(r);
+    return r;
+}
+
+template <class M>
+EON_HD F29 shl5_to261(const Fe<M>& a) {
+    return reduce_top29<M>(shl5_raw(a));
 }
 
 // a^2 2^-261 mod p (limbs < 2^30, a^2 < 0.99 p 2^261, as mul29): each column's cross products

@@ -101,7 +101,10 @@ __global__ void k_eval_block(const Fr* c, uint64_t n, uint32_t width, PtsShoup z
     const uint32_t col = (uint32_t)(t % width);
     const uint64_t b = t / width;
     const uint64_t lo = b * BL, hi = lo + BL < n ? lo + BL : n;
+    // r[] indexed only by unrolled loops, so it stays in registers (a rolled loop over it kept it in
+    // scratch, read and written every coefficient)
     F29 r[MAX_PTS];
+#pragma unroll
     for (uint32_t p = 0; p < MAX_PTS; p++) r[p] = unpack29(Fr::zero());
     for (uint64_t i = hi; i-- > lo;) {
         const F29 x = unpack29(ld(c + i * width + col));  // canonical
@@ -109,8 +112,10 @@ __global__ void k_eval_block(const Fr* c, uint64_t n, uint32_t width, PtsShoup z
         for (uint32_t p = 0; p < MAX_PTS; p++)
             if (p < np) r[p] = add29_norm(x, mul29_shoup<FrP>(r[p], zs.w[p], zs.q[p]));  // < p + 3p
     }
-    for (uint32_t p = 0; p < np; p++)
-        st(totals + ((uint64_t)p * nblk + b) * width + col, pack29<FrP>(canon29<FrP>(reduce_top29<FrP>(r[p]))));
+#pragma unroll
+    for (uint32_t p = 0; p < MAX_PTS; p++)
+        if (p < np)
+            st(totals + ((uint64_t)p * nblk + b) * width + col, pack29<FrP>(canon29<FrP>(reduce_top29<FrP>(r[p]))));
 }
 
 // per (point, chunk of CH blocks, column): P_q = sum_{b in chunk} T_b Z^(b - q CH)

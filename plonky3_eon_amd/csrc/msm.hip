@@ -303,15 +303,24 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
             // one flush site (the run's end or the chunk's), so the checked re-sum is emitted once
             const bool last = e == e1;
 #ifndef EON_PIECE_SCALAR_PAIRS
-            const uint32_t sub = e & 3;
-            if (vec && !last && sub == 0) {
-                kq = *reinterpret_cast<const uint4*>(keys + e);
-                vq = *reinterpret_cast<const uint4*>(vals + e);
+            // the pair is always picked from the register quads (a chunk cut short reloads
+            // component 0 every pair): a pick written as "vec ? quad component : *p" was compiled
+            // as one load through a selected pointer, which kept the quads in scratch (eight
+            // scratch stores per quad, a flat load and a wait per pair)
+            const uint32_t sub = vec ? (e & 3) : 0;
+            if (!last && sub == 0) {
+                if (vec) {
+                    kq = *reinterpret_cast<const uint4*>(keys + e);
+                    vq = *reinterpret_cast<const uint4*>(vals + e);
+                } else {
+                    kq.x = keys[e];
+                    vq.x = vals[e];
+                }
             }
-            auto pick = [&](const uint4& q, const uint32_t* p) __attribute__((always_inline)) {
-                return vec ? (sub == 0 ? q.x : sub == 1 ? q.y : sub == 2 ? q.z : q.w) : *p;
+            auto pick = [&](const uint4& q) __attribute__((always_inline)) {
+                return sub == 0 ? q.x : sub == 1 ? q.y : sub == 2 ? q.z : q.w;
             };
-            const uint32_t k = last ? b : pick(kq, keys + e);
+            const uint32_t k = last ? b : pick(kq);
 #else
             const uint32_t k = last ? b : keys[e];
 #endif
@@ -323,7 +332,7 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
                 run = e;
             }
 #ifndef EON_PIECE_SCALAR_PAIRS
-            const uint32_t v = pick(vq, vals + e);
+            const uint32_t v = pick(vq);
 #else
             const uint32_t v = vals[e];
 #endif

@@ -22,7 +22,8 @@ using namespace eon;
 struct eon_p2air {
     eon_ctx* ctx = nullptr;
     uint32_t hf = 0, pr = 0, vl = 0;
-    DevBuf consts;  // begin (hf*3), partial (pr), end (hf*3)
+    DevBuf consts;    // begin (hf*3), partial (pr), end (hf*3)
+    DevBuf consts29;  // the same as x 2^261 in 29-bit limbs, < 2p (the quotient fold's operands)
 };
 
 namespace eon {
@@ -31,6 +32,9 @@ struct P2Args {
     const Fr* begin;
     const Fr* partial;
     const Fr* end;
+    const F29* begin29;  // the round constants as the quotient fold uses them (eon_p2air::consts29)
+    const F29* partial29;
+    const F29* end29;
     uint32_t hf, pr, vl, ncols;  // ncols = columns of one permutation
 };
 
@@ -87,6 +91,7 @@ __global__ void k_p2_trace(const Fr* inputs, uint64_t n, P2Args a, Fr* trace) {
         }
         const Fr* rc = half == 0 ? a.begin : a.end;
         for (uint32_t r = 0; r < a.hf; r++) {
+#pragma unroll
             for (int i = 0; i < 3; i++) {
                 s[i] = add(s[i], ldg(rc + 3 * r + i));
                 const Fr x2 = sqr(s[i]);
@@ -103,13 +108,16 @@ __global__ void k_p2_trace(const Fr* inputs, uint64_t n, P2Args a, Fr* trace) {
 // Horner fold of one permutation's 160 constraints, in air.rs assert order, in radix-2^29
 // arithmetic (field29.h: 162-multiply-add carry-free products instead of the radix-2^32 product's
 // multiply-adds with carry captures).  Values are held as x 2^261 ("29-Montgomery"): trace cells
-// and round constants are converted on load (shl5_to261, < 2p), alpha arrives converted.  Bounds
+// are converted on load (shl5_to261, < 2p), alpha and the round constants arrive converted.  Bounds
 // (multiples of p; mul29 takes any a b < 167 p^2 and returns < 2p): loaded values and products
 // < 2p; an external layer takes inputs < 2p to outputs < 8p; S-box input s + rc < 9p (or < 11p at
 // the partial round after an internal layer); a constraint value x3 - x^3 + 2p, y - post + 2p < 4p
-// and s - post + 2p < 10p; so acc = acc alpha + C < 12p and acc alpha is a < 24 p^2 product.  The
-// internal layer's s1, s2 are reduced (reduce_top29) every round: they are never reloaded.
+// and s - post + 2p < 10p.  The committed x^3 cells skip the reduction (shl5_raw, < 32p): they only
+// enter x3 - x^3 + 2p (< 34p) and x3 x^2 (< 64 p^2).  So acc = acc alpha + C < 36p and acc alpha
+// is a < 72 p^2 product.  The internal layer's s1, s2 are reduced (reduce_top29) every round: they
+// are never reloaded.  Round constants come pre-converted (P2Args::*29).
 __device__ __forceinline__ F29 ld29(const Fr* p) { return shl5_to261<FrP>(ldg(p)); }
+__device__ __forceinline__ F29 ld29_raw(const Fr* p) { return shl5_raw<FrP>(ldg(p)); }
 
 __device__ __forceinline__ void p2_ext29(F29* s) {
     const F29 t = add29_norm(add29_norm(s[0], s[1]), s[2]);
@@ -139,8 +147,8 @@ __device__ F29 p2_fold29(const Fr* c, const P2Args& a, const F29& alpha) {
     for (uint32_t half = 0; half < 2; half++) {
         if (half == 1) {
             for (uint32_t r = 0; r < a.pr; r++) {
-                const F29 x = add29_norm(s[0], ld29(a.partial + r));
-                const F29 x3 = ld29(c + k), post = ld29(c + k + 1);
+                const F29 x = add29_norm(s[0], a.partial29[r]);
+                const F29 x3 = ld29_raw(c + k), post = ld29(c + k + 1);
                 k += 2;
                 const F29 x2 = sqr29<FrP>(x);
                 horner29(acc, alpha, sub29<FrP, 2>(x3, mul29<FrP>(x2, x)));  // assert_eq(x3, x2 * x)
@@ -149,16 +157,18 @@ __device__ F29 p2_fold29(const Fr* c, const P2Args& a, const F29& alpha) {
                 p2_int29(s);
             }
         }
-        const Fr* rc = half == 0 ? a.begin : a.end;
+        const F29* rc = half == 0 ? a.begin29 : a.end29;
         for (uint32_t r = 0; r < a.hf; r++) {
+#pragma unroll
             for (int i = 0; i < 3; i++) {
-                const F29 x = add29_norm(s[i], ld29(rc + 3 * r + i));
-                const F29 x3 = ld29(c + k + i);
+                const F29 x = add29_norm(s[i], rc[3 * r + i]);
+                const F29 x3 = ld29_raw(c + k + i);
                 const F29 x2 = sqr29<FrP>(x);
                 horner29(acc, alpha, sub29<FrP, 2>(x3, mul29<FrP>(x2, x)));
                 s[i] = mul29<FrP>(x3, x2);
             }
             p2_ext29(s);
+#pragma unroll
             for (int i = 0; i < 3; i++) {
                 const F29 post = ld29(c + k + 3 + i);
                 horner29(acc, alpha, sub29<FrP, 2>(s[i], post));  // assert_eq(state_i, post_i)
@@ -320,6 +330,10 @@ P2Args p2_args(const eon_p2air* air) {
     a.begin = base;
     a.partial = base + 3 * air->hf;
     a.end = base + 3 * air->hf + air->pr;
+    const F29* b29 = air->consts29.as<F29>();
+    a.begin29 = b29;
+    a.partial29 = b29 + 3 * air->hf;
+    a.end29 = b29 + 3 * air->hf + air->pr;
     a.hf = air->hf;
     a.pr = air->pr;
     a.vl = air->vl;
@@ -371,10 +385,15 @@ int eon_p2air_create(eon_ctx* ctx, const eon_poseidon2_constants* k, uint32_t ve
         air->hf = hf;
         air->pr = pr;
         air->vl = vector_len;
+        std::vector<F29> host29(n);
+        for (uint64_t i = 0; i < n; i++) host29[i] = shl5_to261<FrP>(host[i]);
         hipError_t e = air->consts.ensure((n ? n : 1) * sizeof(Fr));
         if (e == hipSuccess && n) e = hipMemcpy(air->consts.p, host.data(), n * sizeof(Fr), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = air->consts29.ensure((n ? n : 1) * sizeof(F29));
+        if (e == hipSuccess && n) e = hipMemcpy(air->consts29.p, host29.data(), n * sizeof(F29), hipMemcpyHostToDevice);
         if (e != hipSuccess) {
             air->consts.release();
+            air->consts29.release();
             delete air;
             EON_HIP(e);
         }
@@ -390,6 +409,7 @@ void eon_p2air_destroy(eon_p2air* air) {
     (void)hipSetDevice(air->ctx->device);
     (void)hipStreamSynchronize(air->ctx->stream);
     air->consts.release();
+    air->consts29.release();
     delete air;
 }
 

@@ -45,6 +45,13 @@ constexpr uint32_t OP_MASK = 0xf, OP_RED = 0x10, K_SHIFT = 8;
 // B_MAX p and every product below B_MAX^2 = 144 p^2, inside mul29's 167 p^2; a reduced input is
 // below 2 B_MAX p = 24 p < 2^261.  The folder's accumulator stays below (2 + B_MAX) p.
 constexpr uint32_t B_MAX = 12;
+// Registers 0 and 1 -- the busiest: the allocator hands out the lowest free register -- are held in
+// VGPRs, the others in LDS (36 bytes each, MemRegs).  At the Poseidon2-AIR's 5 registers and 256
+// threads per block that is 27 KB of LDS per block instead of 45, so occupancy is set by the VGPRs
+// (4 waves per SIMD) instead of the LDS (3).  Measured (round 4, profiles/r04/s13): all registers
+// in LDS 15.6 ms, one in VGPRs 13.6, two 12.9; three spill; 64- or 128-thread blocks and a
+// 5-wave launch bound (spills) are slower or equal.
+constexpr uint32_t AIR_VREGS = 2, AIR_BLOCK = 256;
 // operand = mode << 29 | index
 enum : uint32_t { M_REG = 0, M_LOCAL = 1, M_NEXT = 2, M_CONST = 3, M_FIRST = 4, M_LAST = 5, M_TRANS = 6, M_PREV = 7 };
 constexpr uint32_t IDX_MASK = (1u << 29) - 1;
@@ -117,11 +124,48 @@ struct Window {
     uint64_t row, q;
 };
 
+// the registers held in VGPRs: register j < AIR_VREGS is hj (named values, not an array: an array
+// indexed by the register number went to scratch); the register number is uniform, so the choice
+// is a scalar branch
+static_assert(AIR_VREGS <= 4, "at most four registers in VGPRs");
+struct Hot {
+    F29 h0, h1, h2, h3;
+};
+__device__ __forceinline__ bool hot_get(const Hot& h, uint32_t i, F29& x) {
+    if (i >= AIR_VREGS) return false;
+    // limb-wise value selects (a branch per register was merged into a load through a selected
+    // pointer, which put the registers in scratch)
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        uint32_t v = h.h0.l[k];
+        if (AIR_VREGS > 1) v = i == 1 ? h.h1.l[k] : v;
+        if (AIR_VREGS > 2) v = i == 2 ? h.h2.l[k] : v;
+        if (AIR_VREGS > 3) v = i == 3 ? h.h3.l[k] : v;
+        x.l[k] = v;
+    }
+    return true;
+}
+__device__ __forceinline__ bool hot_set(Hot& h, uint32_t i, const F29& x) {
+    if (i >= AIR_VREGS) return false;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        h.h0.l[k] = i == 0 ? x.l[k] : h.h0.l[k];
+        if (AIR_VREGS > 1) h.h1.l[k] = i == 1 ? x.l[k] : h.h1.l[k];
+        if (AIR_VREGS > 2) h.h2.l[k] = i == 2 ? x.l[k] : h.h2.l[k];
+        if (AIR_VREGS > 3) h.h3.l[k] = i == 3 ? x.l[k] : h.h3.l[k];
+    }
+    return true;
+}
+
 template <class RF>
-__device__ __forceinline__ F29 fetch(uint32_t opnd, const RF& rf, const F29& prev, const Window& w) {
+__device__ __forceinline__ F29 fetch(uint32_t opnd, const RF& rf, const F29& prev, const Hot& hot, const Window& w) {
     const uint32_t i = opnd & IDX_MASK;
     switch (opnd >> 29) {
-        case M_REG: return rf.get(i);
+        case M_REG: {
+            F29 x;
+            if (hot_get(hot, i, x)) return x;
+            return rf.get(i - AIR_VREGS);
+        }
         case M_LOCAL: return ld29(w.local + i);
         case M_NEXT: return ld29(w.next + i);
         case M_CONST: return ld29(w.table + i);
@@ -146,22 +190,22 @@ struct CodeBlock {
 // 15.8 vs 14.8 ms for the Poseidon2-AIR at 2^18 rows (round 4, profiles/r04/s7): not kept.
 template <class RF>
 __device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, const F29& alpha, F29& acc,
-                                      F29& prev) {
+                                      F29& prev, Hot& hot) {
     const uint32_t opc = in.op & OP_MASK;
     if (opc == OP_NOP) return;
-    const F29 x = fetch(in.a, rf, prev, w);
+    const F29 x = fetch(in.a, rf, prev, hot, w);
     if (opc == OP_ASSERT) {
         acc = add29_norm(mul29<FrP>(acc, alpha), x);  // folder.rs:81-85, alpha powers reversed
         return;
     }
     F29 r;
     if (opc == OP_MUL) {
-        r = mul29<FrP>(x, fetch(in.b, rf, prev, w));
+        r = mul29<FrP>(x, fetch(in.b, rf, prev, hot, w));
     } else {
         if (opc == OP_ADD) {
-            r = add29_norm(x, fetch(in.b, rf, prev, w));
+            r = add29_norm(x, fetch(in.b, rf, prev, hot, w));
         } else if (opc == OP_SUB) {
-            r = sub29_k(x, fetch(in.b, rf, prev, w), in.op >> K_SHIFT);
+            r = sub29_k(x, fetch(in.b, rf, prev, hot, w), in.op >> K_SHIFT);
         } else {  // OP_NEG
             F29 z;
 #pragma unroll
@@ -171,7 +215,8 @@ __device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, 
         if (in.op & OP_RED) r = reduce_top29<FrP>(r);
     }
     prev = r;
-    if (in.dst != NO_DST) rf.set(in.dst, r);
+    if (in.dst == NO_DST || hot_set(hot, in.dst, r)) return;
+    rf.set(in.dst - AIR_VREGS, r);
 }
 
 template <class RF>
@@ -179,8 +224,11 @@ __device__ __forceinline__ void run_program(const CodeBlock* __restrict__ code, 
                                             const Window& w, const F29& alpha, F29& acc) {
     if (n_blocks == 0) return;
     F29 prev;
+    Hot hot;
 #pragma unroll
     for (int i = 0; i < 9; i++) prev.l[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) hot.h0.l[i] = hot.h1.l[i] = hot.h2.l[i] = hot.h3.l[i] = 0;
     CodeBlock nx = code[0];
     for (uint32_t bk = 0; bk < n_blocks; bk++) {
         const CodeBlock cur = nx;
@@ -192,7 +240,7 @@ __device__ __forceinline__ void run_program(const CodeBlock* __restrict__ code, 
                            (uint32_t)__builtin_amdgcn_readfirstlane(raw.dst),
                            (uint32_t)__builtin_amdgcn_readfirstlane(raw.a),
                            (uint32_t)__builtin_amdgcn_readfirstlane(raw.b)};
-            exec1(in, rf, w, alpha, acc, prev);
+            exec1(in, rf, w, alpha, acc, prev, hot);
         };
         static_assert(CODE_BLOCK == 4, "four slots below");
         slot(cur.i[0]);
@@ -204,7 +252,7 @@ __device__ __forceinline__ void run_program(const CodeBlock* __restrict__ code, 
 
 // MODE 0: registers in LDS; 1: in the global buffer `gregs` (n_regs 36-byte registers per row)
 template <int MODE>
-__global__ void __launch_bounds__(256) k_air_quotient(const CodeBlock* __restrict__ code, uint32_t n_blocks,
+__global__ void __launch_bounds__(AIR_BLOCK) k_air_quotient(const CodeBlock* __restrict__ code, uint32_t n_blocks,
                                                       uint32_t n_regs, const Fr* __restrict__ lde, uint32_t width,
                                                       uint64_t q, uint64_t next_step, const Fr* __restrict__ table,
                                                       const Fr* __restrict__ sels, const Fr* __restrict__ inv_van,
@@ -217,14 +265,15 @@ __global__ void __launch_bounds__(256) k_air_quotient(const CodeBlock* __restric
     F29 acc;
 #pragma unroll
     for (int i = 0; i < 9; i++) acc.l[i] = 0;
+    const uint32_t n_mem = n_regs > AIR_VREGS ? n_regs - AIR_VREGS : 0;  // registers in memory
     MemRegs rf;
     if (MODE == 0) {
         rf.base = lds_regs + threadIdx.x;
-        rf.top = reinterpret_cast<uint32_t*>(lds_regs + 2ull * n_regs * blockDim.x) + threadIdx.x;
+        rf.top = reinterpret_cast<uint32_t*>(lds_regs + 2ull * n_mem * blockDim.x) + threadIdx.x;
         rf.stride = blockDim.x;
     } else {
         rf.base = gregs + row;
-        rf.top = reinterpret_cast<uint32_t*>(gregs + 2ull * n_regs * q) + row;
+        rf.top = reinterpret_cast<uint32_t*>(gregs + 2ull * n_mem * q) + row;
         rf.stride = q;
     }
     run_program(code, n_blocks, rf, w, shl5_to261<FrP>(alpha), acc);
@@ -629,11 +678,12 @@ int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const e
             const char* e = getenv("EON_AIR_REGS");
             return e && std::string(e) == "global";
         }();
-        const uint64_t per_thread = (uint64_t)prog->n_regs * 36;  // MemRegs: 36 bytes per register
-        uint32_t block = 256;
+        // MemRegs: 36 bytes per register in memory
+        const uint64_t per_thread = (uint64_t)(prog->n_regs > AIR_VREGS ? prog->n_regs - AIR_VREGS : 0) * 36;
+        uint32_t block = AIR_BLOCK;
         while (block > 64 && block * per_thread > 64 * 1024) block /= 2;
         const int mode = !force_global && block * per_thread <= 160 * 1024 ? 0 : 1;
-        if (mode != 0) block = 256;
+        if (mode != 0) block = AIR_BLOCK;
         if (mode == 1) EON_HIP(prog->d_regs.ensure(std::max<uint64_t>(1, q * per_thread)));
         const unsigned grid = (unsigned)((q + block - 1) / block);
         const size_t shmem = mode == 0 ? (size_t)block * per_thread : 0;

@@ -39,12 +39,18 @@ enum : uint32_t { OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_NEG = 3, OP_ASSERT = 4,
 // (OP_SUB / OP_NEG: the multiple of p added, at least the subtrahend's bound)
 constexpr uint32_t OP_MASK = 0xf, OP_RED = 0x10, K_SHIFT = 8;
 // Value bounds.  Every value is held in radix 2^29 as x 2^261 ("29-Montgomery", field29.h) with
-// normalised limbs and a value below B p, B tracked per value by the compiler: loaded leaves and
-// products B = 2, a sum B_a + B_b, a difference B_a + K.  A result whose bound would exceed B_MAX
-// is reduced in the same instruction (OP_RED: reduce_top29, B = 2), so every operand is below
-// B_MAX p and every product below B_MAX^2 = 144 p^2, inside mul29's 167 p^2; a reduced input is
-// below 2 B_MAX p = 24 p < 2^261.  The folder's accumulator stays below (2 + B_MAX) p.
+// normalised limbs and a value below B p, B tracked per value by the compiler: products B = 2, a
+// sum B_a + B_b, a difference B_a + K.  A result whose bound would exceed B_MAX is reduced in the
+// same instruction (OP_RED: reduce_top29, B = 2), so every computed operand is below B_MAX p; with
+// the raw leaves below (OPND_RAW) every product stays below 160 p^2, inside mul29's 167 p^2, and a
+// reduced input below 64 p < 2^261.  The folder's accumulator stays below (2 + B_RAW) p.
 constexpr uint32_t B_MAX = 12;
+// A leaf (trace cell, constant, selector) is loaded either reduced (shl5_to261, B = 2) or raw
+// (shl5_raw, B = 32: the reduction skipped) -- chosen per use by the compiler (OPND_RAW): raw
+// wherever the reader allows it (a sum or difference, whose result is reduced anyway when it
+// exceeds B_MAX, a constraint value, one side of a product whose other side is < 5p), so a
+// two-leaf sum costs one reduction instead of two.  The subtrahend multiple K then reaches 32.
+constexpr uint32_t B_RAW = 32, K_MAX = 32;
 // Registers 0 and 1 -- the busiest: the allocator hands out the lowest free register -- are held in
 // VGPRs, the others in LDS (36 bytes each, MemRegs).  At the Poseidon2-AIR's 5 registers and 256
 // threads per block that is 27 KB of LDS per block instead of 45, so occupancy is set by the VGPRs
@@ -54,19 +60,19 @@ constexpr uint32_t B_MAX = 12;
 constexpr uint32_t AIR_VREGS = 2, AIR_BLOCK = 256;
 // operand = mode << 29 | index
 enum : uint32_t { M_REG = 0, M_LOCAL = 1, M_NEXT = 2, M_CONST = 3, M_FIRST = 4, M_LAST = 5, M_TRANS = 6, M_PREV = 7 };
-constexpr uint32_t IDX_MASK = (1u << 29) - 1;
+constexpr uint32_t OPND_RAW = 1u << 28, IDX_MASK = (1u << 28) - 1;
 constexpr uint32_t NO_DST = ~0u;  // result only forwarded to the next instruction (M_PREV)
 
 struct Instr {
     uint32_t op, dst, a, b;
 };
 
-// K p in normalised 29-bit limbs for K <= B_MAX (OP_SUB / OP_NEG); K is uniform, so its row is
+// K p in normalised 29-bit limbs for K <= K_MAX (OP_SUB / OP_NEG); K is uniform, so its row is
 // read with scalar loads
 struct KpTable {
-    uint32_t l[B_MAX + 1][9];
+    uint32_t l[K_MAX + 1][9];
     constexpr KpTable() : l{} {
-        for (uint32_t k = 0; k <= B_MAX; k++) {
+        for (uint32_t k = 0; k <= K_MAX; k++) {
             uint64_t c = 0;
             for (int i = 0; i < 9; i++) {
                 c += (uint64_t)R29<FrP>::P[i] * k;
@@ -92,8 +98,12 @@ __device__ __forceinline__ F29 sub29_k(const F29& a, const F29& b, uint32_t k) {
     return r;
 }
 
-// a trace cell, constant or selector (canonical, x 2^256) as x 2^261 below 2p
-__device__ __forceinline__ F29 ld29(const Fr* p) { return shl5_to261<FrP>(ld_pinned(p)); }
+// a trace cell, constant or selector (canonical, x 2^256) as x 2^261: below 2p, or below 32p
+// unreduced when the operand is marked raw (the flag is uniform: a scalar branch)
+__device__ __forceinline__ F29 ld29(const Fr* p, bool raw) {
+    const F29 x = shl5_raw<FrP>(ld_pinned(p));
+    return raw ? x : reduce_top29<FrP>(x);
+}
 
 // register file in LDS or in a global buffer: 36 bytes per register in three planes (limbs 0-3
 // and 4-7 as 16-byte planes, limb 8 as a 4-byte one), conflict-free b128 / b32 accesses
@@ -160,18 +170,19 @@ __device__ __forceinline__ bool hot_set(Hot& h, uint32_t i, const F29& x) {
 template <class RF>
 __device__ __forceinline__ F29 fetch(uint32_t opnd, const RF& rf, const F29& prev, const Hot& hot, const Window& w) {
     const uint32_t i = opnd & IDX_MASK;
+    const bool raw = (opnd & OPND_RAW) != 0;
     switch (opnd >> 29) {
         case M_REG: {
             F29 x;
             if (hot_get(hot, i, x)) return x;
             return rf.get(i - AIR_VREGS);
         }
-        case M_LOCAL: return ld29(w.local + i);
-        case M_NEXT: return ld29(w.next + i);
-        case M_CONST: return ld29(w.table + i);
-        case M_FIRST: return ld29(w.sels + w.row);
-        case M_LAST: return ld29(w.sels + w.q + w.row);
-        case M_TRANS: return ld29(w.sels + 2 * w.q + w.row);
+        case M_LOCAL: return ld29(w.local + i, raw);
+        case M_NEXT: return ld29(w.next + i, raw);
+        case M_CONST: return ld29(w.table + i, raw);
+        case M_FIRST: return ld29(w.sels + w.row, raw);
+        case M_LAST: return ld29(w.sels + w.q + w.row, raw);
+        case M_TRANS: return ld29(w.sels + 2 * w.q + w.row, raw);
         default: return prev;
     }
 }
@@ -277,7 +288,7 @@ __global__ void __launch_bounds__(AIR_BLOCK) k_air_quotient(const CodeBlock* __r
         rf.stride = q;
     }
     run_program(code, n_blocks, rf, w, shl5_to261<FrP>(alpha), acc);
-    // acc (x 2^261, < (2 + B_MAX) p) times inv_vanishing in the ABI form: x 2^261 y 2^256 2^-261
+    // acc (x 2^261, < (2 + B_RAW) p) times inv_vanishing in the ABI form: x 2^261 y 2^256 2^-261
     // = x y 2^256 (prover.rs:699)
     const F29 r = mul29<FrP>(acc, unpack29(ld_pinned(inv_van + (row & nr_mask))));
     st_vec(out + row, pack29<FrP>(canon29<FrP>(r)));
@@ -507,33 +518,46 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
             std::sort(free_regs.begin(), free_regs.end(), std::greater<uint32_t>());
         }
     };
-    // value bounds in multiples of p (see B_MAX): leaves and products 2, sums and differences
-    // add up, a result above B_MAX is reduced by its own instruction
+    // value bounds in multiples of p (see B_MAX): products 2, leaves 2 or B_RAW as loaded, sums
+    // and differences add up, a result above B_MAX is reduced by its own instruction
     std::vector<uint32_t> bound(nv, 2);
+    auto is_leaf = [&](uint32_t v) { return vals[v].op == LEAF; };
     for (size_t t = 0; t < items.size(); t++) {
         const Item& it = items[t];
-        if (it.assert_) {
-            p->code.push_back({OP_ASSERT, 0, opnd(it.v), 0});
+        if (it.assert_) {  // acc alpha + x: acc < (2 + B_RAW) p, a < 68 p^2 product
+            p->code.push_back({OP_ASSERT, 0, opnd(it.v) | (is_leaf(it.v) ? OPND_RAW : 0u), 0});
             release(it.v, t);
             continue;
         }
         const Val& x = vals[it.v];
+        const bool unary = x.op == OP_NEG;
+        // per use: the leaf operands raw unless a product's other side is too wide for it
+        bool raw_a = is_leaf(x.a), raw_b = !unary && is_leaf(x.b);
+        if (x.op == OP_MUL) {
+            if (raw_a && raw_b)
+                raw_b = false;  // 32 x 2
+            else if (raw_a && bound[x.b] * B_RAW > 160)
+                raw_a = false;
+            else if (raw_b && bound[x.a] * B_RAW > 160)
+                raw_b = false;
+        }
+        const uint32_t ba = raw_a ? B_RAW : bound[x.a], bb = unary ? 0 : raw_b ? B_RAW : bound[x.b];
         uint32_t op = x.op, b = 2;
         if (x.op == OP_ADD) {
-            b = bound[x.a] + bound[x.b];
+            b = ba + bb;
         } else if (x.op == OP_SUB) {
-            op |= bound[x.b] << K_SHIFT;  // + K p with K = the subtrahend's bound
-            b = bound[x.a] + bound[x.b];
+            op |= bb << K_SHIFT;  // + K p with K = the subtrahend's bound
+            b = ba + bb;
         } else if (x.op == OP_NEG) {
-            op |= bound[x.a] << K_SHIFT;
-            b = bound[x.a];
+            op |= ba << K_SHIFT;
+            b = ba;
         }
         if (b > B_MAX) {
             op |= OP_RED;
             b = 2;
         }
         bound[it.v] = b;
-        Instr in{op, 0, opnd(x.a), x.op == OP_NEG ? 0u : opnd(x.b)};
+        Instr in{op, 0, opnd(x.a) | (raw_a ? OPND_RAW : 0u), unary ? 0u : opnd(x.b) | (raw_b ? OPND_RAW : 0u)};
         release(x.a, t);
         if (x.op != OP_NEG && x.b != x.a) release(x.b, t);
         if (last[it.v] < 0) continue;  // never read (cannot happen for reachable values)

@@ -133,8 +133,10 @@ __device__ __forceinline__ void p2_int29(F29* s) {
     s[2] = reduce_top29<FrP>(add29_norm(add29_norm(s[2], s[2]), t));
 }
 
+// acc alpha + c without carry propagation: both normalised, so the limbs stay < 2^30 -- what mul29
+// takes -- and acc only ever feeds a product (the next step, the lane power, inv_vanishing)
 __device__ __forceinline__ void horner29(F29& acc, const F29& alpha, const F29& c) {
-    acc = add29_norm(mul29<FrP>(acc, alpha), c);
+    acc = add29_lazy(mul29<FrP>(acc, alpha), c);
 }
 
 __device__ F29 p2_fold29(const Fr* c, const P2Args& a, const F29& alpha) {
@@ -147,7 +149,7 @@ __device__ F29 p2_fold29(const Fr* c, const P2Args& a, const F29& alpha) {
     for (uint32_t half = 0; half < 2; half++) {
         if (half == 1) {
             for (uint32_t r = 0; r < a.pr; r++) {
-                const F29 x = add29_norm(s[0], a.partial29[r]);
+                const F29 x = add29_lazy(s[0], a.partial29[r]);  // normalised + normalised: a product input
                 const F29 x3 = ld29_raw(c + k), post = ld29(c + k + 1);
                 k += 2;
                 const F29 x2 = sqr29<FrP>(x);
@@ -161,7 +163,7 @@ __device__ F29 p2_fold29(const Fr* c, const P2Args& a, const F29& alpha) {
         for (uint32_t r = 0; r < a.hf; r++) {
 #pragma unroll
             for (int i = 0; i < 3; i++) {
-                const F29 x = add29_norm(s[i], rc[3 * r + i]);
+                const F29 x = add29_lazy(s[i], rc[3 * r + i]);
                 const F29 x3 = ld29_raw(c + k + i);
                 const F29 x2 = sqr29<FrP>(x);
                 horner29(acc, alpha, sub29<FrP, 2>(x3, mul29<FrP>(x2, x)));

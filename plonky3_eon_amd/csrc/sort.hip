@@ -22,6 +22,7 @@
 #include "sort.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace eon {
 namespace {
@@ -120,11 +121,16 @@ __device__ __forceinline__ uint64_t ld_status(uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// DBITS > 0: the pass's digit width as a compile-time constant (the MSM's 8-bit passes): the
+// ranking's per-bit loop then has no branch on the width (each `b < dbits` test was a VALU compare,
+// wait states and a branch per bit and item); DBITS = 0 reads it from `dbits`
+template <uint32_t DBITS>
 __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __restrict__ ks, const uint32_t* __restrict__ vs,
                                                             uint32_t* __restrict__ kd, uint32_t* __restrict__ vd, uint32_t n,
-                                                            uint32_t shift, uint32_t dbits,
+                                                            uint32_t shift, uint32_t dbits_rt,
                                                             const uint32_t* __restrict__ base, uint64_t* status,
                                                             uint32_t* tile_ctr) {
+    const uint32_t dbits = DBITS ? DBITS : dbits_rt;
     extern __shared__ uint32_t lds[];
     uint32_t* sk = lds;                                 // SORT_TILE keys in digit order
     uint32_t* sv = sk + SORT_TILE;                      // and their values
@@ -140,82 +146,90 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
     const uint32_t tile = misc[0];
     const uint32_t t0 = tile * SORT_TILE;
     const uint32_t wbase = t0 + w * 64 * SORT_ITEMS;
-    uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rk[SORT_ITEMS];
+    // every tile but the last is full: its copy of the body has no per-item bounds checks
+    auto body = [&](auto full_tag) __attribute__((always_inline)) {
+        constexpr bool FULL = decltype(full_tag)::value;
+        uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rk[SORT_ITEMS];
 #pragma unroll
-    for (uint32_t j = 0; j < SORT_ITEMS; j++) {
-        const uint32_t i = wbase + j * 64 + lane;
-        key[j] = i < n ? ks[i] : 0u;
-        val[j] = i < n ? vs[i] : 0u;
-    }
-    const uint64_t lt = (1ull << lane) - 1;
-#pragma unroll
-    for (uint32_t j = 0; j < SORT_ITEMS; j++) {
-        const bool valid = wbase + j * 64 + lane < n;
-        const uint32_t d = (key[j] >> shift) & dmask;
-        uint64_t eq = __ballot(valid);
-#pragma unroll
-        for (uint32_t b = 0; b < 8; b++) {
-            if (b < dbits) {
-                const bool bit = (d >> b) & 1;
-                const uint64_t m = __ballot(bit);
-                eq &= bit ? m : ~m;
-            }
+        for (uint32_t j = 0; j < SORT_ITEMS; j++) {
+            const uint32_t i = wbase + j * 64 + lane;
+            key[j] = (FULL || i < n) ? ks[i] : 0u;
+            val[j] = (FULL || i < n) ? vs[i] : 0u;
         }
-        const uint32_t before = __popcll(eq & lt);
-        const uint32_t old = valid ? cnt[w][d] : 0u;
-        // every lane of the group has read the counter before its lowest lane moves it
-        if (valid && before == 0) cnt[w][d] = old + (uint32_t)__popcll(eq);
-        rk[j] = old + before;
-        __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
-    // per digit: the waves' counts -> exclusive wave offsets, the tile's count
-    uint32_t tcount = 0;
-    if (tid < 256) {
+        const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll
-        for (uint32_t v = 0; v < SORT_WAVES; v++) {
-            const uint32_t c = cnt[v][tid];
-            cnt[v][tid] = tcount;
-            tcount += c;
-        }
-        // publish this tile's counts before anything else, so the next tiles can look back
-        st_status(status + (size_t)tile * 256 + tid, (tile == 0 ? ST_INC : ST_AGG) | (uint64_t)tcount);
-    }
-    uint32_t tot;
-    const uint32_t ts = scan256(tid < 256 ? tcount : 0u, misc + 4, tot);
-    if (tid < 256) tstart[tid] = ts;
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < SORT_ITEMS; j++) {
-        if (wbase + j * 64 + lane < n) {
+        for (uint32_t j = 0; j < SORT_ITEMS; j++) {
+            const bool valid = FULL || wbase + j * 64 + lane < n;
             const uint32_t d = (key[j] >> shift) & dmask;
-            const uint32_t pos = tstart[d] + cnt[w][d] + rk[j];
-            sk[pos] = key[j];
-            sv[pos] = val[j];
-        }
-    }
-    if (tid < 256) {
-        uint32_t excl = 0;
-        if (tile > 0) {
-            for (uint32_t k = tile - 1;; k--) {
-                uint64_t v;
-                while (((v = ld_status(status + (size_t)k * 256 + tid)) >> 62) == 0) __builtin_amdgcn_s_sleep(1);
-                excl += (uint32_t)(v & ST_COUNT);  // a digit's running count is below n < 2^32
-                if (v & ST_INC) break;
+            uint64_t eq = __ballot(valid);
+#pragma unroll
+            for (uint32_t b = 0; b < 8; b++) {
+                if (b < dbits) {
+                    const bool bit = (d >> b) & 1;
+                    const uint64_t m = __ballot(bit);
+                    eq &= bit ? m : ~m;
+                }
             }
-            st_status(status + (size_t)tile * 256 + tid, ST_INC | (uint64_t)(excl + tcount));
+            const uint32_t before = __popcll(eq & lt);
+            const uint32_t old = valid ? cnt[w][d] : 0u;
+            // every lane of the group has read the counter before its lowest lane moves it
+            if (valid && before == 0) cnt[w][d] = old + (uint32_t)__popcll(eq);
+            rk[j] = old + before;
+            __builtin_amdgcn_wave_barrier();
         }
-        goff[tid] = base[tid] + excl;
-    }
-    __syncthreads();
-    const uint32_t valid_n = min(SORT_TILE, n - t0);
-    for (uint32_t i = tid; i < valid_n; i += SORT_THREADS) {
-        const uint32_t k = sk[i];
-        const uint32_t d = (k >> shift) & dmask;
-        const uint32_t dst = goff[d] + i - tstart[d];
-        kd[dst] = k;
-        vd[dst] = sv[i];
-    }
+        __syncthreads();
+        // per digit: the waves' counts -> exclusive wave offsets, the tile's count
+        uint32_t tcount = 0;
+        if (tid < 256) {
+#pragma unroll
+            for (uint32_t v = 0; v < SORT_WAVES; v++) {
+                const uint32_t c = cnt[v][tid];
+                cnt[v][tid] = tcount;
+                tcount += c;
+            }
+            // publish this tile's counts before anything else, so the next tiles can look back
+            st_status(status + (size_t)tile * 256 + tid, (tile == 0 ? ST_INC : ST_AGG) | (uint64_t)tcount);
+        }
+        uint32_t tot;
+        const uint32_t ts = scan256(tid < 256 ? tcount : 0u, misc + 4, tot);
+        if (tid < 256) tstart[tid] = ts;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < SORT_ITEMS; j++) {
+            if (FULL || wbase + j * 64 + lane < n) {
+                const uint32_t d = (key[j] >> shift) & dmask;
+                const uint32_t pos = tstart[d] + cnt[w][d] + rk[j];
+                sk[pos] = key[j];
+                sv[pos] = val[j];
+            }
+        }
+        if (tid < 256) {
+            uint32_t excl = 0;
+            if (tile > 0) {
+                for (uint32_t k = tile - 1;; k--) {
+                    uint64_t v;
+                    while (((v = ld_status(status + (size_t)k * 256 + tid)) >> 62) == 0) __builtin_amdgcn_s_sleep(1);
+                    excl += (uint32_t)(v & ST_COUNT);  // a digit's running count is below n < 2^32
+                    if (v & ST_INC) break;
+                }
+                st_status(status + (size_t)tile * 256 + tid, ST_INC | (uint64_t)(excl + tcount));
+            }
+            goff[tid] = base[tid] + excl;
+        }
+        __syncthreads();
+        const uint32_t valid_n = FULL ? SORT_TILE : min(SORT_TILE, n - t0);
+        for (uint32_t i = tid; i < valid_n; i += SORT_THREADS) {
+            const uint32_t k = sk[i];
+            const uint32_t d = (k >> shift) & dmask;
+            const uint32_t dst = goff[d] + i - tstart[d];
+            kd[dst] = k;
+            vd[dst] = sv[i];
+        }
+    };
+    if (t0 + SORT_TILE <= n)
+        body(std::true_type{});
+    else
+        body(std::false_type{});
 }
 
 // ---- exclusive scan ---------------------------------------------------------------------------
@@ -355,9 +369,9 @@ hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_
     }
     hipLaunchKernelGGL(k_sort_base, dim3(1), dim3(256), 0, st, hist, pb.passes, base);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_sort_pass), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)SORT_LDS);
-    if (e != hipSuccess) return e;
+    for (const void* k : {reinterpret_cast<const void*>(k_sort_pass<8>), reinterpret_cast<const void*>(k_sort_pass<0>)})
+        if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SORT_LDS)) != hipSuccess)
+            return e;
     const uint32_t* sk = keys_in;
     const uint32_t* sv = vals_in;
     for (uint32_t q = 0; q < pb.passes; q++) {
@@ -367,8 +381,8 @@ hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_
         uint32_t* dv = to_out ? vals_out : vtmp;
         if ((e = hipMemsetAsync(ctr, 0, 4, st)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(status, 0, (size_t)tiles * 256 * 8, st)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_sort_pass, dim3(tiles), dim3(SORT_THREADS), SORT_LDS, st, sk, sv, dk, dv, (uint32_t)n,
-                           pb.shift[q], pb.bits[q], base + q * 256, status, ctr);
+        hipLaunchKernelGGL(pb.bits[q] == 8 ? k_sort_pass<8> : k_sort_pass<0>, dim3(tiles), dim3(SORT_THREADS), SORT_LDS,
+                           st, sk, sv, dk, dv, (uint32_t)n, pb.shift[q], pb.bits[q], base + q * 256, status, ctr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         sk = dk;
         sv = dv;

@@ -12,4 +12,4 @@ run() {  # name args...
 run lde --workload lde && run lde_bitrev --workload lde --order bitrev && run msm --workload msm \
   && run msm_small --workload msm --msm-scalars small && run ntt4 --workload ntt4 \
   && run msm_shard --workload msm-shard && run quotient_fused --workload quotient \
-  && run quotient_generic --workload quotient --air generic
+  && run quotient_generic --workload quotient --air generic && run verify --workload verify

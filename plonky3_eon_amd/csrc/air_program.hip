@@ -18,9 +18,9 @@
 // a wave executes the same instruction (uniform program counter: scalar instruction fetch, the next
 // instruction's fetch issued before the current one executes, no divergence).  A value read only
 // by the next instruction is forwarded in registers (operand mode M_PREV, no register-file round
-// trip).  The register file lives in LDS (two
-// 16-byte planes, conflict-free b128 access) sized by the program's register count, or in a global
-// buffer for very large programs.
+// trip).  Arithmetic is radix 2^29 with compiler-tracked value bounds (below).  Registers 0 and 1
+// live in VGPRs, the rest in LDS (three planes: two 16-byte, one 4-byte; conflict-free accesses)
+// sized by the program's register count, or in a global buffer for very large programs.
 #include <algorithm>
 #include <cstdlib>
 #include <map>

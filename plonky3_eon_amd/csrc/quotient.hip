@@ -119,18 +119,19 @@ __global__ void k_p2_trace(const Fr* inputs, uint64_t n, P2Args a, Fr* trace) {
 __device__ __forceinline__ F29 ld29(const Fr* p) { return shl5_to261<FrP>(ldg(p)); }
 __device__ __forceinline__ F29 ld29_raw(const Fr* p) { return shl5_raw<FrP>(ldg(p)); }
 
+// the inner sums carry-free: add29_norm takes one addend with limbs < 2^30
 __device__ __forceinline__ void p2_ext29(F29* s) {
-    const F29 t = add29_norm(add29_norm(s[0], s[1]), s[2]);
+    const F29 t = add29_norm(add29_lazy(s[0], s[1]), s[2]);
     s[0] = add29_norm(s[0], t);
     s[1] = add29_norm(s[1], t);
     s[2] = add29_norm(s[2], t);
 }
 
 __device__ __forceinline__ void p2_int29(F29* s) {
-    const F29 t = add29_norm(s[0], add29_norm(s[1], s[2]));
+    const F29 t = add29_norm(s[0], add29_lazy(s[1], s[2]));
     s[0] = add29_norm(s[0], t);
     s[1] = reduce_top29<FrP>(add29_norm(s[1], t));
-    s[2] = reduce_top29<FrP>(add29_norm(add29_norm(s[2], s[2]), t));
+    s[2] = reduce_top29<FrP>(add29_norm(add29_lazy(s[2], s[2]), t));
 }
 
 // acc alpha + c without carry propagation: both normalised, so the limbs stay < 2^30 -- what mul29

@@ -14,7 +14,8 @@
 // row window (local = row i, next = row (i + 2^qd) mod Q, vertically_packed_row_pair,
 // matrix/src/lib.rs:392-411), the selectors of selectors_on_coset at i, and the folder's
 // accumulator as a Horner chain acc = acc * alpha + C_k (folder.rs:81-85 with the reversed alpha
-// powers of prover.rs:578-579).  out[i] = acc * inv_vanishing[i] (prover.rs:699).  Every lane of
+// powers of prover.rs:578-579), stepped two constraints at a time (acc alpha^2 + C_k alpha +
+// C_k+1: two limb products, one Montgomery reduction).  out[i] = acc * inv_vanishing[i] (prover.rs:699).  Every lane of
 // a wave executes the same instruction (uniform program counter: scalar instruction fetch, the next
 // instruction's fetch issued before the current one executes, no divergence).  A value read only
 // by the next instruction is forwarded in registers (operand mode M_PREV, no register-file round
@@ -38,6 +39,11 @@ enum : uint32_t { OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_NEG = 3, OP_ASSERT = 4,
 // op word: opcode (bits 0-3) | OP_RED (the result is brought below 2p by reduce_top29) | K << K_SHIFT
 // (OP_SUB / OP_NEG: the multiple of p added, at least the subtrahend's bound)
 constexpr uint32_t OP_MASK = 0xf, OP_RED = 0x10, K_SHIFT = 8;
+// OP_ASSERT's kind (in the K field): the constraints are folded in pairs, acc alpha^2 + C_k alpha +
+// C_k+1 with one reduction (mul29_sum2): the first of a pair is held (AS_PEND), the second folds
+// both (AS_PAIR).  With an odd count the first constraint opens the chain alone (AS_INIT: acc = C,
+// acc alpha + C from acc = 0).
+enum : uint32_t { AS_INIT = 0, AS_PEND = 1, AS_PAIR = 2 };
 // Value bounds.  Every value is held in radix 2^29 as x 2^261 ("29-Montgomery", field29.h) with
 // normalised limbs and a value below B p, B tracked per value by the compiler: products B = 2, a
 // sum B_a + B_b, a difference B_a + K.  A result whose bound would exceed B_MAX is reduced in the
@@ -200,13 +206,19 @@ struct CodeBlock {
 // (the slot's words picked by scalar selects, one product for MUL and ASSERT) measured slower,
 // 15.8 vs 14.8 ms for the Poseidon2-AIR at 2^18 rows (round 4, profiles/r04/s7): not kept.
 template <class RF>
-__device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, const F29& alpha, F29& acc,
-                                      F29& prev, Hot& hot) {
+__device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, const F29& alpha,
+                                      const F29& alpha2, F29& acc, F29& pend, F29& prev, Hot& hot) {
     const uint32_t opc = in.op & OP_MASK;
     if (opc == OP_NOP) return;
     const F29 x = fetch(in.a, rf, prev, hot, w);
-    if (opc == OP_ASSERT) {
-        acc = add29_norm(mul29<FrP>(acc, alpha), x);  // folder.rs:81-85, alpha powers reversed
+    if (opc == OP_ASSERT) {  // folder.rs:81-85, alpha powers reversed
+        const uint32_t kind = in.op >> K_SHIFT;
+        if (kind == AS_PAIR)  // acc < 34p, pend < 32p: acc alpha^2 + pend alpha < 132 p^2
+            acc = add29_lazy(mul29_sum2_u<FrP>(alpha2, acc, alpha, pend), x);
+        else if (kind == AS_PEND)
+            pend = x;
+        else
+            acc = x;
         return;
     }
     F29 r;
@@ -234,10 +246,11 @@ template <class RF>
 __device__ __forceinline__ void run_program(const CodeBlock* __restrict__ code, uint32_t n_blocks, RF& rf,
                                             const Window& w, const F29& alpha, F29& acc) {
     if (n_blocks == 0) return;
-    F29 prev;
+    const F29 alpha2 = uniform29(sqr29<FrP>(alpha));
+    F29 prev, pend;
     Hot hot;
 #pragma unroll
-    for (int i = 0; i < 9; i++) prev.l[i] = 0;
+    for (int i = 0; i < 9; i++) prev.l[i] = pend.l[i] = 0;
 #pragma unroll
     for (int i = 0; i < 9; i++) hot.h0.l[i] = hot.h1.l[i] = hot.h2.l[i] = hot.h3.l[i] = 0;
     CodeBlock nx = code[0];
@@ -251,7 +264,7 @@ __device__ __forceinline__ void run_program(const CodeBlock* __restrict__ code, 
                            (uint32_t)__builtin_amdgcn_readfirstlane(raw.dst),
                            (uint32_t)__builtin_amdgcn_readfirstlane(raw.a),
                            (uint32_t)__builtin_amdgcn_readfirstlane(raw.b)};
-            exec1(in, rf, w, alpha, acc, prev, hot);
+            exec1(in, rf, w, alpha, alpha2, acc, pend, prev, hot);
         };
         static_assert(CODE_BLOCK == 4, "four slots below");
         slot(cur.i[0]);
@@ -287,8 +300,8 @@ __global__ void __launch_bounds__(AIR_BLOCK) k_air_quotient(const CodeBlock* __r
         rf.top = reinterpret_cast<uint32_t*>(gregs + 2ull * n_mem * q) + row;
         rf.stride = q;
     }
-    run_program(code, n_blocks, rf, w, shl5_to261<FrP>(alpha), acc);
-    // acc (x 2^261, < (2 + B_RAW) p) times inv_vanishing in the ABI form: x 2^261 y 2^256 2^-261
+    run_program(code, n_blocks, rf, w, uniform29(shl5_to261<FrP>(alpha)), acc);
+    // acc (x 2^261, < (2 + B_RAW) p, limbs < 2^30) times inv_vanishing in the ABI form: x 2^261 y 2^256 2^-261
     // = x y 2^256 (prover.rs:699)
     const F29 r = mul29<FrP>(acc, unpack29(ld_pinned(inv_van + (row & nr_mask))));
     st_vec(out + row, pack29<FrP>(canon29<FrP>(r)));
@@ -522,10 +535,16 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
     // and differences add up, a result above B_MAX is reduced by its own instruction
     std::vector<uint32_t> bound(nv, 2);
     auto is_leaf = [&](uint32_t v) { return vals[v].op == LEAF; };
+    // assert kinds: pairs from the end of the chain, so an odd count leaves the first one alone
+    uint32_t n_asserts = 0, seen = 0;
+    for (const Item& it : items) n_asserts += it.assert_ ? 1 : 0;
     for (size_t t = 0; t < items.size(); t++) {
         const Item& it = items[t];
-        if (it.assert_) {  // acc alpha + x: acc < (2 + B_RAW) p, a < 68 p^2 product
-            p->code.push_back({OP_ASSERT, 0, opnd(it.v) | (is_leaf(it.v) ? OPND_RAW : 0u), 0});
+        if (it.assert_) {  // constraint values: < B_RAW p (raw leaf) or < B_MAX p
+            const uint32_t odd = n_asserts & 1;
+            const uint32_t kind = (odd && seen == 0) ? AS_INIT : ((seen - odd) % 2 == 0 ? AS_PEND : AS_PAIR);
+            seen++;
+            p->code.push_back({OP_ASSERT | kind << K_SHIFT, 0, opnd(it.v) | (is_leaf(it.v) ? OPND_RAW : 0u), 0});
             release(it.v, t);
             continue;
         }

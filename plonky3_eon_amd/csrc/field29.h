@@ -530,6 +530,56 @@ EON_HD F29 mul29_sum2(const F29& a, const F29& b, const F29& c, const F29& d) {
     return r;
 }
 
+// mul29_sum2 with a and c wave-uniform (the Horner powers of a quotient fold): their limbs are
+// read as the SGPR operand of each multiply-add, so the pair costs no VGPRs.  The caller makes
+// them uniform (uniform29).  Same contract and result as mul29_sum2.
+template <class M>
+EON_HD F29 mul29_sum2_u(const F29& a, const F29& b, const F29& c, const F29& d) {
+    uint32_t m[9];
+    F29 r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+#pragma unroll
+        for (int i = 0; i <= k; i++) {
+            mad29_vs(acc, b.l[k - i], a.l[i]);
+            mad29_vs(acc, d.l[k - i], c.l[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
+        m[k] = k < 6 ? (uint32_t)acc * R29<M>::INV : ((uint32_t)acc * R29<M>::INV) & M29;
+        mad29_vs(acc, m[k], R29<M>::P[0]);
+        acc >>= 29;
+    }
+#pragma unroll
+    for (int k = 9; k < 17; k++) {
+#pragma unroll
+        for (int i = k - 8; i < 9; i++) {
+            mad29_vs(acc, b.l[k - i], a.l[i]);
+            mad29_vs(acc, d.l[k - i], c.l[i]);
+            mad29_vs(acc, m[i], R29<M>::P[k - i]);
+        }
+        r.l[k - 9] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
+    r.l[8] = (uint32_t)acc;
+    return r;
+}
+
+// a value the whole wave holds alike, marked uniform limb by limb (SGPRs)
+EON_HD F29 uniform29(const F29& a) {
+    F29 r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+#ifdef __HIP_DEVICE_COMPILE__
+        r.l[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.l[i]);
+#else
+        r.l[i] = a.l[i];
+#endif
+    }
+    return r;
+}
+
 // ---- compile-time overflow guard for the unmasked Montgomery multipliers --------------------------
 // Worst case of every 64-bit column accumulator of mul29 / sqr29 / mul29_sum2: every operand limb
 // at its contract maximum (`prod_max` = the operand products one column position can add), every
@@ -559,6 +609,7 @@ static_assert(columns_fit_u64<FqP>(L30 * L30, 8), "mul29<Fq> column overflow");
 static_assert(columns_fit_u64<FrP>(L30 * L30, 8), "mul29<Fr> column overflow");
 // mul29_sum2: a, c, d normalised, b < 2^31 (a sub29_lazy output), 6 unmasked multipliers
 static_assert(columns_fit_u64<FqP>(L29 * L31 + L29 * L29, 6), "mul29_sum2<Fq> column overflow");
+static_assert(columns_fit_u64<FrP>(L29 * L31 + L29 * L29, 6), "mul29_sum2<Fr> column overflow");
 
 // Same with the product and reduction terms of a column in two accumulators (shorter dependency
 // chains), merged once per column.

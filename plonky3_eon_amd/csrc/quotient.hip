@@ -141,13 +141,13 @@ __device__ __forceinline__ void p2_int29(F29* s) {
 // < 36p 2p + 34p 2p = 140 p^2, inside its 0.99 p 2^261 = 167 p^2)
 __device__ __forceinline__ void horner2_29(F29& acc, const F29& alpha, const F29& alpha2,
                                            const F29& c0, const F29& c1) {
-    acc = add29_lazy(mul29_sum2<FrP>(alpha2, acc, alpha, c0), c1);
+    acc = add29_lazy(mul29_sum2_u<FrP>(alpha2, acc, alpha, c0), c1);
 }
 
 // The constraints are folded in pairs (every round asserts an even number of them): the same
 // acc as one Horner step per constraint, 80 instead of 160 reductions per permutation.
 __device__ F29 p2_fold29(const Fr* c, const P2Args& a, const F29& alpha) {
-    const F29 alpha2 = sqr29<FrP>(alpha);
+    const F29 alpha2 = uniform29(sqr29<FrP>(alpha));  // alpha, alpha^2 in SGPRs
     F29 acc;
 #pragma unroll
     for (int i = 0; i < 9; i++) acc.l[i] = 0;
@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(256) k_p2_quotient(const Fr* lde, uint64_t q, 
     Fr p = Fr::zero();
     if (row < q) {
         const Fr* c = lde + row * (uint64_t)a.ncols * a.vl + (uint64_t)v * a.ncols;
-        F29 acc = p2_fold29(c, a, shl5_to261<FrP>(alpha));
+        F29 acc = p2_fold29(c, a, uniform29(shl5_to261<FrP>(alpha)));
         // the lane's share times its alpha power (29-Montgomery), then times inv_vanishing in the
         // ABI form: mul29 of x 2^261 and y 2^256 is x y 2^256 (prover.rs:699)
         if (a.vl > 1) acc = mul29<FrP>(acc, shl5_to261<FrP>(lane_pow.v[v]));

@@ -7,13 +7,14 @@
 set -o pipefail
 mkdir -p gpurun_out
 [ $# -ge 1 ] || { echo "usage: $0 <variant>..."; exit 2; }
-# PROBE_WORKLOADS (default "msm prove"): the bench.py workloads timed per library
+# PROBE_WORKLOADS (default "msm prove"): the bench.py workloads timed per library; PROBE_ARGS: extra
+# bench.py arguments for every run (e.g. "--air generic")
 run() {
   local line="$1"
   for w in ${PROBE_WORKLOADS:-msm prove}; do
     local st=10
     [ $w = prove ] && st=3
-    timeout -k 10 300 python3 bench.py --workload $w --no-cpu-baseline --steps $st > gpurun_out/probe_${w}_$1.json \
+    timeout -k 10 300 python3 bench.py --workload $w $PROBE_ARGS --no-cpu-baseline --steps $st > gpurun_out/probe_${w}_$1.json \
       2>/dev/null || return 1
     line="$line $w $(python3 -c "import json,sys; print(json.load(open(sys.argv[1]))['ms_per_step'])" \
       gpurun_out/probe_${w}_$1.json)"

@@ -135,7 +135,7 @@ struct MemRegs {
 struct Window {
     const Fr* local;
     const Fr* next;
-    const Fr* table;  // program constants, then public values
+    const F29* table;  // program constants, then public values: x 2^261 (< 2p), converted on the host
     const Fr* sels;   // is_first_row | is_last_row | is_transition, q each (null if unused)
     uint64_t row, q;
 };
@@ -185,7 +185,7 @@ __device__ __forceinline__ F29 fetch(uint32_t opnd, const RF& rf, const F29& pre
         }
         case M_LOCAL: return ld29(w.local + i, raw);
         case M_NEXT: return ld29(w.next + i, raw);
-        case M_CONST: return ld29(w.table + i, raw);
+        case M_CONST: return w.table[i];  // uniform index: scalar loads, no conversion
         case M_FIRST: return ld29(w.sels + w.row, raw);
         case M_LAST: return ld29(w.sels + w.q + w.row, raw);
         case M_TRANS: return ld29(w.sels + 2 * w.q + w.row, raw);
@@ -278,7 +278,7 @@ __device__ __forceinline__ void run_program(const CodeBlock* __restrict__ code, 
 template <int MODE>
 __global__ void __launch_bounds__(AIR_BLOCK) k_air_quotient(const CodeBlock* __restrict__ code, uint32_t n_blocks,
                                                       uint32_t n_regs, const Fr* __restrict__ lde, uint32_t width,
-                                                      uint64_t q, uint64_t next_step, const Fr* __restrict__ table,
+                                                      uint64_t q, uint64_t next_step, const F29* __restrict__ table,
                                                       const Fr* __restrict__ sels, const Fr* __restrict__ inv_van,
                                                       uint32_t nr_mask, Fr alpha, Fr* __restrict__ out,
                                                       uint4* __restrict__ gregs) {
@@ -317,6 +317,7 @@ struct eon_air_program {
     std::vector<Fr> consts;
     DevBuf d_code, d_table, d_sels, d_regs;
     std::vector<Fr> staged;  // host copy of the table for the current launch
+    std::vector<F29> staged29;  // the same in the device's form (x 2^261, < 2p)
 };
 
 namespace {
@@ -535,6 +536,7 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
     // and differences add up, a result above B_MAX is reduced by its own instruction
     std::vector<uint32_t> bound(nv, 2);
     auto is_leaf = [&](uint32_t v) { return vals[v].op == LEAF; };
+    auto is_tleaf = [&](uint32_t v) { return is_leaf(v) && (vals[v].a >> 29) != M_CONST; };
     // assert kinds: pairs from the end of the chain, so an odd count leaves the first one alone
     uint32_t n_asserts = 0, seen = 0;
     for (const Item& it : items) n_asserts += it.assert_ ? 1 : 0;
@@ -544,14 +546,15 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
             const uint32_t odd = n_asserts & 1;
             const uint32_t kind = (odd && seen == 0) ? AS_INIT : ((seen - odd) % 2 == 0 ? AS_PEND : AS_PAIR);
             seen++;
-            p->code.push_back({OP_ASSERT | kind << K_SHIFT, 0, opnd(it.v) | (is_leaf(it.v) ? OPND_RAW : 0u), 0});
+            p->code.push_back({OP_ASSERT | kind << K_SHIFT, 0, opnd(it.v) | (is_tleaf(it.v) ? OPND_RAW : 0u), 0});
             release(it.v, t);
             continue;
         }
         const Val& x = vals[it.v];
         const bool unary = x.op == OP_NEG;
-        // per use: the leaf operands raw unless a product's other side is too wide for it
-        bool raw_a = is_leaf(x.a), raw_b = !unary && is_leaf(x.b);
+        // per use: the leaf operands raw unless a product's other side is too wide for it; constants
+        // arrive reduced (the table is converted on the host), never raw
+        bool raw_a = is_tleaf(x.a), raw_b = !unary && is_tleaf(x.b);
         if (x.op == OP_MUL) {
             if (raw_a && raw_b)
                 raw_b = false;  // 32 x 2
@@ -629,7 +632,7 @@ int eon_air_program_create(eon_ctx* ctx, const eon_sym_node* nodes, uint32_t n_n
         hipError_t e = p->d_code.ensure(std::max<size_t>(1, padded.size()) * sizeof(Instr));
         if (e == hipSuccess && !padded.empty())
             e = hipMemcpy(p->d_code.p, padded.data(), padded.size() * sizeof(Instr), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = p->d_table.ensure(std::max<size_t>(1, p->n_consts + n_public) * sizeof(Fr));
+        if (e == hipSuccess) e = p->d_table.ensure(std::max<size_t>(1, p->n_consts + n_public) * sizeof(F29));
         if (e != hipSuccess) {
             p->d_code.release();
             p->d_table.release();
@@ -697,7 +700,9 @@ int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const e
             prog->staged.push_back(v);
         }
         if (!prog->staged.empty()) {
-            EON_HIP(hipMemcpyAsync(prog->d_table.p, prog->staged.data(), prog->staged.size() * sizeof(Fr),
+            prog->staged29.resize(prog->staged.size());
+            for (size_t i = 0; i < prog->staged.size(); i++) prog->staged29[i] = shl5_to261<FrP>(prog->staged[i]);
+            EON_HIP(hipMemcpyAsync(prog->d_table.p, prog->staged29.data(), prog->staged29.size() * sizeof(F29),
                                    hipMemcpyHostToDevice, ctx->stream));
             EON_HIP(hipStreamSynchronize(ctx->stream));  // `staged` is reused by the next launch
         }
@@ -745,14 +750,14 @@ int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const e
         const Fr* sel = prog->uses_sels ? prog->d_sels.as<Fr>() : nullptr;
         Fr* out_f = reinterpret_cast<Fr*>(out);
         using KernelFn = void (*)(const CodeBlock*, uint32_t, uint32_t, const Fr*, uint32_t, uint64_t, uint64_t,
-                                  const Fr*, const Fr*, const Fr*, uint32_t, Fr, Fr*, uint4*);
+                                  const F29*, const Fr*, const Fr*, uint32_t, Fr, Fr*, uint4*);
         const KernelFn kern = mode == 0 ? k_air_quotient<0> : k_air_quotient<1>;
         if (mode == 0)  // per launch: the attribute is per device, and this context's device may
                         // differ from the one another context set it on
             EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         hipLaunchKernelGGL(kern, dim3(grid), dim3(block), shmem, ctx->stream, code, n_blocks, prog->n_regs, lde_f,
-                           prog->width, q, 1ull << log_qd, prog->d_table.as<Fr>(), sel, inv_van, nr_mask, al, out_f,
+                           prog->width, q, 1ull << log_qd, prog->d_table.as<F29>(), sel, inv_van, nr_mask, al, out_f,
                            mode == 1 ? prog->d_regs.as<uint4>() : nullptr);
         ctx->prof.end(ctx->stream);
         EON_HIP(hipGetLastError());

@@ -35,7 +35,9 @@ using namespace eon;
 
 namespace {
 
-enum : uint32_t { OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_NEG = 3, OP_ASSERT = 4, OP_NOP = 5 };
+enum : uint32_t { OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_NEG = 3, OP_ASSERT = 4, OP_NOP = 5, OP_SQR = 6 };
+// OP_SQR: a product of a value by itself (x * x after hash-consing), sqr29's 45 limb products
+// instead of 81
 // op word: opcode (bits 0-3) | OP_RED (the result is brought below 2p by reduce_top29) | K << K_SHIFT
 // (OP_SUB / OP_NEG: the multiple of p added, at least the subtrahend's bound)
 constexpr uint32_t OP_MASK = 0xf, OP_RED = 0x10, K_SHIFT = 8;
@@ -224,6 +226,8 @@ __device__ __forceinline__ void exec1(const Instr& in, RF& rf, const Window& w, 
     F29 r;
     if (opc == OP_MUL) {
         r = mul29<FrP>(x, fetch(in.b, rf, prev, hot, w));
+    } else if (opc == OP_SQR) {
+        r = sqr29<FrP>(x);
     } else {
         if (opc == OP_ADD) {
             r = add29_norm(x, fetch(in.b, rf, prev, hot, w));
@@ -555,7 +559,10 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
         // per use: the leaf operands raw unless a product's other side is too wide for it; constants
         // arrive reduced (the table is converted on the host), never raw
         bool raw_a = is_tleaf(x.a), raw_b = !unary && is_tleaf(x.b);
-        if (x.op == OP_MUL) {
+        const bool square = x.op == OP_MUL && x.a == x.b;  // sqr29: x < 12.9p, so never a raw leaf
+        if (square) {
+            raw_a = raw_b = false;
+        } else if (x.op == OP_MUL) {
             if (raw_a && raw_b)
                 raw_b = false;  // 32 x 2
             else if (raw_a && bound[x.b] * B_RAW > 160)
@@ -564,7 +571,7 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
                 raw_b = false;
         }
         const uint32_t ba = raw_a ? B_RAW : bound[x.a], bb = unary ? 0 : raw_b ? B_RAW : bound[x.b];
-        uint32_t op = x.op, b = 2;
+        uint32_t op = square ? OP_SQR : x.op, b = 2;
         if (x.op == OP_ADD) {
             b = ba + bb;
         } else if (x.op == OP_SUB) {
@@ -579,7 +586,8 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
             b = 2;
         }
         bound[it.v] = b;
-        Instr in{op, 0, opnd(x.a) | (raw_a ? OPND_RAW : 0u), unary ? 0u : opnd(x.b) | (raw_b ? OPND_RAW : 0u)};
+        Instr in{op, 0, opnd(x.a) | (raw_a ? OPND_RAW : 0u),
+                 (unary || square) ? 0u : opnd(x.b) | (raw_b ? OPND_RAW : 0u)};
         release(x.a, t);
         if (x.op != OP_NEG && x.b != x.a) release(x.b, t);
         if (last[it.v] < 0) continue;  // never read (cannot happen for reachable values)
@@ -741,7 +749,7 @@ int eon_quotient_values_dev(eon_ctx* ctx, const eon_air_program* prog_c, const e
         uint64_t products = 1;
         for (const Instr& in : prog->code) {
             const uint32_t opc = in.op & OP_MASK;
-            products += (opc == OP_MUL || opc == OP_ASSERT) ? 1 : 0;
+            products += (opc == OP_MUL || opc == OP_SQR || opc == OP_ASSERT) ? 1 : 0;
         }
         ctx->prof.begin("k_air_quotient", q * (uint64_t)prog->width * 32 + q * 32, ctx->stream, q * products);
         const CodeBlock* code = prog->d_code.as<CodeBlock>();

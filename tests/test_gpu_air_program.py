@@ -17,7 +17,7 @@ compressed-G1 transcript bytes stay unpinned."""
 import numpy as np
 import pytest
 
-from airs import FibonacciAir, MixedAir, MulAir
+from airs import FibonacciAir, MixedAir, MockAir, MulAir
 from oracle import coracle as C
 from oracle import prove_oracle
 from oracle import pyoracle as O
@@ -64,6 +64,33 @@ def test_quotient_values_vs_oracle(gpu_ctx, air_cls, fn, log_n, log_qd):
     got = prog.quotient_values(torch.from_numpy(lde.view(np.int64)).to("cuda:0"), log_n, log_qd, alpha, pub)
     got = ints(got.cpu().numpy().view(np.uint64))
     want = O.quotient_values_fn([ints(r) for r in lde], log_n, log_qd, fn, alpha, pub)
+    assert got == want
+
+
+@pytest.mark.parametrize("specs", [[(0, 1)], [(0, 0), (1, 2)], [(1, 0), (0, 2), (0, 1)],
+                                   [(0, 0), (0, 1), (1, 1), (0, 2)]])
+def test_constraint_pairing_edges(gpu_ctx, specs):
+    """The device folds constraints in pairs (acc alpha^2 + C_k alpha + C_k+1, one reduction); an
+    odd count opens the chain with a lone constraint.  1-4 constraints (MockAir leaves) against the
+    oracle's one-at-a-time Horner fold."""
+    import torch
+
+    from plonky3_eon_amd.air import AirProgram
+
+    air = MockAir(specs, 3)
+    prog = AirProgram(air, gpu_ctx)
+    assert prog.num_constraints == len(specs)
+    log_n, log_qd = 3, 1
+    q = 1 << (log_n + log_qd)
+    lde = C.random_fr(40 + len(specs), q * prog.width).reshape(q, prog.width, 4)
+    alpha = 0x2F1E0D0C0B0A09080706050403020100
+    got = prog.quotient_values(torch.from_numpy(lde.view(np.int64)).to("cuda:0"), log_n, log_qd, alpha, [])
+    got = ints(got.cpu().numpy().view(np.uint64))
+
+    def fn(loc, nxt, sels, pub):
+        return [(loc if o == 0 else nxt)[i] for o, i in specs]
+
+    want = O.quotient_values_fn([ints(r) for r in lde], log_n, log_qd, fn, alpha, [])
     assert got == want
 
 

@@ -285,6 +285,15 @@ EON_HD void mul29_vv(uint64_t& acc, uint32_t a, uint32_t b) {
 #endif
 }
 
+EON_HD void mul29_vs(uint64_t& acc, uint32_t a, uint32_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    uint64_t c;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(acc), "=s"(c) : "v"(a), "s"(b));
+#else
+    acc = (uint64_t)a * b;
+#endif
+}
+
 // Montgomery product a b 2^-261 mod p (product scanning; see the header comment for the bounds)
 //
 // The reduction multipliers m_0..m_(U-1) are left unmasked (32 bits instead of 29: one v_and
@@ -365,6 +374,44 @@ EON_HD F29 mul29_shoup(const F29& y, const F29& w, const F29& wq) {
             mad29_vv(acc, y.l[0], w.l[k]);
 #pragma unroll
         for (int i = 1; i <= k; i++) mad29_vv(acc, y.l[i], w.l[k - i]);
+#pragma unroll
+        for (int i = 0; i <= k; i++) mad29_vs(acc, q[i], R29<M>::NEGP261[k - i]);
+        r.l[k] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
+    return r;
+}
+
+// mul29_shoup with w and wq wave-uniform (a kernel argument, an evaluation point): their limbs are
+// the SGPR operand of every multiply-add, so the pair costs no VGPRs.  Same contract and result.
+template <class M>
+EON_HD F29 mul29_shoup_u(const F29& y, const F29& w, const F29& wq) {
+    uint64_t acc;
+    uint32_t q[9];
+    mul29_vs(acc, y.l[0], wq.l[7]);
+#pragma unroll
+    for (int i = 1; i <= 7; i++) mad29_vs(acc, y.l[i], wq.l[7 - i]);
+    acc >>= 29;
+#pragma unroll
+    for (int i = 0; i <= 8; i++) mad29_vs(acc, y.l[i], wq.l[8 - i]);
+    acc >>= 29;
+#pragma unroll
+    for (int k = 9; k < 17; k++) {
+#pragma unroll
+        for (int i = k - 8; i < 9; i++) mad29_vs(acc, y.l[i], wq.l[k - i]);
+        q[k - 9] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
+    q[8] = (uint32_t)acc;
+    F29 r;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        if (k == 0)
+            mul29_vs(acc, y.l[0], w.l[0]);
+        else
+            mad29_vs(acc, y.l[0], w.l[k]);
+#pragma unroll
+        for (int i = 1; i <= k; i++) mad29_vs(acc, y.l[i], w.l[k - i]);
 #pragma unroll
         for (int i = 0; i <= k; i++) mad29_vs(acc, q[i], R29<M>::NEGP261[k - i]);
         r.l[k] = (uint32_t)acc & M29;
@@ -537,12 +584,15 @@ template <class M>
 EON_HD F29 mul29_sum2_u(const F29& a, const F29& b, const F29& c, const F29& d) {
     uint32_t m[9];
     F29 r;
-    uint64_t acc = 0;
+    uint64_t acc;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
 #pragma unroll
         for (int i = 0; i <= k; i++) {
-            mad29_vs(acc, b.l[k - i], a.l[i]);
+            if (k == 0)
+                mul29_vs(acc, b.l[0], a.l[0]);
+            else
+                mad29_vs(acc, b.l[k - i], a.l[i]);
             mad29_vs(acc, d.l[k - i], c.l[i]);
         }
 #pragma unroll

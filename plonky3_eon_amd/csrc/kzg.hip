@@ -110,7 +110,7 @@ __global__ void k_eval_block(const Fr* c, uint64_t n, uint32_t width, PtsShoup z
         const F29 x = unpack29(ld(c + i * width + col));  // canonical
 #pragma unroll
         for (uint32_t p = 0; p < MAX_PTS; p++)
-            if (p < np) r[p] = add29_norm(x, mul29_shoup<FrP>(r[p], zs.w[p], zs.q[p]));  // < p + 3p
+            if (p < np) r[p] = add29_norm(x, mul29_shoup_u<FrP>(r[p], zs.w[p], zs.q[p]));  // < p + 3p; z in SGPRs
     }
 #pragma unroll
     for (uint32_t p = 0; p < MAX_PTS; p++)

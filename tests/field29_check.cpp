@@ -57,6 +57,15 @@ static void put(const F29& a) {
     printf(" ");
 }
 
+// the uniform-operand forms (SGPR operands on the device) compute the same columns
+static void same(const F29& x, const F29& y, const char* what) {
+    for (int i = 0; i < 9; i++)
+        if (x.l[i] != y.l[i]) {
+            fprintf(stderr, "%s differs from its VGPR form\n", what);
+            exit(1);
+        }
+}
+
 template <class M>
 static void run(const char* name, int trials) {
     for (int t = 0; t < trials; t++) {
@@ -80,6 +89,7 @@ static void run(const char* name, int trials) {
         put(s_d);
         put(mul29_sum2<M>(s_a, s_b, s_c, s_d));
         printf("\n");
+        same(mul29_sum2_u<M>(s_a, s_b, s_c, s_d), mul29_sum2<M>(s_a, s_b, s_c, s_d), "mul29_sum2_u");
     }
 }
 
@@ -100,6 +110,7 @@ static void run_shoup(int trials) {
         put(wq);
         put(mul29_shoup<FrP>(y, w, wq));
         printf("\n");
+        same(mul29_shoup_u<FrP>(y, w, wq), mul29_shoup<FrP>(y, w, wq), "mul29_shoup_u");
     }
 }
 

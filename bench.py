@@ -24,10 +24,15 @@ Also reported:
   roofline     -- for the dominant kernel (largest total time): algorithmic bytes per launch
                    / average launch duration (HIP events on the launch
                   stream, eon_ctx_profile, over serialized profiled steps after the timed region)
-                  vs 8 TB/s HBM, `traffic` from the committed PMC pass (profiles/traffic_*.json);
+                  vs 8 TB/s HBM, `traffic` from this round's committed PMC pass
+                  (profiles/r05/traffic_*.json, stamped with the commit it measured);
                   `valu` is the binding integer roofline of the same kernel: its algorithmic
                   256-bit Montgomery products per launch / launch duration vs the measured
-                  mulmod peak (tools/ubench_mulmod.hip).
+                  mulmod peak (tools/ubench_r29.hip), and vs the product rate measured live on
+                  this box by the clock probe (`frac_live`).
+  gpu_clock_inkernel_mhz -- the shader clock held under a product chain right after the timed
+                  region (eon_diag_clock_probe: s_memtime / s_memrealtime), beside `gpu_sclk`
+                  (sysfs, which is not the in-kernel clock).
   cpu_baseline -- the C restatement (oracle/eon_oracle.c, OpenMP) of the same work timed on this
                   host on a bounded sample, rank 0 at N = 1 only.
 """
@@ -53,6 +58,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # 1.80e11/s; the radix-2^32 FIPS product of the quotient kernel peaks at 1.29e11/s,
 # tools/ubench_mulmod.hip)
 MULMOD_PEAK_PER_S = 1.80e11
+# PMC traffic files are read from this round's profile directory only (see main())
+TRAFFIC_ROUND = "r05"
 FR_P = [0x43E1F593F0000001, 0x2833E84879B97091, 0xB85045B68181585D, 0x30644E72E131A029]
 
 
@@ -811,6 +818,8 @@ def make_parser() -> argparse.ArgumentParser:
                     help="msm: uniform Fr scalars, or all < 2^64 (kzg/benches/kzg_benches.rs:16-22)")
     ap.add_argument("--cpu-sample-cols", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-clock-probe", action="store_true",
+                    help="skip the in-kernel clock probe after the timed region (~2 s)")
     ap.add_argument("--cpu-full", action="store_true",
                     help="prove: also the larger end-to-end CPU restatement runs (2^10 Horner, 2^12; minutes)")
     ap.add_argument("--serial", action="store_true",
@@ -930,6 +939,12 @@ def main() -> int:
     prof = ctx.profile_report()
     ctx.profile(False)
     ctx.set_serial(args.serial)
+    # the clock the chip holds under this VALU load, and the product peak at that clock, measured
+    # now on this box (eon_diag_clock_probe; MI355X_MICROARCH.md DVFS item 6): ~2 s of the
+    # roofline denominator's own product chain, stamped with s_memtime / s_memrealtime
+    clock = None
+    if not args.no_clock_probe:
+        clock = ctx.clock_probe(160, 1024)
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
@@ -989,6 +1004,10 @@ def main() -> int:
             "peak_mulmod_per_s": MULMOD_PEAK_PER_S,
             "frac": round(rate / MULMOD_PEAK_PER_S, 4),
         }
+        if clock:
+            # the same kernel against the product rate this box sustained at the clock it held
+            roof["valu"]["peak_live_mulmod_per_s"] = round(clock["products_per_s"], 1)
+            roof["valu"]["frac_live"] = round(rate / clock["products_per_s"], 4)
     if mulmods is not None:
         roof["valu_whole_step"] = {
             "achieved_mulmod_per_s": round(mulmods / (gpu_total_ms * 1e-3), 1),
@@ -1024,15 +1043,25 @@ def main() -> int:
         "config": {"workload": workload, "global_batch": gbatch, "seq_len": seq, "parallelism": par},
         "throughput": thr,
         "gpu_sclk": sclk_stats,
+        "gpu_clock_inkernel_mhz": round(clock["clock_mhz_median"], 1) if clock else None,
+        "gpu_clock_probe": ({k: round(v, 4 if k == "ms_per_launch" else 1) for k, v in clock.items()} | {
+            "source": "eon_diag_clock_probe after the timed region: 161 launches of a radix-2^29 product chain "
+                      "(4096 x 256 threads, 2 chains, 1024 products each), median over blocks of "
+                      "delta s_memtime / delta s_memrealtime x 100 MHz"}) if clock else None,
         "roofline": roof,
         "cpu_baseline": None,
     }
-    traffic_file = ROOT / "profiles" / f"traffic_{args.workload}.json"
+    # PMC traffic of THIS round's build only (tools/gpu_pmc.sh -> profiles/<round>/traffic_*.json,
+    # stamped with the commit it measured); an older round's file describes another build
+    traffic_file = ROOT / "profiles" / TRAFFIC_ROUND / f"traffic_{args.workload}.json"
     if traffic_file.exists():
         try:
             tf = json.loads(traffic_file.read_text())
             if tf.get("kernel") == kname and tf.get("workload") == workload:
                 roof["traffic"] = tf.get("bytes_per_launch")
+                roof["traffic_source"] = "%s (commit %s; FETCH_SIZE %.3g GB raw, WRITE_SIZE %.3g GB per launch)" % (
+                    traffic_file.relative_to(ROOT), tf.get("commit", "?"), tf["fetch_size_kb_per_launch"] * 1024 / 1e9,
+                    tf["write_size_kb_per_launch"] * 1024 / 1e9)
         except Exception:
             pass
 

@@ -116,6 +116,12 @@ int eon_ctx_device(const eon_ctx* ctx);
  * the same order. */
 int eon_ctx_set_collective(eon_ctx* ctx, const eon_collective* coll);
 int eon_ctx_synchronize(eon_ctx* ctx);
+/* Give back to the device every cached idle buffer of the context: the transient-buffer pool
+ * (KZG opening-bases tables and scratch; capped at EON_POOL_CAP_GB, default 8, read at creation)
+ * and the kept sorted-digit buffers of destroyed eon_msm_scalars (capped at 48 GB).  Synchronizes
+ * the context's streams first.  Call it between proofs when another allocator in the process
+ * (e.g. torch's caching allocator) needs the memory; the next proof allocates afresh. */
+int eon_ctx_trim(eon_ctx* ctx);
 /* Per-launch kernel timing with HIP events on the launch stream (the analogue of the
  * reference's tracing spans, e.g. dft/src/radix_2_dit_parallel.rs:168).  eon_ctx_profile(ctx, 1)
  * clears the record and starts recording; eon_ctx_profile_report writes a JSON object
@@ -128,6 +134,20 @@ int eon_ctx_profile_report(eon_ctx* ctx, char* buf, uint64_t len);
  * the prove is slower (no overlap of digit sorts with piece sums). */
 int eon_ctx_set_serial(eon_ctx* ctx, int serial);
 int eon_ctx_serial(const eon_ctx* ctx);
+/* ---- diagnostics (measurement only; not on any product path) ------------------------------ */
+typedef struct {
+    double clock_mhz_median; /* in-kernel shader clock: delta s_memtime / delta s_memrealtime x 100 MHz */
+    double clock_mhz_min;    /* over the blocks of the last launch */
+    double clock_mhz_max;
+    double products_per_s;   /* radix-2^29 Montgomery products per second over the timed launches */
+    double ms_per_launch;
+} eon_clock_probe;
+/* Run `launches` back-to-back launches of a radix-2^29 product chain (`iters` products per chain,
+ * two chains per thread, 4096 x 256 threads) on the context stream, after one untimed launch, and
+ * report the shader clock the chip held (median over blocks of the last launch) and the product
+ * rate (MI355X_MICROARCH.md, DVFS item 6).  Synchronous. */
+int eon_diag_clock_probe(eon_ctx* ctx, uint32_t launches, uint32_t iters, eon_clock_probe* out);
+
 /* ABI version; bumped on any signature or struct-layout change (4: the verifier pairings and their
  * eon_g2_affine / eon_fq12 types; 3: eon_collective's all_to_all field).  Bindings must check it
  * at load time: a binding built against an older layout would pass a shorter eon_collective. */

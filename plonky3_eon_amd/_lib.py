@@ -61,6 +61,11 @@ class eon_air_program_stats(ctypes.Structure):
                                                "num_constants")]
 
 
+class eon_clock_probe(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in ("clock_mhz_median", "clock_mhz_min", "clock_mhz_max", "products_per_s",
+                                              "ms_per_launch")]
+
+
 class eon_g1_affine(ctypes.Structure):
     _fields_ = [("x", ctypes.c_uint64 * 4), ("y", ctypes.c_uint64 * 4)]
 
@@ -81,6 +86,8 @@ SIGNATURES = {
     "eon_ctx_device": (_INT, [_P]),
     "eon_ctx_set_collective": (_INT, [_P, _P]),
     "eon_ctx_synchronize": (_INT, [_P]),
+    "eon_ctx_trim": (_INT, [_P]),
+    "eon_diag_clock_probe": (_INT, [_P, _U32, _U32, _P]),
     "eon_ctx_profile": (_INT, [_P, _INT]),
     "eon_ctx_profile_report": (_INT, [_P, ctypes.c_char_p, _U64]),
     "eon_ctx_set_serial": (_INT, [_P, _INT]),

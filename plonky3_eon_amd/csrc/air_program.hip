@@ -338,6 +338,10 @@ struct Leaf {
 // compile nodes -> program; see the file comment
 Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, const eon_fr* consts,
                uint32_t n_consts, const uint32_t* roots, uint32_t n_roots) {
+    // operand indices are 28 bits (bit 28 is OPND_RAW): a wider main-column index, constant slot
+    // or public slot would set the raw flag and read the wrong leaf
+    if (p->width > IDX_MASK || (uint64_t)n_consts + p->n_public > IDX_MASK)
+        return Status::err(EON_E_SHAPE, "trace width and constant + public slots must each be < 2^28");
     // value numbering
     std::vector<uint32_t> vn(n_nodes);
     std::vector<uint32_t> degree(n_nodes);
@@ -608,6 +612,7 @@ Status compile(eon_air_program* p, const eon_sym_node* nodes, uint32_t n_nodes, 
         p->code.push_back(in);
     }
     p->n_regs = n_regs;
+    if (n_regs > IDX_MASK) return Status::err(EON_E_SHAPE, "more than 2^28 - 1 registers");
     return Status::ok();
 }
 

@@ -313,6 +313,7 @@ int eon_ctx_create(int device_ordinal, eon_ctx** out) {
         return EON_E_DEVICE;
     }
     if (const char* e = getenv("EON_SERIAL")) c->serial = e[0] == '1';
+    if (const char* e = getenv("EON_POOL_CAP_GB")) c->pool.cap = (size_t)std::max(0, atoi(e)) << 30;
     if (const char* e = getenv("EON_NTT_MAX_STAGES")) c->ntt_max_stages = (uint32_t)atoi(e);
 #ifdef EON_TUNING_KNOBS
     // NTT plan overrides for tuning builds only (_build.build_variant(..., ["EON_TUNING_KNOBS"]))
@@ -420,6 +421,23 @@ int eon_ctx_synchronize(eon_ctx* ctx) {
         ctx->last_error = hipGetErrorString(e);
         return EON_E_DEVICE;
     }
+    return EON_OK;
+}
+
+int eon_ctx_trim(eon_ctx* ctx) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    (void)hipSetDevice(ctx->device);
+    for (hipStream_t st : {ctx->stream, ctx->msm_side, ctx->msm_side2, ctx->msm_sort}) {
+        hipError_t e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            ctx->last_error = hipGetErrorString(e);
+            return EON_E_DEVICE;
+        }
+    }
+    ctx->pool.release_all();
+    for (auto& sb : ctx->sorted_cache) sb.release();
+    ctx->sorted_cache.clear();
     return EON_OK;
 }
 

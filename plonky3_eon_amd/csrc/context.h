@@ -41,9 +41,10 @@ struct DevBuf {
 // Exact-size cache of large transient device buffers (the KZG opening bases' tables and their
 // scratch): a proof builds the same-sized buffers again, so they go back here instead of
 // hipFree (which synchronises the device and costs host time) and come back instead of hipMalloc.
-// Trimmed past CAP bytes; emptied with the context.
+// Trimmed past `cap` bytes (EON_POOL_CAP_GB at context creation, default 8); emptied by
+// eon_ctx_trim and with the context.
 struct DevPool {
-    static constexpr size_t CAP = size_t(8) << 30;
+    size_t cap = size_t(8) << 30;
     std::multimap<size_t, void*> free_;
     size_t bytes = 0;
     // `b` (empty or holding a smaller buffer, which returns to the pool) gets `need` bytes
@@ -73,7 +74,7 @@ struct DevPool {
     // work still queued on b must be finished (the caller synchronises first)
     void give(DevBuf& b) {
         if (!b.p) return;
-        if (bytes + b.bytes <= CAP) {
+        if (bytes + b.bytes <= cap) {
             free_.emplace(b.bytes, b.p);
             bytes += b.bytes;
         } else {
@@ -90,21 +91,27 @@ struct DevPool {
 };
 
 // The buffers local to one call, taken from a DevPool and given back when the scope ends -- on
-// every path, early error returns included -- after the stream that used them has drained.
+// every path, early error returns included -- after the stream that used them has drained.  The
+// scope keeps its own copy of each (pointer, size) it handed out, never a reference to the
+// caller's DevBuf, so the order in which the scope and the caller's buffers are declared does
+// not matter (a DevBuf declared after the scope ends its lifetime first).
 struct PoolScope {
     DevPool& pool;
     hipStream_t st;
-    std::vector<DevBuf*> bufs;
+    std::vector<DevBuf> owned;
     PoolScope(DevPool& p, hipStream_t s) : pool(p), st(s) {}
     PoolScope(const PoolScope&) = delete;
     PoolScope& operator=(const PoolScope&) = delete;
+    // `b` must be empty: one take per buffer and scope
     hipError_t take(DevBuf& b, size_t need) {
-        bufs.push_back(&b);
-        return pool.take(b, need);
+        if (b.p) return hipErrorInvalidValue;
+        hipError_t e = pool.take(b, need);
+        if (e == hipSuccess) owned.push_back(b);
+        return e;
     }
     ~PoolScope() {
         (void)hipStreamSynchronize(st);
-        for (DevBuf* b : bufs) pool.give(*b);
+        for (DevBuf& b : owned) pool.give(b);
     }
 };
 

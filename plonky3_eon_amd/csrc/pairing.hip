@@ -559,8 +559,8 @@ void fq12_to_abi(const Fq12& a, eon_fq12& out) {
 
 // product of the pairings of m device pairs -> Gt element and the is-one flag (host)
 Status pair_product(eon_ctx* ctx, const G1Affine* P, const G2Affine* Q, uint32_t m, Fq12* gt, bool* one) {
-    PoolScope ps(ctx->pool, ctx->stream);
     DevBuf f, res;
+    PoolScope ps(ctx->pool, ctx->stream);
     EON_HIP(ps.take(f, (size_t)std::max<uint32_t>(m, 1) * sizeof(Fq12)));
     EON_HIP(ps.take(res, sizeof(Fq12) + 16));
     ctx->prof.begin("k_miller_team", (uint64_t)m * (64 + 128 + 384), ctx->stream);
@@ -603,8 +603,8 @@ int eon_g2_mul(eon_ctx* ctx, const eon_g2_affine* base, const eon_fr* k, eon_g2_
         if (base) EON_TRY(g2_from_abi(*base, b));
         const Fr kk = fr_from_abi(k);
         if (!fr_is_canonical(kk)) return Status::err(EON_E_ARG, "scalar is not a canonical Fr");
-        PoolScope ps(ctx->pool, ctx->stream);
         DevBuf d;
+        PoolScope ps(ctx->pool, ctx->stream);
         EON_HIP(ps.take(d, sizeof(G2Affine)));
         hipLaunchKernelGGL(k_g2_mul, dim3(1), dim3(64), 0, ctx->stream, b, kk, d.as<G2Affine>());
         EON_HIP(hipGetLastError());
@@ -630,8 +630,8 @@ int eon_multi_pairing(eon_ctx* ctx, const eon_g1_affine* p, const eon_g2_affine*
             EON_TRY(g1_from_abi(p[i], hp[i]));
             EON_TRY(g2_from_abi(q[i], hq[i]));
         }
-        PoolScope ps(ctx->pool, ctx->stream);
         DevBuf dp, dq;
+        PoolScope ps(ctx->pool, ctx->stream);
         EON_HIP(ps.take(dp, std::max<uint64_t>(n, 1) * sizeof(G1Affine)));
         EON_HIP(ps.take(dq, std::max<uint64_t>(n, 1) * sizeof(G2Affine)));
         if (n) {
@@ -691,8 +691,8 @@ int eon_kzg_verify_batch(eon_ctx* ctx, const eon_g1_affine* commitments, const e
             std::vector<uint32_t> fill(gs.begin(), gs.end() - 1);
             for (uint64_t i = 0; i < n; i++) ord[fill[grp[i]]++] = (uint32_t)i;
         }
-        PoolScope ps(ctx->pool, ctx->stream);
         DevBuf dc, dw, dv, dord, dgs, dz, dsums, dvsum, dP, dQ;
+        PoolScope ps(ctx->pool, ctx->stream);
         EON_HIP(ps.take(dc, n * sizeof(G1Affine)));
         EON_HIP(ps.take(dw, n * sizeof(G1Affine)));
         EON_HIP(ps.take(dv, n * sizeof(Fr)));

@@ -69,6 +69,17 @@ class Context:
         self.check(self.lib.eon_ctx_profile_report(self._h, buf, len(buf)))
         return json.loads(buf.value.decode())
 
+    def trim(self):
+        """Give the context's cached idle device buffers back (eon_ctx_trim)."""
+        self.check(self.lib.eon_ctx_trim(self._h))
+
+    def clock_probe(self, launches: int = 160, iters: int = 1024) -> dict:
+        """Diagnostic (eon_diag_clock_probe): the in-kernel shader clock under a radix-2^29
+        product chain and the product rate at that clock, on this context's stream."""
+        r = _lib.eon_clock_probe()
+        self.check(self.lib.eon_diag_clock_probe(self._h, int(launches), int(iters), ctypes.byref(r)))
+        return {k: getattr(r, k) for k, _ in r._fields_}
+
     def close(self):
         if getattr(self, "_h", None):
             self.lib.eon_ctx_destroy(self._h)

@@ -162,11 +162,12 @@ def test_poseidon2_vl8_generic_equals_fused_2_12(gpu_ctx):
     assert prog.num_constraints == 1280 and air.width == 1312
     log_n, log_qd = 12, 1
     q = 1 << (log_n + log_qd)
-    g = torch.Generator(device="cuda:0")
-    g.manual_seed(1212)
-    lde = torch.randint(-(1 << 63), (1 << 63) - 1, (q, air.width, 4), generator=g, device="cuda:0", dtype=torch.int64)
-    lde[..., 3] &= (1 << 60) - 1
-    alpha = 0x0123456789ABCDEF0123
+    # full-range canonical residues (the top limb unmasked: values up to p - 1, so the interpreter's
+    # 12p reduce threshold and the fused kernel's bounds see their worst operands)
+    host_lde = C.random_fr(1212, q * air.width).reshape(q, air.width, 4)
+    host_lde[::7, ::5] = np.array(O.int_to_limbs(P - 1), dtype=np.uint64)
+    lde = torch.from_numpy(host_lde.view(np.int64)).to("cuda:0")
+    alpha = O.from_mont(P - 1)  # stored residue p - 1
     generic = prog.quotient_values(lde, log_n, log_qd, alpha)
     fused = air.quotient_values(lde, log_n, log_qd, alpha)
     assert torch.equal(generic, fused)  # the fused kernel is oracle-checked at VECTOR_LEN 1/2/8
@@ -195,6 +196,9 @@ def test_program_rejects_bad_input(gpu_ctx):
     assert create([(6, 0, 0)]) == _lib.EON_E_ARG  # operand does not precede its user
     assert create([(1, 5, 0)]) == _lib.EON_E_ARG  # column out of range
     assert create([(2, 0, 0)]) == _lib.EON_E_ARG  # public index out of range (no publics)
+    # operand indices are 28 bits (bit 28 is the raw flag): wider widths / slot counts are shape errors
+    assert create([(1, 0, 0)], width=1 << 28) == _lib.EON_E_SHAPE
+    assert create([(1, 0, 0)], width=2, npub=(1 << 28) - 1) == _lib.EON_E_SHAPE
     prog = AirProgram(FibonacciAir(), gpu_ctx)
     lde = torch.zeros((8, 2, 4), dtype=torch.int64, device="cuda:0")
     with pytest.raises(_lib.EonError) as e:
@@ -350,3 +354,70 @@ def test_mul_air_prove_vs_oracle_and_verify(gpu_ctx, ch_consts, log_n, valid):
     for p in range(2):
         np.testing.assert_array_equal(proof.opened[0].values[0][p], want["trace_open"][0][p])
         np.testing.assert_array_equal(proof.opened[0].witnesses[0][p], want["trace_open"][1][p])
+
+
+PM1 = np.array(O.int_to_limbs(P - 1), dtype=np.uint64)
+
+
+def extreme_lde(kind, rows, width, seed):
+    out = np.zeros((rows, width, 4), dtype=np.uint64)
+    if kind == "pm1":
+        out[:] = PM1
+    elif kind == "alt":
+        out[(np.add.outer(np.arange(rows), np.arange(width)) % 2) == 0] = PM1
+    elif kind == "alt_rows":
+        out[::2] = PM1
+    else:
+        out[:] = C.random_fr(seed, rows * width).reshape(rows, width, 4)
+        out[np.random.default_rng(seed).random((rows, width)) < 0.25] = PM1
+    return out
+
+
+@pytest.mark.parametrize("kind", ["pm1", "alt", "alt_rows", "rand_pm1"])
+def test_generic_quotient_extreme_mixed(gpu_ctx, kind):
+    """k_air_quotient's bound tracking (reduce above 12p, raw leaves of bound 32, K p offsets of the
+    differences) at its worst operands: every LDE cell, public value and alpha stored as p - 1, or
+    p - 1 next to 0, against the oracle's fully reduced fold (MixedAir: every node kind, degree 7)."""
+    import torch
+
+    from plonky3_eon_amd.air import AirProgram
+
+    prog = AirProgram(MixedAir(), gpu_ctx)
+    for log_n, log_qd in ((3, 3), (2, 1)):
+        q = 1 << (log_n + log_qd)
+        lde = extreme_lde(kind, q, prog.width, 5 + log_n)
+        for pub, alpha in (([P - 1, P - 1], P - 1), ([0, P - 1], 0x1234567890ABCDEF1234567)):
+            # public values and alpha are canonical ints given in the Montgomery domain by the
+            # binding; P - 1 as a residue is from_mont(P - 1)
+            pub_i = [O.from_mont(v) for v in pub]
+            alpha_i = O.from_mont(alpha) if alpha == P - 1 else alpha
+            got = prog.quotient_values(torch.from_numpy(lde.view(np.int64)).to("cuda:0"), log_n, log_qd, alpha_i, pub_i)
+            got = ints(got.cpu().numpy().view(np.uint64))
+            want = O.quotient_values_fn([ints(r) for r in lde], log_n, log_qd, mixed_constraints, alpha_i, pub_i)
+            assert got == want, (kind, log_n, pub, hex(alpha))
+
+
+@pytest.mark.parametrize("vl", [1, 8])
+@pytest.mark.parametrize("kind", ["pm1", "alt", "rand_pm1"])
+def test_generic_quotient_extreme_poseidon2(gpu_ctx, vl, kind):
+    """The Poseidon2-AIR through the generic program at worst-case LDE values, with every round
+    constant stored as p - 1, against the C oracle (VECTOR_LEN 1 and 8)."""
+    import torch
+
+    from plonky3_eon_amd.air import AirProgram, Poseidon2Air
+
+    hf, pr = 4, 56
+    k = C.P2Constants([[PM1.copy() for _ in range(3)] for _ in range(hf)], [PM1.copy() for _ in range(pr)],
+                      [[PM1.copy() for _ in range(3)] for _ in range(hf)])
+    air = Poseidon2Air(k.begin, k.partial, k.end, vl, gpu_ctx)
+    prog = AirProgram(air, gpu_ctx)
+    log_n, log_qd = 3, 1
+    q = 1 << (log_n + log_qd)
+    lde = extreme_lde(kind, q, air.width, 70 + vl)
+    dev = torch.from_numpy(lde.view(np.int64)).to("cuda:0")
+    alpha_i = O.from_mont(P - 1)
+    generic = prog.quotient_values(dev, log_n, log_qd, alpha_i).cpu().numpy().view(np.uint64)
+    want = C.p2_quotient_values(lde, log_n, log_qd, vl, k, PM1)
+    np.testing.assert_array_equal(generic, want)
+    fused = air.quotient_values(dev, log_n, log_qd, alpha_i).cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(fused, want)

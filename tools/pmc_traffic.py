@@ -9,6 +9,7 @@ usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <kernel-substring> <w
 import csv
 import glob
 import json
+import os
 import sys
 
 
@@ -41,6 +42,7 @@ def main():
         "write_size_kb_per_launch": w_kb,
         "bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024),
         "correction": "bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (gfx950 FETCH_SIZE halves wide reads)",
+        "commit": os.environ.get("EON_COMMIT", "unknown"),
     }
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))

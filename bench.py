@@ -443,8 +443,8 @@ class ProveWorkload:
     by vector lane over the ranks (plonky3_eon_amd/distributed.py): strong scaling.
 
     The prove runs in the C++ driver (libeonprove.so, include/eon_prove.h; at N > 1 its
-    all-gathers go through torch.distributed's RCCL group or, --collective rccl, its own
-    communicator)."""
+    all-gathers go through its own RCCL communicator, or torch.distributed's process group when the
+    ranks share a GPU / with --collective torch)."""
 
     scaling = "strong"
 
@@ -487,9 +487,17 @@ class ProveWorkload:
         if self.emulate > 1:
             self.coll = EmulatedCollective(0, self.emulate)
         elif world > 1:
-            # torch's RCCL process group (all_gather_into_tensor on device) by default; the
-            # driver's own communicator with --collective rccl
-            self.coll = (RcclCollective(rank, world) if args.collective == "rccl"
+            # the driver's own RCCL communicator (ncclAllGather on the eon stream, called from the
+            # C++ driver thread: no Python on the exchange path) when every rank has its own GPU;
+            # torch.distributed's process group (a ctypes callback into Python per exchange) when
+            # the ranks share a device (EON_BENCH_ONE_DEVICE rehearsals: RCCL refuses two ranks on
+            # one GPU) or with --collective torch
+            kind = args.collective
+            if kind == "auto":
+                shared = os.environ.get("EON_BENCH_ONE_DEVICE") == "1"
+                kind = "torch" if shared or os.environ.get("EON_BENCH_BACKEND", "nccl") != "nccl" else "rccl"
+            self.collective_kind = kind
+            self.coll = (RcclCollective(rank, world) if kind == "rccl"
                          else TorchCollective(rank, world, None, device=dev.index))
         # the same 2^(log_n) x VECTOR_LEN permutation inputs on every rank; rank g takes its lanes
         # (permutation j sits at row j / VECTOR_LEN, lane j % VECTOR_LEN)
@@ -513,7 +521,7 @@ class ProveWorkload:
 
     def describe(self, world):
         w = 164 * self.vl
-        par = f"lane-shard x{world}" if world > 1 else "single"
+        par = f"lane-shard x{world} ({getattr(self, 'collective_kind', 'torch')} collective)" if world > 1 else "single"
         if self.emulate > 1:
             par = (f"EMULATED rank 0 of lane-shard x{self.emulate} on one GPU (its lanes and the full "
                    f"transcript; exchanges replaced by local device copies; not a valid proof)")
@@ -831,9 +839,11 @@ def make_parser() -> argparse.ArgumentParser:
                     help="prove: time rank 0 of an N-rank lane-sharded prove on this one GPU (its lanes, "
                          "the full replicated transcript, local copies for the exchanges) -- a per-rank "
                          "proxy, not a multi-GPU measurement")
-    ap.add_argument("--collective", choices=["torch", "rccl"], default="torch",
-                    help="prove at N > 1: all-gathers through torch.distributed (RCCL "
-                         "process group) or the driver's own RCCL communicator")
+    ap.add_argument("--collective", choices=["auto", "torch", "rccl"], default="auto",
+                    help="prove at N > 1: all-gathers through the driver's own RCCL communicator "
+                         "(rccl: no Python on the exchange path; the default with one GPU per rank) or "
+                         "torch.distributed's process group (torch: a ctypes callback per exchange; the "
+                         "default when the ranks share one device, which RCCL refuses)")
     return ap
 
 

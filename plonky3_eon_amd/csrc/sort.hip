@@ -27,6 +27,10 @@
 namespace eon {
 namespace {
 
+// predecessor status words loaded at once by the decoupled look-back (1: one at a time)
+#ifndef EON_SORT_LB
+#define EON_SORT_LB 1
+#endif
 constexpr uint32_t SORT_THREADS = 512, SORT_WAVES = SORT_THREADS / 64, SORT_ITEMS = 16;
 constexpr uint32_t SORT_TILE = SORT_THREADS * SORT_ITEMS;
 constexpr uint64_t ST_AGG = 1ull << 62, ST_INC = 2ull << 62, ST_COUNT = (1ull << 62) - 1;
@@ -156,12 +160,18 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
             key[j] = (FULL || i < n) ? ks[i] : 0u;
             val[j] = (FULL || i < n) ? vs[i] : 0u;
         }
-        const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll
         for (uint32_t j = 0; j < SORT_ITEMS; j++) {
             const bool valid = FULL || wbase + j * 64 + lane < n;
             const uint32_t d = (key[j] >> shift) & dmask;
-            uint64_t eq = __ballot(valid);
+            // the lanes holding the same digit: per digit bit, the ballot m of the bit and this
+            // lane's bit as an all-ones / zero word s; eq &= m XNOR s on 32-bit halves (the
+            // compiler folds the bits with v_xor / v_or3 / v_bitop3: ~5 VALU per bit, against ~10
+            // for the 64-bit select form bit ? m : ~m)
+            const uint64_t vm = __ballot(valid);
+            uint32_t eq_lo = (uint32_t)vm, eq_hi = (uint32_t)(vm >> 32);
+#ifdef EON_SORT_OLD_RANK  // A/B only: the round-4 64-bit select form
+            uint64_t eq = vm;
 #pragma unroll
             for (uint32_t b = 0; b < 8; b++) {
                 if (b < dbits) {
@@ -170,10 +180,24 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
                     eq &= bit ? m : ~m;
                 }
             }
-            const uint32_t before = __popcll(eq & lt);
+            eq_lo = (uint32_t)eq;
+            eq_hi = (uint32_t)(eq >> 32);
+#else
+#pragma unroll
+            for (uint32_t b = 0; b < 8; b++) {
+                if (b < dbits) {
+                    const int32_t sb = (int32_t)(d << (31 - b)) >> 31;
+                    const uint64_t m = __ballot(sb != 0);
+                    eq_lo &= ~((uint32_t)m ^ (uint32_t)sb);
+                    eq_hi &= ~((uint32_t)(m >> 32) ^ (uint32_t)sb);
+                }
+            }
+#endif
+            // lanes below this one in the group (v_mbcnt), and the group's size
+            const uint32_t before = __builtin_amdgcn_mbcnt_hi(eq_hi, __builtin_amdgcn_mbcnt_lo(eq_lo, 0u));
             const uint32_t old = valid ? cnt[w][d] : 0u;
             // every lane of the group has read the counter before its lowest lane moves it
-            if (valid && before == 0) cnt[w][d] = old + (uint32_t)__popcll(eq);
+            if (valid && before == 0) cnt[w][d] = old + (uint32_t)(__popc(eq_lo) + __popc(eq_hi));
             rk[j] = old + before;
             __builtin_amdgcn_wave_barrier();
         }
@@ -205,15 +229,38 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
         }
         if (tid < 256) {
             uint32_t excl = 0;
+#ifndef EON_SORT_PROBE_NOLOOKBACK
             if (tile > 0) {
+#if EON_SORT_LB > 1
+                // EON_SORT_LB predecessors' status words in flight at once, consumed in order
+                bool done = false;
+                for (int64_t k = (int64_t)tile - 1; !done && k >= 0; k -= EON_SORT_LB) {
+                    uint64_t v[EON_SORT_LB];
+#pragma unroll
+                    for (int q = 0; q < EON_SORT_LB; q++)
+                        v[q] = k - q >= 0 ? ld_status(status + (size_t)(k - q) * 256 + tid) : ST_INC;
+#pragma unroll
+                    for (int q = 0; q < EON_SORT_LB; q++) {
+                        if (done) break;
+                        while ((v[q] >> 62) == 0) {
+                            __builtin_amdgcn_s_sleep(1);
+                            v[q] = ld_status(status + (size_t)(k - q) * 256 + tid);
+                        }
+                        excl += (uint32_t)(v[q] & ST_COUNT);
+                        if (v[q] & ST_INC) done = true;
+                    }
+                }
+#else
                 for (uint32_t k = tile - 1;; k--) {
                     uint64_t v;
                     while (((v = ld_status(status + (size_t)k * 256 + tid)) >> 62) == 0) __builtin_amdgcn_s_sleep(1);
                     excl += (uint32_t)(v & ST_COUNT);  // a digit's running count is below n < 2^32
                     if (v & ST_INC) break;
                 }
+#endif
                 st_status(status + (size_t)tile * 256 + tid, ST_INC | (uint64_t)(excl + tcount));
             }
+#endif
             goff[tid] = base[tid] + excl;
         }
         __syncthreads();
@@ -222,8 +269,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
             const uint32_t k = sk[i];
             const uint32_t d = (k >> shift) & dmask;
             const uint32_t dst = goff[d] + i - tstart[d];
-            kd[dst] = k;
-            vd[dst] = sv[i];
+            if (dst < n) {  // always, for a consistent ranking: the output is never written out of range
+                kd[dst] = k;
+                vd[dst] = sv[i];
+            }
         }
     };
     if (t0 + SORT_TILE <= n)

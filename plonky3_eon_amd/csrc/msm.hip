@@ -693,6 +693,56 @@ __global__ void __launch_bounds__(64) k_segment_reduce29(const G1Raw29* pieces, 
     st_xyzz(seg_out + t, x29_to_xyzz(acc, acc_inf));
 }
 
+// Few groups with several pieces per bucket (a single 2^20 MSM: ~4.5), round 5.  Two short,
+// wide kernels instead of combine level + bucket final + k_segment_sum in radix 2^32:
+//   k_bucket_sums29   one thread per bucket (the whole MSM's buckets: 4 waves per SIMD at 2^18)
+//                     sums its raw pieces -> raw bucket sum, group-major (g B + m)
+//   k_segment_sum29   one thread per segment of SEG buckets: running sums of the bucket sums
+//                     plus lo times their total by double-and-add, in radix 2^29 -> XYZZ
+// then the k_tree_sum levels as before.  The sums are the same group elements as the combine path
+// (exact EC arithmetic; only the order of additions differs).
+__global__ void __launch_bounds__(256) k_bucket_sums29(const G1Raw29* pieces, const uint32_t* piece_off, uint32_t B,
+                                                      uint32_t groups, G1Raw29* sums) {
+    const uint32_t bp = blockIdx.x * blockDim.x + threadIdx.x;  // b' = m groups + g
+    if (bp >= B * groups) return;
+    G1X29 run, x;
+    bool run_inf = true;
+    const uint32_t e1 = piece_off[bp + 1];
+    for (uint32_t e = piece_off[bp]; e < e1; e++) {
+        const bool inf = ld_raw29(pieces + e, x);
+        acc29(run, run_inf, x, inf);
+    }
+    const uint32_t g = bp % groups, m = bp / groups;
+    st_point(sums + (uint64_t)g * B + m, run, run_inf);
+}
+
+__global__ void __launch_bounds__(64) k_segment_sum29(const G1Raw29* sums, uint32_t B, uint32_t groups,
+                                                      G1Xyzz* seg_out) {
+    const uint32_t nseg = B / SEG;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nseg * groups) return;
+    const uint32_t g = t / nseg, s = t % nseg;
+    const uint32_t lo = s * SEG;
+    const G1Raw29* sb = sums + (uint64_t)g * B + lo;
+    G1X29 run, acc, x;
+    bool run_inf = true, acc_inf = true;
+    for (int k = (int)SEG - 1; k >= 0; k--) {  // bucket lo + k holds digit lo + k + 1
+        const bool inf = ld_raw29(sb + k, x);
+        acc29(run, run_inf, x, inf);
+        acc29(acc, acc_inf, run, run_inf);
+    }
+    if (lo && !run_inf) {  // acc += lo * run (double-and-add, MSB first)
+        G1X29 m;
+        bool m_inf = true;
+        for (int bit = 31 - __builtin_clz(lo); bit >= 0; bit--) {
+            if (!m_inf) dbl29(m);
+            if ((lo >> bit) & 1) acc29(m, m_inf, run, false);
+        }
+        acc29(acc, acc_inf, m, m_inf);
+    }
+    st_xyzz(seg_out + t, x29_to_xyzz(acc, acc_inf));
+}
+
 // out[g * gridDim.x + blk] = sum of in[g * n + blk * TREE .. + TREE)
 __global__ void __launch_bounds__(TREE) k_tree_sum(const G1Xyzz* in, uint32_t n, G1Xyzz* out) {
     __shared__ G1Xyzz sh[TREE];
@@ -754,6 +804,9 @@ __global__ void k_batch_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out) {
 }
 
 static uint32_t choose_c(uint64_t n, bool precomputed) {
+#ifdef EON_MSM_C_OVERRIDE  // tuning builds: the window of single fixed-base MSMs of >= 2^18 terms
+    if (precomputed && n >= (1ull << 18)) return EON_MSM_C_OVERRIDE;
+#endif
     // minimise mixed additions n * ceil(255 / c) plus the bucket reduction, ~6 full additions
     // per bucket (per window when the windows keep their own buckets)
     uint32_t best = 4;
@@ -983,6 +1036,10 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     EON_HIP(wk.temp.ensure(std::max(bt.sort_bytes, bt.scan_bytes)));
     bt.log_chunk = LOG_CHUNK_MIN;
     while (bt.log_chunk < LOG_CHUNK_MAX && (E >> (bt.log_chunk + 1)) >= (1ull << 20)) bt.log_chunk++;
+    // few buckets for many pairs (a bucket would collect more than ~8 pieces): longer chunks while
+    // the piece sums keep 2^18 threads (4 waves per SIMD)
+    while (bt.log_chunk < LOG_CHUNK_MAX && (E >> bt.log_chunk) > 8ull * nb && (E >> (bt.log_chunk + 1)) >= (1ull << 18))
+        bt.log_chunk++;
     bt.max_pieces = (E >> bt.log_chunk) + nb + 1;  // >= the real piece count
     if (!wk.host_counts) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&wk.host_counts), 64));
 
@@ -1048,10 +1105,19 @@ static bool fused_reduce(const Batch& bt) {
            (bt.groups >= 64 || (uint64_t)bt.n_pieces <= 2ull * bt.nb);
 }
 
+// few groups, several pieces per bucket, none above PIECE: k_bucket_sums29 + k_segment_sum29
+// (round 5; the combine-level path stays for skewed inputs, whose buckets hold more pieces)
+#ifndef EON_MSM_SUMS29
+#define EON_MSM_SUMS29 1
+#endif
+static bool sums_reduce(const Batch& bt) {
+    return EON_MSM_SUMS29 && bt.levels <= 1 && bt.B >= SEG && bt.groups < 64 && !fused_reduce(bt);
+}
+
 // piece sums of one sorted batch against bases `b` (asynchronous); wk supplies the piece buffers
 static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt, const SortedRef& sr,
                            MsmWork& wk, hipStream_t st) {
-    EON_HIP(wk.piece_sums.ensure(bt.max_pieces * sizeof(G1Xyzz)));
+    EON_HIP(wk.piece_sums.ensure(std::max<uint64_t>(bt.max_pieces * sizeof(G1Xyzz), (uint64_t)bt.nb * sizeof(G1Raw29))));
     EON_HIP(wk.piece_sums2.ensure(bt.max_pieces * sizeof(G1Xyzz)));
     EON_HIP(wk.owner.ensure(bt.max_pieces * 4));
     EON_HIP(wk.bucket_sums.ensure((uint64_t)bt.nb * sizeof(G1Xyzz)));
@@ -1075,7 +1141,7 @@ static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt
         hipLaunchKernelGGL(k_piece_sum29, dim3(blocks), dim3(64), 0, st, sr.keys, sr.vals, sr.start, sr.piece_off,
                            bt.n_pairs, bt.log_chunk, bt.c, bt.groups, bt.nb, pts, wk.piece_raw.as<G1Raw29>());
     ctx->prof.end(st);
-    if (bt.n_pieces && !fused_reduce(bt))
+    if (bt.n_pieces && !fused_reduce(bt) && !sums_reduce(bt))
         hipLaunchKernelGGL(k_raw29_to_xyzz, dim3(blocks_for(bt.n_pieces, 128)), dim3(128), 0, st,
                            wk.piece_raw.as<G1Raw29>(), bt.n_pieces, wk.piece_sums.as<G1Xyzz>());
     EON_HIP(hipGetLastError());
@@ -1099,13 +1165,17 @@ static Status write_columns(const MsmLayout& L, const Batch& bt, const G1Xyzz* p
 
 // sum_d d * B_d per group, few-groups form: k_segment_sum + LDS trees (short dependency chains)
 static Status reduce_segments(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, const SortedRef& sr,
-                              MsmWork& wk, hipStream_t st, bool fused) {
+                              MsmWork& wk, hipStream_t st, bool fused, bool sums29 = false) {
     const uint32_t nseg = bt.B / SEG;  // c >= 4, so B >= SEG
     const uint32_t groups = bt.groups;
     EON_HIP(wk.red_a.ensure((uint64_t)groups * nseg * sizeof(G1Xyzz)));
     EON_HIP(wk.red_b.ensure((uint64_t)groups * nseg * sizeof(G1Xyzz)));
     ctx->prof.begin("k_segment_sum", (uint64_t)bt.nb * 128 + (uint64_t)groups * nseg * 128, st);
-    if (fused)
+    if (sums29) {
+        // raw bucket sums (k_bucket_sums29, in wk.piece_sums as G1Raw29) -> segment sums
+        hipLaunchKernelGGL(k_segment_sum29, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
+                           wk.piece_sums.as<G1Raw29>(), bt.B, groups, wk.red_a.as<G1Xyzz>());
+    } else if (fused)
         hipLaunchKernelGGL(k_segment_reduce29, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
                            wk.piece_raw.as<G1Raw29>(), sr.piece_off, bt.B, groups, wk.red_a.as<G1Xyzz>());
     else
@@ -1196,6 +1266,14 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
         EON_HIP(hipGetLastError());
         df->rows.emplace_back(row0, groups);
         return Status::ok();
+    }
+    if (!fused && sums_reduce(bt)) {
+        prof->begin("k_bucket_sums29", (uint64_t)bt.n_pieces * 144 + (uint64_t)nb * 144, st);
+        hipLaunchKernelGGL(k_bucket_sums29, dim3(blocks_for(nb, 256)), dim3(256), 0, st, wk.piece_raw.as<G1Raw29>(),
+                           sr.piece_off, B, groups, wk.piece_sums.as<G1Raw29>());
+        prof->end(st);
+        EON_HIP(hipGetLastError());
+        return reduce_segments(ctx, L, bt, sr, wk, st, false, true);
     }
     // combine levels until every bucket holds one partial (skewed scalars put many pieces in a
     // bucket: all-equal scalars put n pieces in one bucket per window)

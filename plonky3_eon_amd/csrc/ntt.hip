@@ -82,11 +82,15 @@ __device__ __forceinline__ F29 lds_get29(const uint4* lo, const uint4* hi, const
     return x;
 }
 
-template <bool DIF, int LOG_CB>
+// KS > 0: the pass's stage count as a compile-time constant, launched with exactly CB 2^KS / 2
+// threads (one butterfly per thread and stage): the stage loop unrolls, its index arithmetic folds
+// to constants and the lazy / normalising stage choice is resolved at compile time.  KS = 0 reads
+// the count from the arguments (any block size).
+template <bool DIF, int LOG_CB, int KS = 0>
 __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
     constexpr uint32_t CB = 1u << LOG_CB;
     extern __shared__ __attribute__((aligned(16))) uint4 lds[];
-    const uint32_t k = a.k;
+    const uint32_t k = KS ? (uint32_t)KS : a.k;
     const uint32_t ne = CB << k;
     uint4* lo = lds;
     uint4* hi = lds + ne;
@@ -110,7 +114,7 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
     const uint64_t base_row = low + ((g >> s0) << (s0 + k));
     const uint64_t col0 = (uint64_t)(blockIdx.x % a.col_tiles) * CB;
     const uint64_t width = a.width;
-    const uint32_t T = blockDim.x;
+    const uint32_t T = KS ? (CB << KS) / 2 : blockDim.x;
 
     for (uint32_t q = threadIdx.x + 1; q < (1u << k); q += T) {
         const uint32_t l = 31 - __builtin_clz(q);
@@ -169,7 +173,8 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         pin29(w);
         return w;
     };
-    for (uint32_t it = 0; it < k; it++) {
+#pragma unroll
+    for (uint32_t it = 0; it < (KS ? (uint32_t)KS : k); it++) {
         const uint32_t l = DIF ? (k - 1 - it) : it;
         const uint32_t half = 1u << l;
         for (uint32_t b = threadIdx.x; b < (ne >> 1); b += T) {
@@ -279,6 +284,7 @@ __global__ void k_tw_shoup(Fr* tw, uint32_t* twq, uint64_t n) {
     q[0] = make_uint4(wq.l[0], wq.l[1], wq.l[2], wq.l[3]);
     q[1] = make_uint4(wq.l[4], wq.l[5], wq.l[6], wq.l[7]);
     q[2] = make_uint4(wq.l[8], 0u, 0u, 0u);
+
 }
 
 // tw[2^s + j] = tw[2^(L-1) + (j << (L-1-s))] for s < L-1 (sub-sampling the largest stage).
@@ -291,6 +297,10 @@ __global__ void k_tw_fill_lower(Fr* tw, uint32_t L) {
     tw[q] = tw[top + (j << (L - 1 - s))];
 }
 
+#ifndef EON_NTT_FIXED_K
+#define EON_NTT_FIXED_K 1
+#endif
+
 static hipError_t launch_pass(bool dif, uint32_t log_cb, const PassArgs& a, uint64_t groups,
                               uint64_t col_tiles, uint32_t max_threads, hipStream_t st) {
     const uint32_t ne = (1u << log_cb) << a.k;
@@ -302,6 +312,21 @@ static hipError_t launch_pass(bool dif, uint32_t log_cb, const PassArgs& a, uint
     const size_t lds = (((size_t)ne * 36 + 15) & ~(size_t)15) + 2 * (size_t)tw_set_bytes(1u << a.k);
     dim3 grid((unsigned)(groups * col_tiles));
 #define EON_LAUNCH(D, C) hipLaunchKernelGGL((k_ntt_pass29<D, C>), grid, dim3(threads), lds, st, a)
+#define EON_LAUNCH_K(D, KK) hipLaunchKernelGGL((k_ntt_pass29<D, 3, KK>), grid, dim3((8u << KK) / 2), lds, st, a)
+#if EON_NTT_FIXED_K
+    // the network shapes of the prove and the LDE (8-column tiles of 2^5 .. 2^7 rows)
+    if (log_cb == 3 && a.k >= 5 && a.k <= 7 && threads == ne / 2) {
+        switch ((dif ? 8 : 0) + a.k) {
+            case 5: EON_LAUNCH_K(false, 5); break;
+            case 6: EON_LAUNCH_K(false, 6); break;
+            case 7: EON_LAUNCH_K(false, 7); break;
+            case 13: EON_LAUNCH_K(true, 5); break;
+            case 14: EON_LAUNCH_K(true, 6); break;
+            case 15: EON_LAUNCH_K(true, 7); break;
+        }
+        return hipGetLastError();
+    }
+#endif
     switch ((dif ? 4 : 0) + log_cb) {
         case 0: EON_LAUNCH(false, 0); break;
         case 1: EON_LAUNCH(false, 1); break;
@@ -313,6 +338,7 @@ static hipError_t launch_pass(bool dif, uint32_t log_cb, const PassArgs& a, uint
         case 7: EON_LAUNCH(true, 3); break;
     }
 #undef EON_LAUNCH
+#undef EON_LAUNCH_K
     return hipGetLastError();
 }
 

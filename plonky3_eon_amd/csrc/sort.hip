@@ -27,6 +27,10 @@
 namespace eon {
 namespace {
 
+// EON_SORT_EARLY_AGG: publish the tile's digit counts before ranking (see k_sort_pass)
+#ifndef EON_SORT_EARLY_AGG
+#define EON_SORT_EARLY_AGG 0
+#endif
 // predecessor status words loaded at once by the decoupled look-back (1: one at a time)
 #ifndef EON_SORT_LB
 #define EON_SORT_LB 1
@@ -145,6 +149,9 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t dmask = (1u << dbits) - 1;
     for (uint32_t i = tid; i < SORT_WAVES * 256; i += SORT_THREADS) (&cnt[0][0])[i] = 0;
+#if EON_SORT_EARLY_AGG
+    if (tid < 256) goff[tid] = 0;  // the tile's digit histogram until the look-back fills it
+#endif
     if (tid == 0) misc[0] = atomicAdd(tile_ctr, 1u);
     __syncthreads();
     const uint32_t tile = misc[0];
@@ -160,6 +167,16 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
             key[j] = (FULL || i < n) ? ks[i] : 0u;
             val[j] = (FULL || i < n) ? vs[i] : 0u;
         }
+#if EON_SORT_EARLY_AGG
+        // the tile's digit counts first (LDS atomics), published before the ranking: the next
+        // tiles' look-backs find this tile's aggregate while it is still ranking, instead of
+        // waiting for it
+#pragma unroll
+        for (uint32_t j = 0; j < SORT_ITEMS; j++)
+            if (FULL || wbase + j * 64 + lane < n) atomicAdd(&goff[(key[j] >> shift) & dmask], 1u);
+        __syncthreads();
+        if (tid < 256) st_status(status + (size_t)tile * 256 + tid, (tile == 0 ? ST_INC : ST_AGG) | (uint64_t)goff[tid]);
+#endif
 #pragma unroll
         for (uint32_t j = 0; j < SORT_ITEMS; j++) {
             const bool valid = FULL || wbase + j * 64 + lane < n;
@@ -211,8 +228,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
                 cnt[v][tid] = tcount;
                 tcount += c;
             }
+#if !EON_SORT_EARLY_AGG
             // publish this tile's counts before anything else, so the next tiles can look back
             st_status(status + (size_t)tile * 256 + tid, (tile == 0 ? ST_INC : ST_AGG) | (uint64_t)tcount);
+#endif
         }
         uint32_t tot;
         const uint32_t ts = scan256(tid < 256 ? tcount : 0u, misc + 4, tot);

@@ -27,14 +27,6 @@
 namespace eon {
 namespace {
 
-// EON_SORT_EARLY_AGG: publish the tile's digit counts before ranking (see k_sort_pass)
-#ifndef EON_SORT_EARLY_AGG
-#define EON_SORT_EARLY_AGG 0
-#endif
-// predecessor status words loaded at once by the decoupled look-back (1: one at a time)
-#ifndef EON_SORT_LB
-#define EON_SORT_LB 1
-#endif
 constexpr uint32_t SORT_THREADS = 512, SORT_WAVES = SORT_THREADS / 64, SORT_ITEMS = 16;
 constexpr uint32_t SORT_TILE = SORT_THREADS * SORT_ITEMS;
 constexpr uint64_t ST_AGG = 1ull << 62, ST_INC = 2ull << 62, ST_COUNT = (1ull << 62) - 1;
@@ -149,9 +141,6 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t dmask = (1u << dbits) - 1;
     for (uint32_t i = tid; i < SORT_WAVES * 256; i += SORT_THREADS) (&cnt[0][0])[i] = 0;
-#if EON_SORT_EARLY_AGG
-    if (tid < 256) goff[tid] = 0;  // the tile's digit histogram until the look-back fills it
-#endif
     if (tid == 0) misc[0] = atomicAdd(tile_ctr, 1u);
     __syncthreads();
     const uint32_t tile = misc[0];
@@ -167,16 +156,6 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
             key[j] = (FULL || i < n) ? ks[i] : 0u;
             val[j] = (FULL || i < n) ? vs[i] : 0u;
         }
-#if EON_SORT_EARLY_AGG
-        // the tile's digit counts first (LDS atomics), published before the ranking: the next
-        // tiles' look-backs find this tile's aggregate while it is still ranking, instead of
-        // waiting for it
-#pragma unroll
-        for (uint32_t j = 0; j < SORT_ITEMS; j++)
-            if (FULL || wbase + j * 64 + lane < n) atomicAdd(&goff[(key[j] >> shift) & dmask], 1u);
-        __syncthreads();
-        if (tid < 256) st_status(status + (size_t)tile * 256 + tid, (tile == 0 ? ST_INC : ST_AGG) | (uint64_t)goff[tid]);
-#endif
 #pragma unroll
         for (uint32_t j = 0; j < SORT_ITEMS; j++) {
             const bool valid = FULL || wbase + j * 64 + lane < n;
@@ -187,19 +166,6 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
             // for the 64-bit select form bit ? m : ~m)
             const uint64_t vm = __ballot(valid);
             uint32_t eq_lo = (uint32_t)vm, eq_hi = (uint32_t)(vm >> 32);
-#ifdef EON_SORT_OLD_RANK  // A/B only: the round-4 64-bit select form
-            uint64_t eq = vm;
-#pragma unroll
-            for (uint32_t b = 0; b < 8; b++) {
-                if (b < dbits) {
-                    const bool bit = (d >> b) & 1;
-                    const uint64_t m = __ballot(bit);
-                    eq &= bit ? m : ~m;
-                }
-            }
-            eq_lo = (uint32_t)eq;
-            eq_hi = (uint32_t)(eq >> 32);
-#else
 #pragma unroll
             for (uint32_t b = 0; b < 8; b++) {
                 if (b < dbits) {
@@ -209,7 +175,6 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
                     eq_hi &= ~((uint32_t)(m >> 32) ^ (uint32_t)sb);
                 }
             }
-#endif
             // lanes below this one in the group (v_mbcnt), and the group's size
             const uint32_t before = __builtin_amdgcn_mbcnt_hi(eq_hi, __builtin_amdgcn_mbcnt_lo(eq_lo, 0u));
             const uint32_t old = valid ? cnt[w][d] : 0u;
@@ -228,10 +193,8 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
                 cnt[v][tid] = tcount;
                 tcount += c;
             }
-#if !EON_SORT_EARLY_AGG
             // publish this tile's counts before anything else, so the next tiles can look back
             st_status(status + (size_t)tile * 256 + tid, (tile == 0 ? ST_INC : ST_AGG) | (uint64_t)tcount);
-#endif
         }
         uint32_t tot;
         const uint32_t ts = scan256(tid < 256 ? tcount : 0u, misc + 4, tot);
@@ -248,38 +211,15 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
         }
         if (tid < 256) {
             uint32_t excl = 0;
-#ifndef EON_SORT_PROBE_NOLOOKBACK
             if (tile > 0) {
-#if EON_SORT_LB > 1
-                // EON_SORT_LB predecessors' status words in flight at once, consumed in order
-                bool done = false;
-                for (int64_t k = (int64_t)tile - 1; !done && k >= 0; k -= EON_SORT_LB) {
-                    uint64_t v[EON_SORT_LB];
-#pragma unroll
-                    for (int q = 0; q < EON_SORT_LB; q++)
-                        v[q] = k - q >= 0 ? ld_status(status + (size_t)(k - q) * 256 + tid) : ST_INC;
-#pragma unroll
-                    for (int q = 0; q < EON_SORT_LB; q++) {
-                        if (done) break;
-                        while ((v[q] >> 62) == 0) {
-                            __builtin_amdgcn_s_sleep(1);
-                            v[q] = ld_status(status + (size_t)(k - q) * 256 + tid);
-                        }
-                        excl += (uint32_t)(v[q] & ST_COUNT);
-                        if (v[q] & ST_INC) done = true;
-                    }
-                }
-#else
                 for (uint32_t k = tile - 1;; k--) {
                     uint64_t v;
                     while (((v = ld_status(status + (size_t)k * 256 + tid)) >> 62) == 0) __builtin_amdgcn_s_sleep(1);
                     excl += (uint32_t)(v & ST_COUNT);  // a digit's running count is below n < 2^32
                     if (v & ST_INC) break;
                 }
-#endif
                 st_status(status + (size_t)tile * 256 + tid, ST_INC | (uint64_t)(excl + tcount));
             }
-#endif
             goff[tid] = base[tid] + excl;
         }
         __syncthreads();

@@ -337,6 +337,57 @@ EON_HD F29 mul29(const F29& a, const F29& b) {
     return r;
 }
 
+// N independent Montgomery products r[c] = a[c] b[c] 2^-261 (mul29's contract each), their
+// multiply-add chains interleaved column by column: for latency-bound code (a wave alone on its
+// SIMD: the few-group MSM reduction's segment sums and trees), where one product's dependent
+// chain leaves the issue slots of the others free.  Same results as N calls of mul29.
+template <class M, int N>
+EON_HD void mul29_n(const F29 (&a)[N], const F29 (&b)[N], F29 (&r)[N]) {
+    uint32_t m[N][9];
+    uint64_t acc[N];
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+#pragma unroll
+        for (int i = 0; i <= k; i++) {
+#pragma unroll
+            for (int c = 0; c < N; c++) {
+                if (k == 0)
+                    mul29_vv(acc[c], a[c].l[0], b[c].l[0]);
+                else
+                    mad29_vv(acc[c], a[c].l[i], b[c].l[k - i]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < k; i++)
+#pragma unroll
+            for (int c = 0; c < N; c++) mad29_vs(acc[c], m[c][i], R29<M>::P[k - i]);
+#pragma unroll
+        for (int c = 0; c < N; c++) {
+            m[c][k] = k < 8 ? (uint32_t)acc[c] * R29<M>::INV : ((uint32_t)acc[c] * R29<M>::INV) & M29;
+            mad29_vs(acc[c], m[c][k], R29<M>::P[0]);
+            acc[c] >>= 29;
+        }
+    }
+#pragma unroll
+    for (int k = 9; k < 17; k++) {
+#pragma unroll
+        for (int i = k - 8; i < 9; i++) {
+#pragma unroll
+            for (int c = 0; c < N; c++) {
+                mad29_vv(acc[c], a[c].l[i], b[c].l[k - i]);
+                mad29_vs(acc[c], m[c][i], R29<M>::P[k - i]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < N; c++) {
+            r[c].l[k - 9] = (uint32_t)acc[c] & M29;
+            acc[c] >>= 29;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < N; c++) r[c].l[8] = (uint32_t)acc[c];
+}
+
 // y w mod p for a constant w < p with its Shoup quotient wq = floor(w 2^261 / p), both as
 // normalised 29-bit limbs (the NTT's twiddles): q = floor(y wq / 2^261) from the product's columns
 // 7..16 -- the columns below 7 sum to less than 2^235, so the estimate is q or q - 1 -- then

@@ -716,31 +716,80 @@ __global__ void __launch_bounds__(256) k_bucket_sums29(const G1Raw29* pieces, co
     st_point(sums + (uint64_t)g * B + m, run, run_inf);
 }
 
-__global__ void __launch_bounds__(64) k_segment_sum29(const G1Raw29* sums, uint32_t B, uint32_t groups,
-                                                      G1Xyzz* seg_out) {
+// One thread per segment of SEG bucket sums, 256 segments of one group per block (segments past
+// the group's last are the identity): running sums and lo times their total, then the block's
+// LDS tree -> one raw partial per block (part[g bpg + blk]).  Latency-bound (a 2^20 MSM has 32768
+// segments: half a wave per SIMD), so every addition / doubling issues its independent products
+// together (add29_ilp / dbl29_ilp).
+constexpr uint32_t SEG_BLOCK = 256;
+__device__ __forceinline__ void st_raw_point(G1Raw29* p, const G1X29& a, bool inf) {
+    if (inf)
+        st_raw29_inf(p);
+    else
+        st_raw29(p, a);
+}
+
+__global__ void __launch_bounds__(SEG_BLOCK) k_segment_sum29(const G1Raw29* sums, uint32_t B, uint32_t bpg,
+                                                             G1Raw29* part) {
+    __shared__ G1Raw29 sh[SEG_BLOCK];
     const uint32_t nseg = B / SEG;
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nseg * groups) return;
-    const uint32_t g = t / nseg, s = t % nseg;
-    const uint32_t lo = s * SEG;
-    const G1Raw29* sb = sums + (uint64_t)g * B + lo;
-    G1X29 run, acc, x;
-    bool run_inf = true, acc_inf = true;
-    for (int k = (int)SEG - 1; k >= 0; k--) {  // bucket lo + k holds digit lo + k + 1
-        const bool inf = ld_raw29(sb + k, x);
-        acc29(run, run_inf, x, inf);
-        acc29(acc, acc_inf, run, run_inf);
-    }
-    if (lo && !run_inf) {  // acc += lo * run (double-and-add, MSB first)
-        G1X29 m;
-        bool m_inf = true;
-        for (int bit = 31 - __builtin_clz(lo); bit >= 0; bit--) {
-            if (!m_inf) dbl29(m);
-            if ((lo >> bit) & 1) acc29(m, m_inf, run, false);
+    const uint32_t g = blockIdx.x / bpg, blk = blockIdx.x % bpg;
+    const uint32_t s = blk * SEG_BLOCK + threadIdx.x;
+    G1X29 acc, x;
+    bool acc_inf = true;
+    if (s < nseg) {
+        const uint32_t lo = s * SEG;
+        const G1Raw29* sb = sums + (uint64_t)g * B + lo;
+        G1X29 run;
+        bool run_inf = true;
+        for (int k = (int)SEG - 1; k >= 0; k--) {  // bucket lo + k holds digit lo + k + 1
+            const bool inf = ld_raw29(sb + k, x);
+            acc29_ilp(run, run_inf, x, inf);
+            acc29_ilp(acc, acc_inf, run, run_inf);
         }
-        acc29(acc, acc_inf, m, m_inf);
+        if (lo && !run_inf) {  // acc += lo * run (double-and-add, MSB first)
+            G1X29 m;
+            bool m_inf = true;
+            for (int bit = 31 - __builtin_clz(lo); bit >= 0; bit--) {
+                if (!m_inf) dbl29_ilp(m);
+                if ((lo >> bit) & 1) acc29_ilp(m, m_inf, run, false);
+            }
+            acc29_ilp(acc, acc_inf, m, m_inf);
+        }
     }
-    st_xyzz(seg_out + t, x29_to_xyzz(acc, acc_inf));
+    st_raw_point(sh + threadIdx.x, acc, acc_inf);
+    __syncthreads();
+    for (uint32_t w = SEG_BLOCK / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            const bool inf = ld_raw29(sh + threadIdx.x + w, x);
+            acc29_ilp(acc, acc_inf, x, inf);
+            st_raw_point(sh + threadIdx.x, acc, acc_inf);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) st_raw_point(part + blockIdx.x, acc, acc_inf);
+}
+
+// out[g] = sum of part[g bpg .. (g + 1) bpg), one block per group (LDS tree, radix 2^29)
+__global__ void __launch_bounds__(SEG_BLOCK) k_tree_sum29(const G1Raw29* part, uint32_t bpg, G1Xyzz* out) {
+    __shared__ G1Raw29 sh[SEG_BLOCK];
+    G1X29 acc, x;
+    bool acc_inf = true;
+    for (uint32_t i = threadIdx.x; i < bpg; i += SEG_BLOCK) {
+        const bool inf = ld_raw29(part + (uint64_t)blockIdx.x * bpg + i, x);
+        acc29_ilp(acc, acc_inf, x, inf);
+    }
+    st_raw_point(sh + threadIdx.x, acc, acc_inf);
+    __syncthreads();
+    for (uint32_t w = SEG_BLOCK / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            const bool inf = ld_raw29(sh + threadIdx.x + w, x);
+            acc29_ilp(acc, acc_inf, x, inf);
+            st_raw_point(sh + threadIdx.x, acc, acc_inf);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) st_xyzz(out + blockIdx.x, x29_to_xyzz(acc, acc_inf));
 }
 
 // out[g * gridDim.x + blk] = sum of in[g * n + blk * TREE .. + TREE)
@@ -1035,7 +1084,11 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     bt.scan_bytes = exclusive_scan_temp_bytes(nb + 1);
     EON_HIP(wk.temp.ensure(std::max(bt.sort_bytes, bt.scan_bytes)));
     bt.log_chunk = LOG_CHUNK_MIN;
-    while (bt.log_chunk < LOG_CHUNK_MAX && (E >> (bt.log_chunk + 1)) >= (1ull << 20)) bt.log_chunk++;
+#ifndef EON_PIECE_MIN_THREADS_LOG  // tuning builds: the fewest piece-sum threads a chunk size keeps
+#define EON_PIECE_MIN_THREADS_LOG 20
+#endif
+    while (bt.log_chunk < LOG_CHUNK_MAX && (E >> (bt.log_chunk + 1)) >= (1ull << EON_PIECE_MIN_THREADS_LOG))
+        bt.log_chunk++;
     // few buckets for many pairs (a bucket would collect more than ~8 pieces): longer chunks while
     // the piece sums keep 2^18 threads (4 waves per SIMD)
     while (bt.log_chunk < LOG_CHUNK_MAX && (E >> bt.log_chunk) > 8ull * nb && (E >> (bt.log_chunk + 1)) >= (1ull << 18))
@@ -1172,9 +1225,17 @@ static Status reduce_segments(eon_ctx* ctx, const MsmLayout& L, const Batch& bt,
     EON_HIP(wk.red_b.ensure((uint64_t)groups * nseg * sizeof(G1Xyzz)));
     ctx->prof.begin("k_segment_sum", (uint64_t)bt.nb * 128 + (uint64_t)groups * nseg * 128, st);
     if (sums29) {
-        // raw bucket sums (k_bucket_sums29, in wk.piece_sums as G1Raw29) -> segment sums
-        hipLaunchKernelGGL(k_segment_sum29, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
-                           wk.piece_sums.as<G1Raw29>(), bt.B, groups, wk.red_a.as<G1Xyzz>());
+        // raw bucket sums (k_bucket_sums29, in wk.piece_sums as G1Raw29) -> one raw partial per
+        // 256 segments -> one point per group, all in radix 2^29
+        const uint32_t bpg = (nseg + SEG_BLOCK - 1) / SEG_BLOCK;
+        EON_HIP(wk.red_b.ensure((uint64_t)groups * bpg * sizeof(G1Raw29)));
+        hipLaunchKernelGGL(k_segment_sum29, dim3(groups * bpg), dim3(SEG_BLOCK), 0, st, wk.piece_sums.as<G1Raw29>(),
+                           bt.B, bpg, wk.red_b.as<G1Raw29>());
+        hipLaunchKernelGGL(k_tree_sum29, dim3(groups), dim3(SEG_BLOCK), 0, st, wk.red_b.as<G1Raw29>(), bpg,
+                           wk.red_a.as<G1Xyzz>());
+        ctx->prof.end(st);
+        EON_HIP(hipGetLastError());
+        return write_columns(L, bt, wk.red_a.as<G1Xyzz>(), st);
     } else if (fused)
         hipLaunchKernelGGL(k_segment_reduce29, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
                            wk.piece_raw.as<G1Raw29>(), sr.piece_off, bt.B, groups, wk.red_a.as<G1Xyzz>());

@@ -492,13 +492,17 @@ class ProveWorkload:
             # torch.distributed's process group (a ctypes callback into Python per exchange) when
             # the ranks share a device (EON_BENCH_ONE_DEVICE rehearsals: RCCL refuses two ranks on
             # one GPU) or with --collective torch
-            kind = args.collective
-            if kind == "auto":
-                shared = os.environ.get("EON_BENCH_ONE_DEVICE") == "1"
-                kind = "torch" if shared or os.environ.get("EON_BENCH_BACKEND", "nccl") != "nccl" else "rccl"
+            kind = choose_collective(args.collective, os.environ)
             self.collective_kind = kind
-            self.coll = (RcclCollective(rank, world) if kind == "rccl"
-                         else TorchCollective(rank, world, None, device=dev.index))
+            self.coll = None
+            if kind == "rccl":
+                try:
+                    self.coll = RcclCollective(rank, world)
+                except Exception as e:  # every rank sees the same failure (ncclCommInitRank is collective)
+                    print(f"bench.py: RCCL communicator failed ({e}); using torch.distributed", file=sys.stderr)
+                    self.collective_kind = "torch (rccl init failed)"
+            if self.coll is None:
+                self.coll = TorchCollective(rank, world, None, device=dev.index)
         # the same 2^(log_n) x VECTOR_LEN permutation inputs on every rank; rank g takes its lanes
         # (permutation j sits at row j / VECTOR_LEN, lane j % VECTOR_LEN)
         inputs = synthetic_fr(n * self.vl, 3, 5).reshape(n, self.vl, 3, 4)[:, l0:l1]
@@ -802,6 +806,16 @@ class MsmShardWorkload:
             "sample": f"C Pippenger restatement on 2^18 points ({dt:.2f} s), scaled linearly to "
                       f"2^{self.args.log_shard_msm}",
         }
+
+def choose_collective(flag: str, env) -> str:
+    """The N > 1 prove's exchange path: the driver's own RCCL communicator unless the ranks share
+    one device (EON_BENCH_ONE_DEVICE=1: RCCL refuses two ranks on one GPU) or the process group is
+    not nccl (EON_BENCH_BACKEND=gloo rehearsals), or as --collective says."""
+    if flag != "auto":
+        return flag
+    shared = env.get("EON_BENCH_ONE_DEVICE") == "1"
+    return "torch" if shared or env.get("EON_BENCH_BACKEND", "nccl") != "nccl" else "rccl"
+
 
 def make_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser()

@@ -339,10 +339,13 @@ uint32_t* radix_sort_histograms(void* temp, uint64_t n) {
     return reinterpret_cast<uint32_t*>(static_cast<char*>(temp) + 2 * align256(n * 4));
 }
 
+// per pass: a 64-byte tile counter and the tiles' status words, every pass's zeroed by one memset
+static size_t pass_state_bytes(uint64_t tiles) { return 64 + align256(tiles * 256 * 8); }
+
 size_t radix_sort_temp_bytes(uint64_t n, uint32_t bits) {
     const uint64_t tiles = (n + SORT_TILE - 1) / SORT_TILE;
-    (void)bits;
-    return 2 * align256(n * 4) + 2 * align256(MAX_PASSES * 256 * 4) + 256 + align256(tiles * 256 * 8 + 8);
+    const uint32_t passes = bits ? split_bits(bits).passes : 1;
+    return 2 * align256(n * 4) + 2 * align256(MAX_PASSES * 256 * 4) + 256 + passes * pass_state_bytes(tiles);
 }
 
 hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
@@ -365,9 +368,9 @@ hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_
     p += align256(MAX_PASSES * 256 * 4);
     uint32_t* base = reinterpret_cast<uint32_t*>(p);
     p += align256(MAX_PASSES * 256 * 4);
-    uint32_t* ctr = reinterpret_cast<uint32_t*>(p);
     p += 256;
-    uint64_t* status = reinterpret_cast<uint64_t*>(p);
+    char* state = p;  // pass q: counter at state + q * pass_state_bytes, status words 64 bytes after
+    const size_t psb = pass_state_bytes(tiles);
 
     hipError_t e = hipSuccess;
     if (!hist_ready) {
@@ -380,15 +383,16 @@ hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_
     for (const void* k : {reinterpret_cast<const void*>(k_sort_pass<8>), reinterpret_cast<const void*>(k_sort_pass<0>)})
         if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SORT_LDS)) != hipSuccess)
             return e;
+    if ((e = hipMemsetAsync(state, 0, pb.passes * psb, st)) != hipSuccess) return e;
     const uint32_t* sk = keys_in;
     const uint32_t* sv = vals_in;
     for (uint32_t q = 0; q < pb.passes; q++) {
+        uint32_t* ctr = reinterpret_cast<uint32_t*>(state + q * psb);
+        uint64_t* status = reinterpret_cast<uint64_t*>(state + q * psb + 64);
         // the last pass lands in the output; earlier ones alternate between the output and temp
         const bool to_out = ((pb.passes - 1 - q) & 1) == 0;
         uint32_t* dk = to_out ? keys_out : ktmp;
         uint32_t* dv = to_out ? vals_out : vtmp;
-        if ((e = hipMemsetAsync(ctr, 0, 4, st)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(status, 0, (size_t)tiles * 256 * 8, st)) != hipSuccess) return e;
         hipLaunchKernelGGL(pb.bits[q] == 8 ? k_sort_pass<8> : k_sort_pass<0>, dim3(tiles), dim3(SORT_THREADS), SORT_LDS,
                            st, sk, sv, dk, dv, (uint32_t)n, pb.shift[q], pb.bits[q], base + q * 256, status, ctr);
         if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -45,3 +45,18 @@ def test_self_launch_builds_the_launcher_command(monkeypatch):
     assert cmd[1:3] == ["-m", "torch.distributed.run"]
     assert "--nproc-per-node=8" in cmd and "127.0.0.1" in cmd
     assert cmd[-4:] == ["--gpus", "8", "--steps", "2"]
+
+
+def test_collective_choice():
+    """The N > 1 prove uses the driver's RCCL communicator by default, torch.distributed when the
+    ranks share a device or the backend is gloo, and whatever --collective names."""
+    import bench
+
+    assert bench.choose_collective("auto", {}) == "rccl"
+    assert bench.choose_collective("auto", {"EON_BENCH_BACKEND": "nccl"}) == "rccl"
+    assert bench.choose_collective("auto", {"EON_BENCH_ONE_DEVICE": "1"}) == "torch"
+    assert bench.choose_collective("auto", {"EON_BENCH_BACKEND": "gloo"}) == "torch"
+    assert bench.choose_collective("torch", {}) == "torch"
+    assert bench.choose_collective("rccl", {"EON_BENCH_ONE_DEVICE": "1"}) == "rccl"
+    args = bench.make_parser().parse_args([])
+    assert args.collective == "auto" and not args.no_clock_probe

@@ -853,9 +853,6 @@ __global__ void k_batch_to_affine(const G1Xyzz* in, uint64_t m, G1Affine* out) {
 }
 
 static uint32_t choose_c(uint64_t n, bool precomputed) {
-#ifdef EON_MSM_C_OVERRIDE  // tuning builds: the window of single fixed-base MSMs of >= 2^18 terms
-    if (precomputed && n >= (1ull << 18)) return EON_MSM_C_OVERRIDE;
-#endif
     // minimise mixed additions n * ceil(255 / c) plus the bucket reduction, ~6 full additions
     // per bucket (per window when the windows keep their own buckets)
     uint32_t best = 4;
@@ -1084,11 +1081,7 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     bt.scan_bytes = exclusive_scan_temp_bytes(nb + 1);
     EON_HIP(wk.temp.ensure(std::max(bt.sort_bytes, bt.scan_bytes)));
     bt.log_chunk = LOG_CHUNK_MIN;
-#ifndef EON_PIECE_MIN_THREADS_LOG  // tuning builds: the fewest piece-sum threads a chunk size keeps
-#define EON_PIECE_MIN_THREADS_LOG 20
-#endif
-    while (bt.log_chunk < LOG_CHUNK_MAX && (E >> (bt.log_chunk + 1)) >= (1ull << EON_PIECE_MIN_THREADS_LOG))
-        bt.log_chunk++;
+    while (bt.log_chunk < LOG_CHUNK_MAX && (E >> (bt.log_chunk + 1)) >= (1ull << 20)) bt.log_chunk++;
     // few buckets for many pairs (a bucket would collect more than ~8 pieces): longer chunks while
     // the piece sums keep 2^18 threads (4 waves per SIMD)
     while (bt.log_chunk < LOG_CHUNK_MAX && (E >> bt.log_chunk) > 8ull * nb && (E >> (bt.log_chunk + 1)) >= (1ull << 18))

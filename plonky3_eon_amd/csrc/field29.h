@@ -18,7 +18,10 @@
 // x 2^256 mod p, and to256 / to261 convert with one product each.  unpack29 / pack29 only re-split
 // the bits of an integer < 2^256.
 #pragma once
+#include <type_traits>
+
 #include "field.h"
+#include "mad_blocks.h"
 
 namespace eon {
 
@@ -195,7 +198,7 @@ EON_HD F29 sub29_lazy(const F29& a, const F29& b) {
     return r;
 }
 
-// a - b + K p normalised, for a with limbs < 2^31 (an add29_lazy / sub29_lazy output) and b
+// a - b + K p normalised, for a with limbs < 2.5 2^30 (add29_lazy / sub29_lazy outputs) and b
 // normalised with b < K p: limb by limb a_i + (K p borrowed)_i - b_i + c in unsigned arithmetic
 // (never negative: the borrowed limbs are >= 2^29 - 1 >= b_i, and the top limb is the nonnegative
 // remainder of a - b + K p >= 0), so no signed column can overflow as in sub29
@@ -294,6 +297,56 @@ EON_HD void mul29_vs(uint64_t& acc, uint32_t a, uint32_t b) {
 #endif
 }
 
+// One column's terms: acc (= 0 when FIRST) + sum va[i] vb[i] + sum sa[i] sb[i], sb wave-uniform
+// (SGPRs).  With EON_MAD_BLOCKS (default) the terms go out as one asm statement per up to 9 + 9
+// of them (mad_blocks.h): the compiler puts an s_nop between any two adjacent asm statements,
+// which cost 11-16 % of a chain's throughput as one statement per term
+// (profiles/r05/s11/ubench_mad_nop.txt).  Without it, one statement per term (mad29_vv / _vs).
+#ifndef EON_MAD_BLOCKS
+#define EON_MAD_BLOCKS 1
+#endif
+template <int NV, int NS, bool FIRST = false>
+EON_HD void madcol(uint64_t& acc, const uint32_t* va, const uint32_t* vb, const uint32_t* sa,
+                   const uint32_t* sb) {
+#if defined(__HIP_DEVICE_COMPILE__) && EON_MAD_BLOCKS
+    if constexpr (NV > 9) {
+        MadAsm<9, 0, FIRST>::run(acc, va, vb, sa, sb);
+        madcol<NV - 9, NS, false>(acc, va + 9, vb + 9, sa, sb);
+    } else if constexpr (NS > 9) {
+        madcol<NV, 9, FIRST>(acc, va, vb, sa, sb);
+        madcol<0, NS - 9, false>(acc, va, vb, sa + 9, sb + 9);
+    } else if constexpr (NV + NS > 0) {
+        MadAsm<NV, NS, FIRST>::run(acc, va, vb, sa, sb);
+    }
+#else
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        if (FIRST && i == 0)
+            mul29_vv(acc, va[0], vb[0]);
+        else
+            mad29_vv(acc, va[i], vb[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < NS; i++) {
+        if (FIRST && NV == 0 && i == 0)
+            mul29_vs(acc, sa[0], sb[0]);
+        else
+            mad29_vs(acc, sa[i], sb[i]);
+    }
+#endif
+}
+
+// f(integral_constant<int, I>) for I = B .. E - 1: column loops whose term counts are template
+// arguments of madcol
+template <int B, int E, class F>
+EON_HD void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+#define EON_K(kc) decltype(kc)::value
+
 // Montgomery product a b 2^-261 mod p (product scanning; see the header comment for the bounds)
 //
 // The reduction multipliers m_0..m_(U-1) are left unmasked (32 bits instead of 29: one v_and
@@ -308,31 +361,38 @@ EON_HD F29 mul29(const F29& a, const F29& b) {
     uint32_t m[9];
     F29 r;
     uint64_t acc;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
+    static_for<0, 9>([&](auto kc) {
+        constexpr int k = EON_K(kc);
+        uint32_t va[k + 1], vb[k + 1], sa[k + 1], sb[k + 1];
 #pragma unroll
         for (int i = 0; i <= k; i++) {
-            if (k == 0)
-                mul29_vv(acc, a.l[0], b.l[0]);
-            else
-                mad29_vv(acc, a.l[i], b.l[k - i]);
+            va[i] = a.l[i];
+            vb[i] = b.l[k - i];
         }
 #pragma unroll
-        for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
+        for (int i = 0; i < k; i++) {
+            sa[i] = m[i];
+            sb[i] = R29<M>::P[k - i];
+        }
+        madcol<k + 1, k, k == 0>(acc, va, vb, sa, sb);
         m[k] = k < U ? (uint32_t)acc * R29<M>::INV : ((uint32_t)acc * R29<M>::INV) & M29;
         mad29_vs(acc, m[k], R29<M>::P[0]);
         acc >>= 29;
-    }
-#pragma unroll
-    for (int k = 9; k < 17; k++) {
+    });
+    static_for<9, 17>([&](auto kc) {
+        constexpr int k = EON_K(kc), n = 17 - k;
+        uint32_t va[n], vb[n], sa[n], sb[n];
 #pragma unroll
         for (int i = k - 8; i < 9; i++) {
-            mad29_vv(acc, a.l[i], b.l[k - i]);
-            mad29_vs(acc, m[i], R29<M>::P[k - i]);
+            va[i - (k - 8)] = a.l[i];
+            vb[i - (k - 8)] = b.l[k - i];
+            sa[i - (k - 8)] = m[i];
+            sb[i - (k - 8)] = R29<M>::P[k - i];
         }
+        madcol<n, n>(acc, va, vb, sa, sb);
         r.l[k - 9] = (uint32_t)acc & M29;
         acc >>= 29;
-    }
+    });
     r.l[8] = (uint32_t)acc;
     return r;
 }
@@ -345,45 +405,50 @@ template <class M, int N>
 EON_HD void mul29_n(const F29 (&a)[N], const F29 (&b)[N], F29 (&r)[N]) {
     uint32_t m[N][9];
     uint64_t acc[N];
+    static_for<0, 9>([&](auto kc) {
+        constexpr int k = EON_K(kc);
 #pragma unroll
-    for (int k = 0; k < 9; k++) {
+        for (int c = 0; c < N; c++) {
+            uint32_t va[k + 1], vb[k + 1], sa[k + 1], sb[k + 1];
 #pragma unroll
-        for (int i = 0; i <= k; i++) {
-#pragma unroll
-            for (int c = 0; c < N; c++) {
-                if (k == 0)
-                    mul29_vv(acc[c], a[c].l[0], b[c].l[0]);
-                else
-                    mad29_vv(acc[c], a[c].l[i], b[c].l[k - i]);
+            for (int i = 0; i <= k; i++) {
+                va[i] = a[c].l[i];
+                vb[i] = b[c].l[k - i];
             }
+#pragma unroll
+            for (int i = 0; i < k; i++) {
+                sa[i] = m[c][i];
+                sb[i] = R29<M>::P[k - i];
+            }
+            madcol<k + 1, k, k == 0>(acc[c], va, vb, sa, sb);
         }
-#pragma unroll
-        for (int i = 0; i < k; i++)
-#pragma unroll
-            for (int c = 0; c < N; c++) mad29_vs(acc[c], m[c][i], R29<M>::P[k - i]);
 #pragma unroll
         for (int c = 0; c < N; c++) {
             m[c][k] = k < 8 ? (uint32_t)acc[c] * R29<M>::INV : ((uint32_t)acc[c] * R29<M>::INV) & M29;
             mad29_vs(acc[c], m[c][k], R29<M>::P[0]);
             acc[c] >>= 29;
         }
-    }
+    });
+    static_for<9, 17>([&](auto kc) {
+        constexpr int k = EON_K(kc), n = 17 - k;
 #pragma unroll
-    for (int k = 9; k < 17; k++) {
+        for (int c = 0; c < N; c++) {
+            uint32_t va[n], vb[n], sa[n], sb[n];
 #pragma unroll
-        for (int i = k - 8; i < 9; i++) {
-#pragma unroll
-            for (int c = 0; c < N; c++) {
-                mad29_vv(acc[c], a[c].l[i], b[c].l[k - i]);
-                mad29_vs(acc[c], m[c][i], R29<M>::P[k - i]);
+            for (int i = k - 8; i < 9; i++) {
+                va[i - (k - 8)] = a[c].l[i];
+                vb[i - (k - 8)] = b[c].l[k - i];
+                sa[i - (k - 8)] = m[c][i];
+                sb[i - (k - 8)] = R29<M>::P[k - i];
             }
+            madcol<n, n>(acc[c], va, vb, sa, sb);
         }
 #pragma unroll
         for (int c = 0; c < N; c++) {
             r[c].l[k - 9] = (uint32_t)acc[c] & M29;
             acc[c] >>= 29;
         }
-    }
+    });
 #pragma unroll
     for (int c = 0; c < N; c++) r[c].l[8] = (uint32_t)acc[c];
 }
@@ -400,36 +465,44 @@ template <class M>
 EON_HD F29 mul29_shoup(const F29& y, const F29& w, const F29& wq) {
     uint64_t acc;
     uint32_t q[9];
-    mul29_vv(acc, y.l[0], wq.l[7]);
+    {
+        uint32_t vb[8];
 #pragma unroll
-    for (int i = 1; i <= 7; i++) mad29_vv(acc, y.l[i], wq.l[7 - i]);
-    acc >>= 29;
+        for (int i = 0; i <= 7; i++) vb[i] = wq.l[7 - i];
+        madcol<8, 0, true>(acc, y.l, vb, nullptr, nullptr);
+        acc >>= 29;
+    }
+    {
+        uint32_t vb[9];
 #pragma unroll
-    for (int i = 0; i <= 8; i++) mad29_vv(acc, y.l[i], wq.l[8 - i]);
-    acc >>= 29;
+        for (int i = 0; i <= 8; i++) vb[i] = wq.l[8 - i];
+        madcol<9, 0>(acc, y.l, vb, nullptr, nullptr);
+        acc >>= 29;
+    }
+    static_for<9, 17>([&](auto kc) {
+        constexpr int k = EON_K(kc), n = 17 - k;
+        uint32_t vb[n];
 #pragma unroll
-    for (int k = 9; k < 17; k++) {
-#pragma unroll
-        for (int i = k - 8; i < 9; i++) mad29_vv(acc, y.l[i], wq.l[k - i]);
+        for (int i = k - 8; i < 9; i++) vb[i - (k - 8)] = wq.l[k - i];
+        madcol<n, 0>(acc, y.l + (k - 8), vb, nullptr, nullptr);
         q[k - 9] = (uint32_t)acc & M29;
         acc >>= 29;
-    }
+    });
     q[8] = (uint32_t)acc;  // q < y < 2^261
     F29 r;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
+    static_for<0, 9>([&](auto kc) {
         // column k: (k + 1) products of each half, at most 18 products < 2^58 (< 2^62.2 with carry)
-        if (k == 0)
-            mul29_vv(acc, y.l[0], w.l[0]);
-        else
-            mad29_vv(acc, y.l[0], w.l[k]);
+        constexpr int k = EON_K(kc);
+        uint32_t vb[k + 1], sb[k + 1];
 #pragma unroll
-        for (int i = 1; i <= k; i++) mad29_vv(acc, y.l[i], w.l[k - i]);
-#pragma unroll
-        for (int i = 0; i <= k; i++) mad29_vs(acc, q[i], R29<M>::NEGP261[k - i]);
+        for (int i = 0; i <= k; i++) {
+            vb[i] = w.l[k - i];
+            sb[i] = R29<M>::NEGP261[k - i];
+        }
+        madcol<k + 1, k + 1, k == 0>(acc, y.l, vb, q, sb);
         r.l[k] = (uint32_t)acc & M29;
         acc >>= 29;
-    }
+    });
     return r;
 }
 
@@ -439,35 +512,45 @@ template <class M>
 EON_HD F29 mul29_shoup_u(const F29& y, const F29& w, const F29& wq) {
     uint64_t acc;
     uint32_t q[9];
-    mul29_vs(acc, y.l[0], wq.l[7]);
+    {
+        uint32_t sb[8];
 #pragma unroll
-    for (int i = 1; i <= 7; i++) mad29_vs(acc, y.l[i], wq.l[7 - i]);
-    acc >>= 29;
+        for (int i = 0; i <= 7; i++) sb[i] = wq.l[7 - i];
+        madcol<0, 8, true>(acc, nullptr, nullptr, y.l, sb);
+        acc >>= 29;
+    }
+    {
+        uint32_t sb[9];
 #pragma unroll
-    for (int i = 0; i <= 8; i++) mad29_vs(acc, y.l[i], wq.l[8 - i]);
-    acc >>= 29;
+        for (int i = 0; i <= 8; i++) sb[i] = wq.l[8 - i];
+        madcol<0, 9>(acc, nullptr, nullptr, y.l, sb);
+        acc >>= 29;
+    }
+    static_for<9, 17>([&](auto kc) {
+        constexpr int k = EON_K(kc), n = 17 - k;
+        uint32_t sb[n];
 #pragma unroll
-    for (int k = 9; k < 17; k++) {
-#pragma unroll
-        for (int i = k - 8; i < 9; i++) mad29_vs(acc, y.l[i], wq.l[k - i]);
+        for (int i = k - 8; i < 9; i++) sb[i - (k - 8)] = wq.l[k - i];
+        madcol<0, n>(acc, nullptr, nullptr, y.l + (k - 8), sb);
         q[k - 9] = (uint32_t)acc & M29;
         acc >>= 29;
-    }
+    });
     q[8] = (uint32_t)acc;
     F29 r;
+    static_for<0, 9>([&](auto kc) {
+        constexpr int k = EON_K(kc);
+        uint32_t sa[2 * k + 2], sb[2 * k + 2];
 #pragma unroll
-    for (int k = 0; k < 9; k++) {
-        if (k == 0)
-            mul29_vs(acc, y.l[0], w.l[0]);
-        else
-            mad29_vs(acc, y.l[0], w.l[k]);
-#pragma unroll
-        for (int i = 1; i <= k; i++) mad29_vs(acc, y.l[i], w.l[k - i]);
-#pragma unroll
-        for (int i = 0; i <= k; i++) mad29_vs(acc, q[i], R29<M>::NEGP261[k - i]);
+        for (int i = 0; i <= k; i++) {
+            sa[i] = y.l[i];
+            sb[i] = w.l[k - i];
+            sa[k + 1 + i] = q[i];
+            sb[k + 1 + i] = R29<M>::NEGP261[k - i];
+        }
+        madcol<0, 2 * k + 2, k == 0>(acc, nullptr, nullptr, sa, sb);
         r.l[k] = (uint32_t)acc & M29;
         acc >>= 29;
-    }
+    });
     return r;
 }
 
@@ -546,44 +629,53 @@ EON_HD F29 sqr29(const F29& a) {
     uint32_t m[9];
     F29 r;
     uint64_t acc;
-    mul29_vv(acc, a.l[0], a.l[0]);  // column 0: the square term only
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-        if (k > 0) {
+    static_for<0, 9>([&](auto kc) {
+        constexpr int k = EON_K(kc), nc = (k + 1) / 2, nq = (k & 1) ? 0 : 1;
+        if constexpr (nc > 0) {
             uint64_t cross;
+            uint32_t va[nc], vb[nc];
 #pragma unroll
-            for (int i = 0; 2 * i < k; i++) {
-                if (i == 0)
-                    mul29_vv(cross, a.l[0], a.l[k]);
-                else
-                    mad29_vv(cross, a.l[i], a.l[k - i]);
+            for (int i = 0; i < nc; i++) {
+                va[i] = a.l[i];
+                vb[i] = a.l[k - i];
             }
+            madcol<nc, 0, true>(cross, va, vb, nullptr, nullptr);
             acc += cross << 1;
-            if ((k & 1) == 0) mad29_vv(acc, a.l[k / 2], a.l[k / 2]);
         }
+        uint32_t va[1] = {a.l[k / 2]}, sa[k + 1], sb[k + 1];
 #pragma unroll
-        for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
+        for (int i = 0; i < k; i++) {
+            sa[i] = m[i];
+            sb[i] = R29<M>::P[k - i];
+        }
+        madcol<nq, k, k == 0>(acc, va, va, sa, sb);
         m[k] = k < U ? (uint32_t)acc * R29<M>::INV : ((uint32_t)acc * R29<M>::INV) & M29;
         mad29_vs(acc, m[k], R29<M>::P[0]);
         acc >>= 29;
-    }
+    });
+    static_for<9, 17>([&](auto kc) {
+        constexpr int k = EON_K(kc), nc = (k - 1) / 2 - (k - 8) + 1, nq = (k & 1) ? 0 : 1, n = 17 - k;
+        if constexpr (nc > 0) {
+            uint64_t cross;
+            uint32_t va[nc], vb[nc];
 #pragma unroll
-    for (int k = 9; k < 17; k++) {
-        uint64_t cross = 0;
-#pragma unroll
-        for (int i = k - 8; 2 * i < k; i++) {
-            if (i == k - 8)
-                mul29_vv(cross, a.l[i], a.l[k - i]);
-            else
-                mad29_vv(cross, a.l[i], a.l[k - i]);
+            for (int i = 0; i < nc; i++) {
+                va[i] = a.l[k - 8 + i];
+                vb[i] = a.l[8 - i];
+            }
+            madcol<nc, 0, true>(cross, va, vb, nullptr, nullptr);
+            acc += cross << 1;
         }
-        acc += cross << 1;
-        if ((k & 1) == 0) mad29_vv(acc, a.l[k / 2], a.l[k / 2]);
+        uint32_t va[1] = {a.l[k / 2]}, sa[n], sb[n];
 #pragma unroll
-        for (int i = k - 8; i < 9; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
+        for (int i = k - 8; i < 9; i++) {
+            sa[i - (k - 8)] = m[i];
+            sb[i - (k - 8)] = R29<M>::P[k - i];
+        }
+        madcol<nq, n>(acc, va, va, sa, sb);
         r.l[k - 9] = (uint32_t)acc & M29;
         acc >>= 29;
-    }
+    });
     r.l[8] = (uint32_t)acc;
     return r;
 }
@@ -597,33 +689,43 @@ EON_HD F29 mul29_sum2(const F29& a, const F29& b, const F29& c, const F29& d) {
     uint32_t m[9];
     F29 r;
     uint64_t acc;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
+    static_for<0, 9>([&](auto kc) {
+        constexpr int k = EON_K(kc);
+        uint32_t va[2 * k + 2], vb[2 * k + 2], sa[k + 1], sb[k + 1];
 #pragma unroll
         for (int i = 0; i <= k; i++) {
-            if (k == 0)
-                mul29_vv(acc, a.l[0], b.l[0]);
-            else
-                mad29_vv(acc, a.l[i], b.l[k - i]);
-            mad29_vv(acc, c.l[i], d.l[k - i]);
+            va[i] = a.l[i];
+            vb[i] = b.l[k - i];
+            va[k + 1 + i] = c.l[i];
+            vb[k + 1 + i] = d.l[k - i];
         }
 #pragma unroll
-        for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
+        for (int i = 0; i < k; i++) {
+            sa[i] = m[i];
+            sb[i] = R29<M>::P[k - i];
+        }
+        madcol<2 * k + 2, k, k == 0>(acc, va, vb, sa, sb);
         m[k] = k < 6 ? (uint32_t)acc * R29<M>::INV : ((uint32_t)acc * R29<M>::INV) & M29;
         mad29_vs(acc, m[k], R29<M>::P[0]);
         acc >>= 29;
-    }
-#pragma unroll
-    for (int k = 9; k < 17; k++) {
+    });
+    static_for<9, 17>([&](auto kc) {
+        constexpr int k = EON_K(kc), n = 17 - k;
+        uint32_t va[2 * n], vb[2 * n], sa[n], sb[n];
 #pragma unroll
         for (int i = k - 8; i < 9; i++) {
-            mad29_vv(acc, a.l[i], b.l[k - i]);
-            mad29_vv(acc, c.l[i], d.l[k - i]);
-            mad29_vs(acc, m[i], R29<M>::P[k - i]);
+            const int j = i - (k - 8);
+            va[j] = a.l[i];
+            vb[j] = b.l[k - i];
+            va[n + j] = c.l[i];
+            vb[n + j] = d.l[k - i];
+            sa[j] = m[i];
+            sb[j] = R29<M>::P[k - i];
         }
+        madcol<2 * n, n>(acc, va, vb, sa, sb);
         r.l[k - 9] = (uint32_t)acc & M29;
         acc >>= 29;
-    }
+    });
     r.l[8] = (uint32_t)acc;
     return r;
 }
@@ -636,33 +738,43 @@ EON_HD F29 mul29_sum2_u(const F29& a, const F29& b, const F29& c, const F29& d) 
     uint32_t m[9];
     F29 r;
     uint64_t acc;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
+    static_for<0, 9>([&](auto kc) {
+        constexpr int k = EON_K(kc);
+        uint32_t sa[3 * k + 2], sb[3 * k + 2];
 #pragma unroll
         for (int i = 0; i <= k; i++) {
-            if (k == 0)
-                mul29_vs(acc, b.l[0], a.l[0]);
-            else
-                mad29_vs(acc, b.l[k - i], a.l[i]);
-            mad29_vs(acc, d.l[k - i], c.l[i]);
+            sa[i] = b.l[k - i];
+            sb[i] = a.l[i];
+            sa[k + 1 + i] = d.l[k - i];
+            sb[k + 1 + i] = c.l[i];
         }
 #pragma unroll
-        for (int i = 0; i < k; i++) mad29_vs(acc, m[i], R29<M>::P[k - i]);
+        for (int i = 0; i < k; i++) {
+            sa[2 * k + 2 + i] = m[i];
+            sb[2 * k + 2 + i] = R29<M>::P[k - i];
+        }
+        madcol<0, 3 * k + 2, k == 0>(acc, nullptr, nullptr, sa, sb);
         m[k] = k < 6 ? (uint32_t)acc * R29<M>::INV : ((uint32_t)acc * R29<M>::INV) & M29;
         mad29_vs(acc, m[k], R29<M>::P[0]);
         acc >>= 29;
-    }
-#pragma unroll
-    for (int k = 9; k < 17; k++) {
+    });
+    static_for<9, 17>([&](auto kc) {
+        constexpr int k = EON_K(kc), n = 17 - k;
+        uint32_t sa[3 * n], sb[3 * n];
 #pragma unroll
         for (int i = k - 8; i < 9; i++) {
-            mad29_vs(acc, b.l[k - i], a.l[i]);
-            mad29_vs(acc, d.l[k - i], c.l[i]);
-            mad29_vs(acc, m[i], R29<M>::P[k - i]);
+            const int j = i - (k - 8);
+            sa[j] = b.l[k - i];
+            sb[j] = a.l[i];
+            sa[n + j] = d.l[k - i];
+            sb[n + j] = c.l[i];
+            sa[2 * n + j] = m[i];
+            sb[2 * n + j] = R29<M>::P[k - i];
         }
+        madcol<0, 3 * n>(acc, nullptr, nullptr, sa, sb);
         r.l[k - 9] = (uint32_t)acc & M29;
         acc >>= 29;
-    }
+    });
     r.l[8] = (uint32_t)acc;
     return r;
 }
@@ -711,6 +823,31 @@ static_assert(columns_fit_u64<FrP>(L30 * L30, 8), "mul29<Fr> column overflow");
 // mul29_sum2: a, c, d normalised, b < 2^31 (a sub29_lazy output), 6 unmasked multipliers
 static_assert(columns_fit_u64<FqP>(L29 * L31 + L29 * L29, 6), "mul29_sum2<Fq> column overflow");
 static_assert(columns_fit_u64<FrP>(L29 * L31 + L29 * L29, 6), "mul29_sum2<Fr> column overflow");
+
+// mul29_shoup's columns for y limbs < ly: the quotient columns 7..16 of y wq (wq normalised, the
+// low columns' carry into column 7 included) and the remainder columns 0..8 of y w + q (2^261 - p)
+template <class M>
+constexpr bool shoup_columns_fit_u64(unsigned __int128 ly) {
+    unsigned __int128 carry = 0;
+    for (int k = 0; k < 17; k++) {
+        unsigned __int128 col = carry;
+        for (int i = 0; i < 9; i++)
+            if (k - i >= 0 && k - i <= 8) col += ly * M29;
+        if (col >= ((unsigned __int128)1 << 64)) return false;
+        carry = col >> 29;
+    }
+    carry = 0;
+    for (int k = 0; k < 9; k++) {
+        unsigned __int128 col = carry;
+        for (int i = 0; i <= k; i++) col += ly * M29 + (unsigned __int128)M29 * R29<M>::NEGP261[k - i];
+        if (col >= ((unsigned __int128)1 << 64)) return false;
+        carry = col >> 29;
+    }
+    return true;
+}
+// the DIT NTT normalises every third stage: two carry-free stages take limbs from < 2^29 to
+// < 1.5 2^30 (x + t, x + (4p borrowed) - t) and then < 2.5 2^30, the widest Shoup input
+static_assert(shoup_columns_fit_u64<FrP>((unsigned __int128)5 << 29), "mul29_shoup<Fr> column overflow");
 
 // Same with the product and reduction terms of a column in two accumulators (shorter dependency
 // chains), merged once per column.

@@ -82,6 +82,13 @@ __device__ __forceinline__ F29 lds_get29(const uint4* lo, const uint4* hi, const
     return x;
 }
 
+// DIT stages between carry propagations (k_ntt_pass29; 2 or 3 -- see the bound there)
+#ifndef EON_NTT_NORM_EVERY
+#define EON_NTT_NORM_EVERY 3
+#endif
+constexpr uint32_t NTT_NORM_EVERY = EON_NTT_NORM_EVERY;
+static_assert(NTT_NORM_EVERY == 2 || NTT_NORM_EVERY == 3, "EON_NTT_NORM_EVERY: 2 or 3");
+
 // KS > 0: the pass's stage count as a compile-time constant, launched with exactly CB 2^KS / 2
 // threads (one butterfly per thread and stage): the stage loop unrolls, its index arithmetic folds
 // to constants and the lazy / normalising stage choice is resolved at compile time.  KS = 0 reads
@@ -203,11 +210,13 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
                 // stages ends below 37p, inside the range mul29_shoup takes (any value
                 // < 2^261 = 169p); the store brings it back below 2p (reduce_top29)
                 const F29 t = unit ? y : mul29_shoup<FrP>(y, w, wq);
-                // carries propagated every other stage: a lazy stage (inputs normalised) leaves
-                // limbs < 2^31 (x + t, x - t + 4p), which the next stage's Shoup product (columns
-                // < 9 2^60 + 9 2^58) and its carry-propagating add / sub29_wide take; the pass's
-                // last stage normalises.  Values grow by <= 4p per stage: < 37p after 10
-                if ((k - 1 - it) & 1) {
+                // carries propagated every NTT_NORM_EVERY-th stage counted back from the pass's
+                // last: a lazy stage takes limbs < L to < L + 2^30 (x + t; x + (4p borrowed) - t,
+                // borrowed limbs < 2^30), so two lazy stages after normalised inputs leave limbs
+                // < 2.5 2^30, which the next stage's Shoup product (field29.h:
+                // shoup_columns_fit_u64) and its carry-propagating add / sub29_wide (< 3.5 2^30 +
+                // carry per limb) take.  Values grow by <= 4p per stage: < 42p after 10
+                if ((k - 1 - it) % NTT_NORM_EVERY) {
                     u = add29_lazy(x, t);
                     v = sub29_lazy<FrP, 4>(x, t);
                 } else {

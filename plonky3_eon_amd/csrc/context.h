@@ -143,9 +143,15 @@ struct MsmWork {
         temp, results, piece_raw, stat;
     SortedBufs sorted;
     uint32_t* host_counts = nullptr;  // pinned read-back slots
+    hipEvent_t counts_ev = nullptr;   // recorded after the count read-back's copies
+    uint32_t* or_host = nullptr;      // pinned read-back of k_scalar_or's copies
     void release() {
         if (host_counts) (void)hipHostFree(host_counts);
         host_counts = nullptr;
+        if (or_host) (void)hipHostFree(or_host);
+        or_host = nullptr;
+        if (counts_ev) (void)hipEventDestroy(counts_ev);
+        counts_ev = nullptr;
         for (DevBuf* b : {&keys, &vals, &count, &off2, &off3, &owner, &piece_sums, &piece_sums2,
                           &bucket_sums, &red_a, &red_b, &temp, &results, &piece_raw, &stat})
             b->release();

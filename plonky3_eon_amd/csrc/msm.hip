@@ -226,13 +226,19 @@ __global__ void __launch_bounds__(256) k_msm_digits4(const Fr* scalars, uint64_t
 
 // OR of every canonical scalar into or_out[8] (zeroed before): its top set bit bounds the
 // digits a single MSM needs (active windows, msm_run_columns)
+constexpr uint32_t SCALAR_OR_COPIES = 64;
 __global__ void __launch_bounds__(256) k_scalar_or(const Fr* scalars, uint64_t n, uint32_t* or_out) {
     __shared__ uint32_t acc[8];
     if (threadIdx.x < 8) acc[threadIdx.x] = 0;
     __syncthreads();
     uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    F29 thirty_two;
+#pragma unroll
+    for (int j = 0; j < 9; j++) thirty_two.l[j] = j == 0 ? 32u : 0u;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const Fr s = to_canonical(ld_pinned(scalars + i));
+        // canonical x from x 2^256: the radix-2^29 product by the plain integer 32 is
+        // x 2^256 32 2^-261 = x (under half the instructions of the radix-2^32 to_canonical)
+        const Fr s = pack29<FrP>(canon29<FrP>(mul29<FrP>(unpack29(ld_pinned(scalars + i)), thirty_two)));
 #pragma unroll
         for (int j = 0; j < 8; j++) v[j] |= s.v[j];
     }
@@ -243,7 +249,10 @@ __global__ void __launch_bounds__(256) k_scalar_or(const Fr* scalars, uint64_t n
         if ((threadIdx.x & 63) == 0 && x) atomicOr(&acc[j], x);
     }
     __syncthreads();
-    if (threadIdx.x < 8 && acc[threadIdx.x]) atomicOr(or_out + threadIdx.x, acc[threadIdx.x]);
+    // SCALAR_OR_COPIES copies of the 8 words (block b ORs into copy b % SCALAR_OR_COPIES): few
+    // atomics per address -- one copy's 32k atomics from 4096 blocks took 56 us (profiles/r05/s14)
+    if (threadIdx.x < 8 && acc[threadIdx.x])
+        atomicOr(or_out + (blockIdx.x % SCALAR_OR_COPIES) * 8 + threadIdx.x, acc[threadIdx.x]);
 }
 
 // bucket index b' of a sorted key (nb for the zero-digit sentinel)
@@ -344,8 +353,10 @@ __device__ __forceinline__ bool piece_run29(const uint32_t* vals, const G1Affine
 
 __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
     const uint32_t* keys, const uint32_t* vals, const uint32_t* start, const uint32_t* piece_off,
-    uint32_t n_pairs, uint32_t log_chunk, uint32_t c, uint32_t groups, uint32_t nb,
-    const G1Affine* pts29, G1Raw29* piece_raw) {
+    uint32_t log_chunk, uint32_t c, uint32_t groups, uint32_t nb, const G1Affine* pts29, G1Raw29* piece_raw) {
+    // the nonzero-digit pairs (start[nb]): read here, so that the launch need not wait for the
+    // count read-back (the grid covers every pair of the batch)
+    const uint32_t n_pairs = start[nb];
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; ((uint64_t)t << log_chunk) < n_pairs;
          t += gridDim.x * blockDim.x) {
         const uint32_t e0 = t << log_chunk;
@@ -716,11 +727,11 @@ __global__ void __launch_bounds__(256) k_bucket_sums29(const G1Raw29* pieces, co
     st_point(sums + (uint64_t)g * B + m, run, run_inf);
 }
 
-// One thread per segment of SEG bucket sums, 256 segments of one group per block (segments past
-// the group's last are the identity): running sums and lo times their total, then the block's
-// LDS tree -> one raw partial per block (part[g bpg + blk]).  Latency-bound (a 2^20 MSM has 32768
-// segments: half a wave per SIMD), so every addition / doubling issues its independent products
-// together (add29_ilp / dbl29_ilp).
+// One thread per segment of `seg` bucket sums (seg29_for), 256 segments of one group per block
+// (segments past the group's last are the identity): running sums and lo times their total, then
+// the block's LDS tree -> one raw partial per block (part[g bpg + blk]).  Latency-bound (a 2^20
+// MSM has 65536 segments: one wave per SIMD), so every addition / doubling issues its independent
+// products together (add29_ilp / dbl29_ilp).
 constexpr uint32_t SEG_BLOCK = 256;
 __device__ __forceinline__ void st_raw_point(G1Raw29* p, const G1X29& a, bool inf) {
     if (inf)
@@ -729,20 +740,30 @@ __device__ __forceinline__ void st_raw_point(G1Raw29* p, const G1X29& a, bool in
         st_raw29(p, a);
 }
 
-__global__ void __launch_bounds__(SEG_BLOCK) k_segment_sum29(const G1Raw29* sums, uint32_t B, uint32_t bpg,
-                                                             G1Raw29* part) {
+// Buckets per k_segment_sum29 thread (seg29): the fewest (>= 4) that keep the threads within one
+// wave per SIMD -- below that the waves are issue-bound alone and a shorter chain per wave is the
+// gain (2^18 buckets: 4 per thread, 0.31 ms, against 8: 0.36 ms, half the SIMDs idle); above it
+// the SIMDs share waves and the total work counts (2^19 buckets at 4: 0.60 ms, at 8: 0.43 ms).
+// profiles/r05/s17.
+static uint32_t seg29_for(uint64_t buckets) {
+    uint32_t seg = 4;
+    while (seg < 64 && buckets / seg > (1u << 16)) seg <<= 1;
+    return seg;
+}
+__global__ void __launch_bounds__(SEG_BLOCK) k_segment_sum29(const G1Raw29* sums, uint32_t B, uint32_t seg,
+                                                             uint32_t bpg, G1Raw29* part) {
     __shared__ G1Raw29 sh[SEG_BLOCK];
-    const uint32_t nseg = B / SEG;
+    const uint32_t nseg = B / seg;
     const uint32_t g = blockIdx.x / bpg, blk = blockIdx.x % bpg;
     const uint32_t s = blk * SEG_BLOCK + threadIdx.x;
     G1X29 acc, x;
     bool acc_inf = true;
     if (s < nseg) {
-        const uint32_t lo = s * SEG;
+        const uint32_t lo = s * seg;
         const G1Raw29* sb = sums + (uint64_t)g * B + lo;
         G1X29 run;
         bool run_inf = true;
-        for (int k = (int)SEG - 1; k >= 0; k--) {  // bucket lo + k holds digit lo + k + 1
+        for (int k = (int)seg - 1; k >= 0; k--) {  // bucket lo + k holds digit lo + k + 1
             const bool inf = ld_raw29(sb + k, x);
             acc29_ilp(run, run_inf, x, inf);
             acc29_ilp(acc, acc_inf, run, run_inf);
@@ -999,6 +1020,8 @@ struct Batch {
     size_t sort_bytes = 0, scan_bytes = 0;
     uint32_t n_pieces = 0, n_pairs = 0;
     uint32_t levels = 0;  // PIECE-way combine levels until every bucket holds <= 1 partial
+    bool counted = false;  // n_pieces / n_pairs / levels read back (batch_counts)
+    size_t prof_rec = SIZE_MAX;  // the k_piece_sum profiler record to complete with the counts
     uint32_t w_act = 0;   // windows that can hold a nonzero digit (0: all of the layout's)
 };
 
@@ -1056,7 +1079,7 @@ static hipError_t sort_pairs(void* temp, const uint32_t* k_in, uint32_t* k_out, 
 // digits + radix sort + bucket starts + piece offsets of one batch into `out`; `wk` supplies the
 // unsorted pairs, the sort / scan scratch and the count read-back slots
 static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t ld, Batch& bt,
-                         MsmWork& wk, SortedBufs& out, hipStream_t st) {
+                         MsmWork& wk, SortedBufs& out, hipStream_t st, hipEvent_t sorted_ev) {
     bt.c = L.c;
     bt.W = bt.w_act ? std::min(bt.w_act, L.W) : L.W;
     bt.B = 1u << (bt.c - 1);
@@ -1120,19 +1143,35 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     EON_HIP(hipMemsetAsync(wk.stat.p, 0, 16, st));
     EON_HIP(exclusive_scan_chunk_counts(wk.temp.p, out.start.as<uint32_t>(), nb, bt.log_chunk,
                                         out.piece_off.as<uint32_t>(), wk.stat.as<uint32_t>(), st));
-    // launches are sized by the real counts (12-byte read-back: pieces, nonzero digits, max pieces)
+    // the sorted pairs are ready for the piece sums (sorted_ev), ahead of the count read-back
+    EON_HIP(hipEventRecord(sorted_ev, st));
+    // the reduction's launches are sized by the real counts (12-byte read-back: pieces, nonzero
+    // digits, max pieces); batch_counts waits for them
     EON_HIP(hipMemcpyAsync(wk.host_counts, out.piece_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
     EON_HIP(hipMemcpyAsync(wk.host_counts + 1, out.start.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
     EON_HIP(hipMemcpyAsync(wk.host_counts + 3, wk.stat.p, 4, hipMemcpyDeviceToHost, st));
-    EON_HIP(hipStreamSynchronize(st));
+    if (!wk.counts_ev) EON_HIP(hipEventCreateWithFlags(&wk.counts_ev, hipEventDisableTiming));
+    EON_HIP(hipEventRecord(wk.counts_ev, st));
+    bt.counted = false;
+    return Status::ok();
+}
+
+static Status batch_counts(eon_ctx* ctx, Batch& bt, MsmWork& wk, uint64_t n) {
+    EON_HIP(hipEventSynchronize(wk.counts_ev));
     bt.n_pieces = wk.host_counts[0];
     bt.n_pairs = wk.host_counts[1];
     bt.levels = 0;
     for (uint64_t m = wk.host_counts[3]; m > 1; m = (m + PIECE - 1) / PIECE) bt.levels++;
     if (msm_debug())
         fprintf(stderr, "msm_batch n=%llu cols=%u c=%u W=%u nb=%u E=%llu pairs=%u pieces=%u\n",
-                (unsigned long long)n, bt.cols, bt.c, bt.W, nb, (unsigned long long)E, bt.n_pairs,
+                (unsigned long long)n, bt.cols, bt.c, bt.W, bt.nb, (unsigned long long)bt.E, bt.n_pairs,
                 bt.n_pieces);
+    bt.counted = true;
+    if (bt.prof_rec < ctx->prof.recs.size()) {  // k_piece_sum was launched before the counts
+        ctx->prof.recs[bt.prof_rec].alg_mulmods = (uint64_t)bt.n_pairs * 10;
+        ctx->prof.recs[bt.prof_rec].design_bytes = (uint64_t)bt.n_pairs * 72 + (uint64_t)bt.n_pieces * 144;
+        bt.prof_rec = SIZE_MAX;
+    }
     return Status::ok();
 }
 
@@ -1161,7 +1200,7 @@ static bool sums_reduce(const Batch& bt) {
 }
 
 // piece sums of one sorted batch against bases `b` (asynchronous); wk supplies the piece buffers
-static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt, const SortedRef& sr,
+static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, const SortedRef& sr,
                            MsmWork& wk, hipStream_t st) {
     EON_HIP(wk.piece_sums.ensure(std::max<uint64_t>(bt.max_pieces * sizeof(G1Xyzz), (uint64_t)bt.nb * sizeof(G1Raw29))));
     EON_HIP(wk.piece_sums2.ensure(bt.max_pieces * sizeof(G1Xyzz)));
@@ -1180,13 +1219,18 @@ static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, const Batch& bt
     // 144-byte partial per piece
     // mulmods: one XYZZ mixed addition (madd-2008-s, 8M + 2S) per nonzero digit
     const uint64_t msm_n = bt.E / ((uint64_t)bt.W * bt.cols);
+    // launched before the count read-back (batch_counts), the grid covers all E pairs and the
+    // profiler record gets its counts later
+    const uint64_t pairs_max = bt.counted ? bt.n_pairs : bt.E;
+    if (!bt.counted && ctx->prof.enabled) bt.prof_rec = ctx->prof.recs.size();
     ctx->prof.begin("k_piece_sum", (uint64_t)bt.cols * msm_n * 96, st, (uint64_t)bt.n_pairs * 10,
                     (uint64_t)bt.n_pairs * 72 + (uint64_t)bt.n_pieces * 144);
-    const uint32_t blocks = blocks_for(((uint64_t)bt.n_pairs + (1u << bt.log_chunk) - 1) >> bt.log_chunk, 64);
-    if (bt.n_pairs)
+    const uint32_t blocks = blocks_for((pairs_max + (1u << bt.log_chunk) - 1) >> bt.log_chunk, 64);
+    if (pairs_max)
         hipLaunchKernelGGL(k_piece_sum29, dim3(blocks), dim3(64), 0, st, sr.keys, sr.vals, sr.start, sr.piece_off,
-                           bt.n_pairs, bt.log_chunk, bt.c, bt.groups, bt.nb, pts, wk.piece_raw.as<G1Raw29>());
+                           bt.log_chunk, bt.c, bt.groups, bt.nb, pts, wk.piece_raw.as<G1Raw29>());
     ctx->prof.end(st);
+    if (!bt.counted) EON_TRY(batch_counts(ctx, bt, wk, msm_n));
     if (bt.n_pieces && !fused_reduce(bt) && !sums_reduce(bt))
         hipLaunchKernelGGL(k_raw29_to_xyzz, dim3(blocks_for(bt.n_pieces, 128)), dim3(128), 0, st,
                            wk.piece_raw.as<G1Raw29>(), bt.n_pieces, wk.piece_sums.as<G1Xyzz>());
@@ -1220,10 +1264,11 @@ static Status reduce_segments(eon_ctx* ctx, const MsmLayout& L, const Batch& bt,
     if (sums29) {
         // raw bucket sums (k_bucket_sums29, in wk.piece_sums as G1Raw29) -> one raw partial per
         // 256 segments -> one point per group, all in radix 2^29
-        const uint32_t bpg = (nseg + SEG_BLOCK - 1) / SEG_BLOCK;
+        const uint32_t seg = std::min(bt.B, seg29_for((uint64_t)bt.B * groups));
+        const uint32_t bpg = (bt.B / seg + SEG_BLOCK - 1) / SEG_BLOCK;
         EON_HIP(wk.red_b.ensure((uint64_t)groups * bpg * sizeof(G1Raw29)));
         hipLaunchKernelGGL(k_segment_sum29, dim3(groups * bpg), dim3(SEG_BLOCK), 0, st, wk.piece_sums.as<G1Raw29>(),
-                           bt.B, bpg, wk.red_b.as<G1Raw29>());
+                           bt.B, seg, bpg, wk.red_b.as<G1Raw29>());
         hipLaunchKernelGGL(k_tree_sum29, dim3(groups), dim3(SEG_BLOCK), 0, st, wk.red_b.as<G1Raw29>(), bpg,
                            wk.red_a.as<G1Xyzz>());
         ctx->prof.end(st);
@@ -1706,16 +1751,19 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
     // of 16 bits.  One OR-reduction over the scalars and a 32-byte read-back.
     static const bool all_windows = getenv("EON_MSM_ALL_WINDOWS") != nullptr;
     if (width == 1 && !keep && !all_windows) {
-        EON_HIP(ctx->msm.stat.ensure(64));
-        EON_HIP(hipMemsetAsync(ctx->msm.stat.p, 0, 32, ctx->stream));
+        constexpr size_t or_bytes = SCALAR_OR_COPIES * 8 * 4;
+        EON_HIP(ctx->msm.stat.ensure(std::max<size_t>(64, or_bytes)));
+        EON_HIP(hipMemsetAsync(ctx->msm.stat.p, 0, or_bytes, ctx->stream));
         const unsigned blocks = (unsigned)std::min<uint64_t>(blocks_for(n, 256), 4096);
         hipLaunchKernelGGL(k_scalar_or, dim3(blocks), dim3(256), 0, ctx->stream, scalars, n,
                            ctx->msm.stat.as<uint32_t>());
         EON_HIP(hipGetLastError());
-        if (!ctx->msm.host_counts) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->msm.host_counts), 64));
-        uint32_t* h = ctx->msm.host_counts + 8;
-        EON_HIP(hipMemcpyAsync(h, ctx->msm.stat.p, 32, hipMemcpyDeviceToHost, ctx->stream));
+        if (!ctx->msm.or_host) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->msm.or_host), or_bytes));
+        EON_HIP(hipMemcpyAsync(ctx->msm.or_host, ctx->msm.stat.p, or_bytes, hipMemcpyDeviceToHost, ctx->stream));
         EON_HIP(hipStreamSynchronize(ctx->stream));
+        uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t k = 0; k < SCALAR_OR_COPIES; k++)
+            for (int j = 0; j < 8; j++) h[j] |= ctx->msm.or_host[k * 8 + j];
         uint32_t bits = 0;
         for (int j = 7; j >= 0 && !bits; j--)
             if (h[j]) bits = 32 * j + 32 - __builtin_clz(h[j]);
@@ -1743,11 +1791,13 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
     EON_HIP(hipStreamWaitEvent(sort_st, ctx->msm_ev[0], 0));
     for (hipStream_t st : comp)
         if (st != ctx->stream) EON_HIP(hipStreamWaitEvent(st, ctx->msm_ev[0], 0));
-    auto sort_batch = [&](size_t k) -> Status {
+    // wait: read the batch's counts back before returning (otherwise batch_pieces does, after
+    // launching its piece sums over all pairs: the first batch's read-back then overlaps them)
+    auto sort_batch = [&](size_t k, bool wait) -> Status {
         const int w = (int)(k % 3);
         if (k >= 3) EON_HIP(hipStreamWaitEvent(sort_st, ctx->msm_reduced[w], 0));
-        EON_TRY(batch_sort(ctx, L, n, width, batches[k], *wks[w], sorted_of(k), sort_st));
-        EON_HIP(hipEventRecord(ctx->msm_sorted[w], sort_st));
+        EON_TRY(batch_sort(ctx, L, n, width, batches[k], *wks[w], sorted_of(k), sort_st, ctx->msm_sorted[w]));
+        if (wait) EON_TRY(batch_counts(ctx, batches[k], *wks[w], n));
         return Status::ok();
     };
     auto pieces = [&](size_t k) -> Status {
@@ -1757,13 +1807,13 @@ Status msm_run_columns(eon_ctx* ctx, const eon_msm_bases* b, const Fr* scalars, 
     };
     DeferredFinish df;
     EON_TRY(prepare_deferred(ctx, L, width, res_xyzz, df));
-    EON_TRY(sort_batch(0));
+    EON_TRY(sort_batch(0, false));
     for (size_t k = 0; k < batches.size(); k++) {
         const int i = (int)(k & 1), w = (int)(k % 3);
         // pieces(k + 1) is enqueued only after reduce(k)'s read-backs: launched earlier it starves
         // the latency-bound reduction (measured +20 ms per prove)
         EON_TRY(pieces(k));
-        if (k + 1 < batches.size()) EON_TRY(sort_batch(k + 1));
+        if (k + 1 < batches.size()) EON_TRY(sort_batch(k + 1, true));
         EON_TRY(batch_reduce(ctx, L, batches[k], sorted_ref(sorted_of(k)), *wks[w], comp[i],
                              fused_reduce(batches[k]), &df));
         EON_HIP(hipEventRecord(ctx->msm_reduced[w], comp[i]));

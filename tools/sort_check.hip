@@ -120,7 +120,10 @@ int main(int argc, char** argv) {
     struct Case { uint32_t n, bits, mode; };
     std::vector<Case> cases = {{0, 16, 0}, {1, 16, 0}, {1000, 16, 0}, {8191, 16, 1}, {8192, 16, 0}, {8193, 16, 2},
                                {100003, 8, 1}, {100003, 19, 0}, {100003, 23, 1}, {1u << 20, 16, 0}, {(1u << 20) + 7, 32, 1},
-                               {3u << 20, 5, 2}, {(1u << 22) + 3, 16, 0}};
+                               {3u << 20, 5, 2}, {(1u << 22) + 3, 16, 0},
+                               // two passes of 9 / 10 bits (17..20 key bits, 1024-bin passes)
+                               {8193, 19, 2}, {100003, 17, 0}, {100003, 18, 1}, {(1u << 20) + 5, 20, 0},
+                               {3u << 20, 19, 1}, {(1u << 22) + 1, 20, 2}};
     for (const Case& cs : cases) {
         uint32_t *k, *v, *k2, *v2;
         const size_t nb = std::max<size_t>(cs.n, 1) * 4;
@@ -128,7 +131,9 @@ int main(int argc, char** argv) {
         CK(hipMalloc(&v, nb));
         CK(hipMalloc(&k2, nb));
         CK(hipMalloc(&v2, nb));
-        if (cs.n) hipLaunchKernelGGL(k_fill, dim3((cs.n + 255) / 256), dim3(256), 0, 0, k, v, cs.n, 16, 1u << 17, cs.mode);
+        if (cs.n)
+            hipLaunchKernelGGL(k_fill, dim3((cs.n + 255) / 256), dim3(256), 0, 0, k, v, cs.n, std::min(std::max(16u, cs.bits), 24u),
+                               1u << 17, cs.mode);
         void* tmp;
         CK(hipMalloc(&tmp, eon::radix_sort_temp_bytes(cs.n, cs.bits) + 256));
         CK(eon::radix_sort_pairs(tmp, k, k2, v, v2, cs.n, cs.bits, 0));
@@ -164,7 +169,7 @@ int main(int argc, char** argv) {
     }
     if (!big) return 0;
     // timing at the prove's batch size: 2^28 MSM-like pairs, 16 key bits (c = 16)
-    for (uint32_t bits : {16u, 19u}) {
+    for (uint32_t bits : {16u, 19u, 20u}) {
         const uint32_t n = 1u << 28;
         uint32_t *k, *v, *k2, *v2;
         CK(hipMalloc(&k, n * 4ull));

@@ -1047,13 +1047,20 @@ struct MsmLayout {
     uint64_t cpb = 1;
 };
 
+// digit pairs per column batch: 2^29 (the prove's 1312 columns in 6 batches of <= 256, a rank's
+// 164 of the 8-way sharded prove in one): fewer, larger piece-sum launches than 2^28 -- prove
+// -0.5 %, emulated 8-rank prove -1 % (profiles/r05/s23, s24; 2^30 measured the same)
+#ifndef EON_MSM_BATCH_LOG_PAIRS
+#define EON_MSM_BATCH_LOG_PAIRS 29
+#endif
 static MsmLayout msm_layout(const eon_msm_bases* b, uint64_t n, uint32_t width) {
     MsmLayout L;
     L.precomputed = b->precomputed;
     L.c = b->precomputed ? b->c : choose_c(n, false);
     L.W = (255 + L.c - 1) / L.c;
-    // columns per batch: keep the digit pairs of one batch at <= 2^28 (4 GiB of sort buffers)
-    uint64_t cpb = (1ull << 28) / (n * L.W);
+    // columns per batch: keep the digit pairs of one batch at <= 2^EON_MSM_BATCH_LOG_PAIRS (8 GiB of
+    // sort buffers at 2^29)
+    uint64_t cpb = (1ull << EON_MSM_BATCH_LOG_PAIRS) / (n * L.W);
     if (cpb < 1) cpb = 1;
     const uint64_t max_groups = b->precomputed ? cpb : cpb * L.W;
     if (max_groups > 65535) cpb = b->precomputed ? 65535 : 65535 / L.W;

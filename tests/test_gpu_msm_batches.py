@@ -1,5 +1,5 @@
-"""The multi-batch MSM pipeline at full size (eon_msm_g1_columns_dev: batches of <= 2^28 digit
-pairs alternating over two compute streams with three workspaces and a sort stream): 260 columns
+"""The multi-batch MSM pipeline at full size (eon_msm_g1_columns_dev: batches of <= 2^29 digit
+pairs alternating over two compute streams with three workspaces and a sort stream): 520 columns
 of 2^17 scalars are 3 batches.  Columns are col_j = s + j t, so MSM(col_j) = S + j T must hold for
 every column (a cross-batch ordering race breaks it with overwhelming probability); col_0 and
 col_1 are checked against the C Pippenger restatement."""
@@ -18,7 +18,7 @@ def test_multibatch_columns_linear(gpu_ctx):
     from plonky3_eon_amd.distributed import combine_partials
     from plonky3_eon_amd.msm import MsmBases, srs_powers
 
-    n, width = 1 << 17, 260
+    n, width = 1 << 17, 520
     srs = srs_powers(n, 4242, gpu_ctx)
     bases = MsmBases(srs, gpu_ctx, precompute=True)
     st = torch.from_numpy(np.stack([C.random_fr(31, n).reshape(n, 4), C.random_fr(32, n).reshape(n, 4)])

@@ -8,8 +8,9 @@
 
 namespace eon {
 
-// Largest n radix_sort_pairs takes: u32 positions, the last tile's indices must not wrap.
-constexpr uint64_t RADIX_SORT_MAX_PAIRS = (1ull << 32) - 8192;
+// Largest n radix_sort_pairs takes: u32 positions, the last tile's indices must not wrap (tiles
+// of up to 16384 pairs).
+constexpr uint64_t RADIX_SORT_MAX_PAIRS = (1ull << 32) - 16384;
 
 // The LSD passes of a sort on `bits` low key bits: pass p sorts key bits [shift[p], shift[p] +
 // bits[p]) (<= 8 bits each).  A producer of the keys may count every pass's 256-bin histogram

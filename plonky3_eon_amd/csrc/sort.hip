@@ -5,7 +5,7 @@
 //   k_sort_hist   one read of the keys: the digit histogram of every pass (LDS counters, one
 //                 global atomic per bin and block)
 //   k_sort_base   exclusive scan of each pass's 256 bins -> the digit's first output position
-//   k_sort_pass   one launch per pass.  A 512-thread block takes the next tile of 8192 pairs (a
+//   k_sort_pass   one launch per pass.  A 1024-thread block takes the next tile of 16384 pairs (a
 //                 virtual tile index from an atomic counter, so every earlier tile is already
 //                 running), each wave ranks its 1024 pairs slot by slot -- the lanes holding the
 //                 same digit found by one ballot per digit bit, the per-wave digit counters in
@@ -27,10 +27,17 @@
 namespace eon {
 namespace {
 
-constexpr uint32_t SORT_THREADS = 512, SORT_WAVES = SORT_THREADS / 64, SORT_ITEMS = 16;
+// threads per sort tile (16 pairs each): 1024 -- half the tiles of 512, so half the look-back
+// steps, at one 146-KB block of 16 waves per CU instead of two of 8: sort 2^28 x 16 bits 2.77 ->
+// 2.47 ms, sort passes 25.6 -> 23.5 ms per prove, prove unchanged (profiles/r05/s26)
+#ifndef EON_SORT_THREADS
+#define EON_SORT_THREADS 1024
+#endif
+constexpr uint32_t SORT_THREADS = EON_SORT_THREADS, SORT_WAVES = SORT_THREADS / 64, SORT_ITEMS = 16;
 constexpr uint32_t SORT_TILE = SORT_THREADS * SORT_ITEMS;
 constexpr uint64_t ST_AGG = 1ull << 62, ST_INC = 2ull << 62, ST_COUNT = (1ull << 62) - 1;
-static_assert(RADIX_SORT_MAX_PAIRS == (1ull << 32) - SORT_TILE, "sort.h's limit is this tile's");
+static_assert(SORT_THREADS == 512 || SORT_THREADS == 1024, "tile threads");
+static_assert(RADIX_SORT_MAX_PAIRS <= (1ull << 32) - SORT_TILE, "the last tile's indices must not wrap");
 constexpr uint32_t MAX_PASSES = RADIX_SORT_MAX_PASSES;
 constexpr size_t SORT_LDS = (size_t)SORT_TILE * 8 + SORT_WAVES * 256 * 4 + 2 * 256 * 4 + 64;
 

@@ -121,9 +121,11 @@ int main(int argc, char** argv) {
     std::vector<Case> cases = {{0, 16, 0}, {1, 16, 0}, {1000, 16, 0}, {8191, 16, 1}, {8192, 16, 0}, {8193, 16, 2},
                                {100003, 8, 1}, {100003, 19, 0}, {100003, 23, 1}, {1u << 20, 16, 0}, {(1u << 20) + 7, 32, 1},
                                {3u << 20, 5, 2}, {(1u << 22) + 3, 16, 0},
-                               // two passes of 9 / 10 bits (17..20 key bits, 1024-bin passes)
+                               // 17..20 key bits (three passes)
                                {8193, 19, 2}, {100003, 17, 0}, {100003, 18, 1}, {(1u << 20) + 5, 20, 0},
-                               {3u << 20, 19, 1}, {(1u << 22) + 1, 20, 2}};
+                               {3u << 20, 19, 1}, {(1u << 22) + 1, 20, 2},
+                               // the edges of a 16384-pair tile (1024 threads x 16)
+                               {16383, 16, 0}, {16384, 16, 1}, {16385, 16, 2}, {32769, 19, 0}};
     for (const Case& cs : cases) {
         uint32_t *k, *v, *k2, *v2;
         const size_t nb = std::max<size_t>(cs.n, 1) * 4;

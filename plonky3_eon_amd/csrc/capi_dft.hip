@@ -116,6 +116,18 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
 #ifndef EON_LDE_DIT
 #define EON_LDE_DIT 1
 #endif
+// the DIT networks exchange unreduced 29-limb planes between passes (EON_NTT_MID, ntt.hip PassArgs::mid)
+#ifndef EON_NTT_MID
+#define EON_NTT_MID 1
+#endif
+    auto mid_for = [&](uint64_t rows) -> uint4* {
+        if (!EON_NTT_MID) return nullptr;
+        if (ctx->mid29.ensure(rows * width * 36) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;  // the packed exchange through `dst` instead
+        }
+        return ctx->mid29.as<uint4>();
+    };
     if (op == Op::CosetLde) {
         EON_HIP(ctx->scratch.ensure(mat_bytes));
         Fr* coeffs = ctx->scratch.as<Fr>();
@@ -148,6 +160,8 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
             f.first_stage = b;
             f.load_mode = LOAD_BITREV_SPREAD;
             f.load_param = b | (n << 8);
+            // one plane buffer serves both networks (they run one after the other on `st`)
+            a.mid = f.mid = mid_for((uint64_t)height << b);
         } else if (natural) {
             a.dif = true;  // natural evals -> bit-reversed coefficients
             EON_TRY(get_power_table(ctx, n, shift, ntt_scale_form(n_inv), true, &table));
@@ -197,6 +211,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
             f.first_stage = b;
             f.load_mode = LOAD_BITREV_SPREAD;
             f.load_param = b | (n << 8);
+            f.mid = mid_for((uint64_t)height << b);
         } else {
             f.dif = true;
             f.load_mode = LOAD_ZEROPAD;
@@ -223,6 +238,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
     if (!s.dif) {
         s.load_mode = LOAD_BITREV;
         s.load_param = n;
+        s.mid = mid_for(height);
         if (in == out && n > 0) {  // the gather cannot run in place
             EON_HIP(ctx->scratch.ensure(mat_bytes));
             EON_HIP(hipMemcpyAsync(ctx->scratch.p, in, mat_bytes, hipMemcpyDeviceToDevice, st));
@@ -376,6 +392,7 @@ void eon_ctx_destroy(eon_ctx* ctx) {
     ctx->scratch.release();
     ctx->stage_in.release();
     ctx->stage_out.release();
+    ctx->mid29.release();
     (void)hipStreamDestroy(ctx->own_stream);
     (void)hipStreamDestroy(ctx->msm_side);
     (void)hipStreamDestroy(ctx->msm_side2);
@@ -455,6 +472,7 @@ int eon_ctx_trim(eon_ctx* ctx) {
     ctx->pool.release_all();
     for (auto& sb : ctx->sorted_cache) sb.release();
     ctx->sorted_cache.clear();
+    ctx->mid29.release();
     return EON_OK;
 }
 

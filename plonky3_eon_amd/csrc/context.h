@@ -236,8 +236,9 @@ struct eon_ctx {
     // opening bases' tables and scratch, reused across proofs (opening.hip, msm.hip)
     eon::DevPool pool;
 
-    // scratch: NTT intermediates, host-API staging
-    eon::DevBuf scratch, stage_in, stage_out;
+    // scratch: NTT intermediates, host-API staging; the DIT networks' unreduced 29-limb planes
+    // between passes (NetworkSpec::mid)
+    eon::DevBuf scratch, stage_in, stage_out, mid29;
 };
 
 namespace eon {

@@ -46,6 +46,9 @@ struct NetworkSpec {
     uint32_t max_threads = 0;          // 0 = default (512, 1024 for 2048-element tiles); tuning knob
     uint32_t log_tile = 0;             // log2 elements per LDS tile (0 = 10); tuning knob
     int log_cb_override = -1;          // columns per tile = 2^log_cb; -1 = by width
+    // DIT only: 36 * 2^log_m * width bytes for the unreduced 29-limb planes exchanged between the
+    // passes (PassArgs::mid); null = values reduced and packed into `dst` between passes
+    uint4* mid = nullptr;
 };
 
 // Optional per-launch timing (eon_ctx_profile_*): a launch is bracketed by two events.

@@ -38,7 +38,28 @@ struct PassArgs {
     uint32_t has_load_const;
     uint32_t col_tiles;
     uint32_t last;  // the network's last pass: canonical output (earlier passes store values < 2p)
+    // DIT networks of several passes: the passes between them exchange the tile limbs as they are
+    // (normalised, unreduced: values below (2 + 4 x stages) p < 169 p, the Shoup products' input
+    // range) in three planes -- limbs 0-3 at mid[i], 4-7 at mid[mid_n + i], 8 at the u32 array
+    // after them -- instead of reduced and packed into 32 bytes (no reduce / pack / unpack)
+    uint4* mid;
+    uint64_t mid_n;
+    uint32_t in_mid, out_mid;
 };
+
+__device__ __forceinline__ F29 mid_get(const uint4* mid, uint64_t n, uint64_t i) {
+    const uint4 a = mid[i], b = mid[n + i];
+    F29 x;
+    x.l[0] = a.x; x.l[1] = a.y; x.l[2] = a.z; x.l[3] = a.w;
+    x.l[4] = b.x; x.l[5] = b.y; x.l[6] = b.z; x.l[7] = b.w;
+    x.l[8] = reinterpret_cast<const uint32_t*>(mid + 2 * n)[i];
+    return x;
+}
+__device__ __forceinline__ void mid_put(uint4* mid, uint64_t n, uint64_t i, const F29& x) {
+    mid[i] = make_uint4(x.l[0], x.l[1], x.l[2], x.l[3]);
+    mid[n + i] = make_uint4(x.l[4], x.l[5], x.l[6], x.l[7]);
+    reinterpret_cast<uint32_t*>(mid + 2 * n)[i] = x.l[8];
+}
 
 // LDS bytes of one twiddle set (roots or quotients) of nt entries: two 16-B planes and a 4-B one,
 // rounded up to 16 B so the next set's planes stay aligned
@@ -142,7 +163,9 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         const uint64_t p = base_row + ((uint64_t)m << s0);
         const uint64_t col = col0 + c;
         F29 x = unpack29(Fr::zero());
-        if (col < width) {
+        if (col < width && a.in_mid) {
+            x = mid_get(a.mid, a.mid_n, p * width + col);
+        } else if (col < width) {
             uint64_t r = p;
             bool present = true;
             switch (a.load_mode) {
@@ -196,7 +219,9 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
             // the twiddle-free butterflies are skipped only where a whole stage is twiddle-free
             // (half = 1 at low = 0: a uniform branch); elsewhere a unit twiddle is multiplied like
             // any other (its 29-form is 2^261 mod p), as a per-lane choice would run both paths
-            const bool unit = half == 1 && low == 0;
+            // (not on unreduced inputs from a previous pass: t = y would break the < 3p bound the
+            // lazy subtraction needs; the unit root is multiplied, which reduces y below 3p)
+            const bool unit = half == 1 && low == 0 && !a.in_mid;
             F29 u, v;
             F29 w, wq;
             if (!unit) {
@@ -250,7 +275,9 @@ __global__ void __launch_bounds__(1024) k_ntt_pass29(PassArgs a) {
         const uint32_t m = e >> LOG_CB;
         const uint64_t p = base_row + ((uint64_t)m << s0);
         const uint64_t col = col0 + c;
-        if (col < width) {
+        if (col < width && a.out_mid) {
+            mid_put(a.mid, a.mid_n, p * width + col, lds_get29(lo, hi, top, e));
+        } else if (col < width) {
             // below 2p (fits 256 bits) between passes, canonical after the last one
             F29 r = reduce_top29<FrP>(lds_get29(lo, hi, top, e));
             if (a.store_scale) r = mul29<FrP>(r, unpack29(ld_pinned(a.store_scale + p)));
@@ -425,6 +452,12 @@ hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
         }
         a.store_scale = last ? s.store_scale : nullptr;
         a.last = last ? 1u : 0u;
+        if (!s.dif && s.mid && passes > 1) {
+            a.mid = s.mid;
+            a.mid_n = (1ull << s.log_m) * s.width;
+            a.in_mid = first ? 0u : 1u;
+            a.out_mid = last ? 0u : 1u;
+        }
         const uint64_t groups = (1ull << s.log_m) >> a.k;
         static const char* names[8] = {"k_ntt_pass29<false, 0>", "k_ntt_pass29<false, 1>",
                                          "k_ntt_pass29<false, 2>", "k_ntt_pass29<false, 3>",

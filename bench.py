@@ -25,7 +25,7 @@ Also reported:
                    / average launch duration (HIP events on the launch
                   stream, eon_ctx_profile, over serialized profiled steps after the timed region)
                   vs 8 TB/s HBM, `traffic` from this round's committed PMC pass
-                  (profiles/r05/traffic_*.json, stamped with the commit it measured);
+                  (profiles/<round>/traffic_*.json, raw FETCH + WRITE, stamped with the commit it measured);
                   `valu` is the binding integer roofline of the same kernel: its algorithmic
                   256-bit Montgomery products per launch / launch duration vs the measured
                   mulmod peak (tools/ubench_r29.hip), and vs the product rate measured live on
@@ -59,7 +59,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # tools/ubench_mulmod.hip)
 MULMOD_PEAK_PER_S = 1.80e11
 # PMC traffic files are read from this round's profile directory only (see main())
-TRAFFIC_ROUND = "r05"
+TRAFFIC_ROUND = "r06"
 FR_P = [0x43E1F593F0000001, 0x2833E84879B97091, 0xB85045B68181585D, 0x30644E72E131A029]
 
 
@@ -480,7 +480,8 @@ class ProveWorkload:
             from plonky3_eon_amd.air import AirProgram
 
             self.air = AirProgram(self.p2air, ctx)
-        from plonky3_eon_amd.native import EmulatedCollective, NativeKzgPcs, RcclCollective, TorchCollective
+        from plonky3_eon_amd.native import (EmulatedCollective, NativeKzgPcs, RcclCollective, RcclInitError,
+                                            TorchCollective)
 
         self.pcs = NativeKzgPcs(n, 12345, ctx)
         self.coll = None
@@ -498,7 +499,9 @@ class ProveWorkload:
             if kind == "rccl":
                 try:
                     self.coll = RcclCollective(rank, world)
-                except Exception as e:  # every rank sees the same failure (ncclCommInitRank is collective)
+                except RcclInitError as e:
+                    # raised on every rank alike (the ranks agree on the outcome inside
+                    # RcclCollective), so all of them fall back together; anything else fails fast
                     print(f"bench.py: RCCL communicator failed ({e}); using torch.distributed", file=sys.stderr)
                     self.collective_kind = "torch (rccl init failed)"
             if self.coll is None:
@@ -861,6 +864,40 @@ def make_parser() -> argparse.ArgumentParser:
     return ap
 
 
+def rank_evidence(wl, rank: int, local_rank: int, dev, elapsed_s: float, steps: int, world: int) -> dict:
+    """One rank's record for the N > 1 line (bench.py main): where it ran, what the RCCL
+    communicator reports (when the workload uses the driver's own, native.RcclCollective.info),
+    and its own timings before the max over ranks."""
+    import socket
+
+    import torch
+
+    p = torch.cuda.get_device_properties(dev)
+    rec = {
+        "rank": rank,
+        "local_rank": local_rank,
+        "hostname": socket.gethostname(),
+        "device": torch.cuda.current_device(),
+        "pci_bus_id": "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id),
+        "gpu": p.name,
+        "collective": getattr(wl, "collective_kind", "torch"),
+        "ms_per_step": round(elapsed_s * 1e3 / steps, 3),
+    }
+    coll = getattr(wl, "coll", None)
+    if coll is not None and hasattr(coll, "info"):
+        try:
+            rec.update(coll.info())
+        except Exception as e:  # the record is evidence, not the measurement: say what failed
+            rec["nccl_info_error"] = str(e)
+    try:
+        thr, _ = wl.throughput(world, elapsed_s * 1e3 / steps)
+        if isinstance(thr, dict) and "stage_ms" in thr:
+            rec["stage_ms"] = thr["stage_ms"]
+    except Exception:
+        pass
+    return rec
+
+
 def _free_port() -> int:
     import socket
 
@@ -972,7 +1009,14 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
+    ranks = None
     if world > 1:
+        # what each rank ran on and saw, gathered to rank 0: the device ordinal and PCI address
+        # torch reports, the RCCL communicator's own view (ncclCommCount / ncclCommUserRank /
+        # ncclCommCuDevice, and that device's PCI bus id), and the rank's own timings -- so that
+        # the N-GPU line shows N ranks on N distinct GPUs under one N-rank communicator
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rank_evidence(wl, rank, local_rank, dev, elapsed, args.steps, world))
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -1083,12 +1127,20 @@ def main() -> int:
             tf = json.loads(traffic_file.read_text())
             if tf.get("kernel") == kname and tf.get("workload") == workload:
                 roof["traffic"] = tf.get("bytes_per_launch")
-                roof["traffic_source"] = "%s (commit %s; FETCH_SIZE %.3g GB raw, WRITE_SIZE %.3g GB per launch)" % (
+                roof["traffic_source"] = ("%s (commit %s; raw FETCH_SIZE %.3g GB + WRITE_SIZE %.3g GB per launch; "
+                                          "the x2 streaming-read correction is not applied to these gathers)") % (
                     traffic_file.relative_to(ROOT), tf.get("commit", "?"), tf["fetch_size_kb_per_launch"] * 1024 / 1e9,
                     tf["write_size_kb_per_launch"] * 1024 / 1e9)
+                if tf.get("bytes_per_launch_x2_streaming"):
+                    roof["traffic_x2_streaming_upper"] = tf["bytes_per_launch_x2_streaming"]
         except Exception:
             pass
 
+    if ranks is not None:
+        result["ranks"] = ranks
+        result["distinct_gpus"] = len({r["pci_bus_id"] for r in ranks})
+        counts = {r.get("nccl_comm_count") for r in ranks}
+        result["rccl_comm_count"] = counts.pop() if len(counts) == 1 else sorted(counts, key=str)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = wl.cpu_baseline()
     if world > 1:

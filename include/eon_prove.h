@@ -46,6 +46,12 @@ const char* eon_kzg_pcs_last_error(const eon_kzg_pcs* pcs);
  * communicator on the current HIP device (the context's). */
 int eon_rccl_unique_id(uint8_t id[128]);
 int eon_rccl_collective_init(uint32_t rank, uint32_t world, const uint8_t id[128], eon_collective* out);
+/* What the communicator itself reports (evidence that RCCL saw `world` ranks on distinct GPUs):
+ * ncclCommCount, ncclCommUserRank, ncclCommCuDevice and that device's PCI bus id (NUL-terminated,
+ * at most pci_len bytes); any output pointer may be NULL.  EON_E_ARG if `coll` is not an RCCL
+ * collective of eon_rccl_collective_init. */
+int eon_rccl_collective_info(const eon_collective* coll, int32_t* count, int32_t* user_rank, int32_t* device,
+                             char* pci_bus_id, uint32_t pci_len);
 void eon_rccl_collective_finalize(eon_collective* coll);
 /* The one-GPU proxy of rank `rank` in a `world`-rank lane-sharded prove (bench.py
  * --emulate-world): its all-gather writes this rank's block into every slot, its all-to-all

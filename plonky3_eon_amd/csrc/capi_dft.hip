@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <initializer_list>
 #include <vector>
 
 #include "context.h"
@@ -120,13 +121,20 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
 #ifndef EON_NTT_MID
 #define EON_NTT_MID 1
 #endif
-    auto mid_for = [&](uint64_t rows) -> uint4* {
-        if (!EON_NTT_MID) return nullptr;
-        if (ctx->mid29.ensure(rows * width * 36) != hipSuccess) {
+    // the plane buffer of a DIT network, allocated only when the network runs more than one pass
+    // (a one-pass network exchanges nothing); it grows with the largest multi-pass transform and
+    // is given back by eon_ctx_trim, and by ctx_ensure when another allocation runs out of memory
+    auto mid_for = [&](std::initializer_list<NetworkSpec*> specs) {
+        uint64_t need = 0;
+        for (NetworkSpec* sp : specs)
+            if (!sp->dif && network_passes(*sp) > 1) need = std::max<uint64_t>(need, (1ull << sp->log_m) * sp->width * 36);
+        if (!EON_NTT_MID || need == 0) return;
+        if (ctx_ensure(ctx, ctx->mid29, need) != hipSuccess) {
             (void)hipGetLastError();
-            return nullptr;  // the packed exchange through `dst` instead
+            return;  // the packed exchange through `dst` instead
         }
-        return ctx->mid29.as<uint4>();
+        for (NetworkSpec* sp : specs)
+            if (!sp->dif && network_passes(*sp) > 1) sp->mid = ctx->mid29.as<uint4>();
     };
     if (op == Op::CosetLde) {
         EON_HIP(ctx->scratch.ensure(mat_bytes));
@@ -146,6 +154,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         f.tw = ctx->tw_fwd.as<Fr>();
         f.twq = ctx->twq_fwd.as<uint32_t>();
         const Fr* table = nullptr;
+        bool want_mid = false;
         if (natural && EON_LDE_DIT) {
             // two DIT networks: bit-reversed gather -> natural coefficients, then the forward
             // network gathers them bit-reversed and spread.  The DIT butterfly (lazy sums, carries
@@ -161,7 +170,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
             f.load_mode = LOAD_BITREV_SPREAD;
             f.load_param = b | (n << 8);
             // one plane buffer serves both networks (they run one after the other on `st`)
-            a.mid = f.mid = mid_for((uint64_t)height << b);
+            want_mid = true;
         } else if (natural) {
             a.dif = true;  // natural evals -> bit-reversed coefficients
             EON_TRY(get_power_table(ctx, n, shift, ntt_scale_form(n_inv), true, &table));
@@ -186,6 +195,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         a.max_threads = f.max_threads = ctx->ntt_tpb;
         a.log_tile = f.log_tile = ctx->ntt_log_tile;
         a.log_cb_override = f.log_cb_override = ctx->ntt_log_cb;
+        if (want_mid) mid_for({&a, &f});
         EON_HIP(run_network(a, st, &ctx->prof));
         EON_HIP(run_network(f, st, &ctx->prof));
         return Status::ok();
@@ -211,7 +221,6 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
             f.first_stage = b;
             f.load_mode = LOAD_BITREV_SPREAD;
             f.load_param = b | (n << 8);
-            f.mid = mid_for((uint64_t)height << b);
         } else {
             f.dif = true;
             f.load_mode = LOAD_ZEROPAD;
@@ -221,6 +230,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
         f.max_threads = ctx->ntt_tpb;
         f.log_tile = ctx->ntt_log_tile;
         f.log_cb_override = ctx->ntt_log_cb;
+        if (natural) mid_for({&f});
         EON_HIP(run_network(f, st, &ctx->prof));
         return Status::ok();
     }
@@ -238,7 +248,6 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
     if (!s.dif) {
         s.load_mode = LOAD_BITREV;
         s.load_param = n;
-        s.mid = mid_for(height);
         if (in == out && n > 0) {  // the gather cannot run in place
             EON_HIP(ctx->scratch.ensure(mat_bytes));
             EON_HIP(hipMemcpyAsync(ctx->scratch.p, in, mat_bytes, hipMemcpyDeviceToDevice, st));
@@ -265,6 +274,7 @@ Status dft_dev(eon_ctx* ctx, Op op, const Fr* in, Fr* out, uint64_t height, uint
     s.max_threads = ctx->ntt_tpb;
     s.log_tile = ctx->ntt_log_tile;
     s.log_cb_override = ctx->ntt_log_cb;
+    if (!s.dif) mid_for({&s});
     EON_HIP(run_network(s, st, &ctx->prof));
     return Status::ok();
 }
@@ -309,6 +319,22 @@ Status dft_natural_dev(eon_ctx* ctx, const Fr* in, Fr* out, uint64_t height, uin
     return dft_dev(ctx, Op::Dft, in, out, height, width, 0, nullptr, EON_ORDER_NATURAL);
 }
 
+}  // namespace eon
+
+namespace eon {
+hipError_t ctx_ensure(eon_ctx* ctx, DevBuf& b, size_t need) {
+    hipError_t e = b.ensure(need);
+    if (e != hipErrorOutOfMemory) return e;
+    (void)hipGetLastError();
+    // the buffers below may still be read by queued work: drain the context's streams first
+    for (hipStream_t st : {ctx->stream, ctx->msm_side, ctx->msm_side2, ctx->msm_sort})
+        if (st && (e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    ctx->pool.release_all();
+    for (auto& sb : ctx->sorted_cache) sb.release();
+    ctx->sorted_cache.clear();
+    if (&b != &ctx->mid29) ctx->mid29.release();
+    return b.ensure(need);
+}
 }  // namespace eon
 
 extern "C" {

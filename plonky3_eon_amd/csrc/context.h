@@ -244,6 +244,11 @@ struct eon_ctx {
 namespace eon {
 
 Status ensure_twiddles(eon_ctx* ctx, uint32_t log_n);
+// DevBuf::ensure for the large per-call workspaces: on an out-of-memory error it first drains the
+// context's streams and gives back what the context keeps only for speed -- the idle pool buffers,
+// the cached sorted-digit buffers, the NTT plane buffer (what eon_ctx_trim frees) -- and tries
+// once more (capi_dft.hip)
+hipError_t ctx_ensure(eon_ctx* ctx, DevBuf& b, size_t need);
 // table[j] = scale * base^j (natural) or table[j] = scale * base^reverse_bits(j, log_n) (bitrev)
 Status get_power_table(eon_ctx* ctx, uint32_t log_n, const Fr& base, const Fr& scale, bool bitrev,
                        const Fr** out);

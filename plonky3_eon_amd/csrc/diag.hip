@@ -73,16 +73,17 @@ extern "C" int eon_diag_clock_probe(eon_ctx* ctx, uint32_t launches, uint32_t it
         PoolScope ps(ctx->pool, ctx->stream);
         EON_HIP(ps.take(stamps, (size_t)PROBE_BLOCKS * 2 * sizeof(uint64_t)));
         EON_HIP(ps.take(sink, 64));
-        hipEvent_t a, b;
-        EON_HIP(hipEventCreate(&a));
-        EON_HIP(hipEventCreate(&b));
+        // the guard exists before either event is created, and destroys only those that were
         struct Ev {
-            hipEvent_t a, b;
+            hipEvent_t a = nullptr, b = nullptr;
             ~Ev() {
-                (void)hipEventDestroy(a);
-                (void)hipEventDestroy(b);
+                if (a) (void)hipEventDestroy(a);
+                if (b) (void)hipEventDestroy(b);
             }
-        } ev{a, b};
+        } ev;
+        EON_HIP(hipEventCreate(&ev.a));
+        EON_HIP(hipEventCreate(&ev.b));
+        hipEvent_t a = ev.a, b = ev.b;
         // one untimed launch, then `launches` back to back (the clock settles under the load)
         hipLaunchKernelGGL(k_clock_probe, dim3(PROBE_BLOCKS), dim3(PROBE_THREADS), 0, ctx->stream, iters, 0u,
                            stamps.as<uint64_t>(), sink.as<uint32_t>());

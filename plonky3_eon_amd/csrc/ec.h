@@ -185,10 +185,18 @@ __device__ __forceinline__ void st_xyzz(G1Xyzz* p, const G1Xyzz& a) {
     st_vec(&p->ZZZ, a.ZZZ);
 }
 
+// all four 16-byte loads issued before any pin: pinning x first (two ld_pinned calls) made the
+// y loads wait for x's, two memory round trips per point instead of one
 __device__ __forceinline__ G1Affine ld_affine(const G1Affine* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
     G1Affine r;
-    r.x = ld_pinned(&p->x);
-    r.y = ld_pinned(&p->y);
+    r.x.v[0] = a.x; r.x.v[1] = a.y; r.x.v[2] = a.z; r.x.v[3] = a.w;
+    r.x.v[4] = b.x; r.x.v[5] = b.y; r.x.v[6] = b.z; r.x.v[7] = b.w;
+    r.y.v[0] = c.x; r.y.v[1] = c.y; r.y.v[2] = c.z; r.y.v[3] = c.w;
+    r.y.v[4] = d.x; r.y.v[5] = d.y; r.y.v[6] = d.z; r.y.v[7] = d.w;
+    pin(r.x);
+    pin(r.y);
     return r;
 }
 

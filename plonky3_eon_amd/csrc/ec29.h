@@ -2,7 +2,8 @@
 //
 // Same formulas as ec.h (madd-2008-s, mdbl-2008-s-1, a = 0) with lazy reduction: no conditional
 // subtraction anywhere, each coordinate carries a bound in multiples of p instead:
-//   X < 8p, Y < 4p, ZZ < 2p, ZZZ < 2p        (invariant of an accumulator between additions)
+//   X < 8p, Y < 4p, ZZ < 2p, ZZZ < 3p        (invariant of an accumulator between additions;
+//                                           ZZZ may have lazy limbs < 2^30: it only feeds mul29)
 // and every product input stays below 13p (mul29's limit, field29.h).  Affine bases are read in
 // 29-Montgomery form (x 2^261 mod p, canonical, as a 256-bit integer in the 64-byte G1Affine
 // slot; see k_table_to29 in msm.hip), so a load is a bit re-split with no product.
@@ -70,6 +71,43 @@ __device__ __forceinline__ bool madd29(G1X29& acc, const F29& ax, const F29& ay)
 
 __device__ __forceinline__ void madd29_unchecked(G1X29& acc, const F29& ax, const F29& ay) {
     madd29<false>(acc, ax, ay);
+}
+
+// madd29_unchecked computed with Pn = X - U2 instead of P = U2 - X, so that PPPn = Pn PP = -PPP
+// comes out of the product directly: Y3 = R (Q - X3) - Y PPP = R (Q - X3 + 9p) + Y PPPn needs no
+// normalising negation (madd29's 2p - PPP), and X3 = R^2 + PPPn - 2Q + 4p.  The one place PPP's
+// sign shows is ZZZ3 = ZZZ PPP: this returns ZZZ PPPn = -ZZZ3, i.e. (X3, Y3, ZZ3, -ZZZ3) -- the
+// tuple of the NEGATED sum -(acc + A).  The piece loop (k_piece_sum29) carries that sign as one
+// bit per lane: it adds the next base with the opposite sign when the bit is set (the conditional
+// base negation it needs anyway for negative digits), and fixes the sign at the run's flush
+// (neg_zzz29_lazy).  Same bounds as madd29: X3 < 8p, Y3 < 2p, ZZ3, ZZZ3 < 2p normalised; ay may be
+// a lazy negation (limbs < 2^30, value < 2p: it only feeds mul29).
+__device__ __forceinline__ void madd29_negsum(G1X29& acc, const F29& ax, const F29& ay) {
+    const F29 U2 = mul29<FqP>(ax, acc.ZZ);            // < 2p
+    const F29 Pn = sub29<FqP, 2>(acc.X, U2);          // X - U2 + 2p < 10p
+    const F29 PP = sqr29<FqP>(Pn);                     // < 2p
+    const F29 PPPn = mul29<FqP>(Pn, PP);              // -PPP, < 2p
+    const F29 Q = mul29<FqP>(acc.X, PP);              // < 2p
+    const F29 S2 = mul29<FqP>(ay, acc.ZZZ);           // < 2p
+    const F29 R = sub29<FqP, 4>(S2, acc.Y);           // < 6p
+    acc.ZZ = mul29<FqP>(acc.ZZ, PP);                  // < 2p
+    acc.ZZZ = mul29<FqP>(acc.ZZZ, PPPn);              // -ZZZ3, < 2p
+    // X3 = R^2 + PPPn - 2Q + 4p (2Q < 4p, lazy limbs < 2^30): < 8p
+    const F29 X3 = sub29<FqP, 4>(add29_lazy(sqr29<FqP>(R), PPPn), add29_lazy(Q, Q));
+    // Y3 = R (Q - X3 + 9p) + Y PPPn, one shared reduction (6p 11p + 4p 2p < p 2^261), < 2p
+    acc.Y = mul29_sum2<FqP>(R, sub29_lazy<FqP, 9>(Q, X3), acc.Y, PPPn);
+    acc.X = X3;
+}
+
+// -a as K p - a limb by limb, no carries (a normalised, a < (K - 1) p): limbs < 2^30, value < K p.
+// Only for values that feed nothing but mul29 / sqr29 (a base's y, an accumulator's ZZZ).
+template <uint32_t K>
+__device__ __forceinline__ F29 neg29_lazy(const F29& a) {
+    constexpr KPB29<FqP, K> kp{};
+    F29 r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.l[i] = kp.l[i] - a.l[i];
+    return r;
 }
 
 // exceptional case of madd29: x(acc) == x(A); returns the sum (doubling when y(acc) == y(A))

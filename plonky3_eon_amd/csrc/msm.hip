@@ -44,6 +44,7 @@
 #include "ec29.h"
 #include "msm.h"
 #include "sort.h"
+#include "fq_host.h"
 
 using namespace eon;
 
@@ -319,6 +320,10 @@ __global__ void k_piece_owner(const uint32_t* piece_off, uint32_t nb, uint32_t* 
 #ifndef EON_PIECE_MINWAVES
 #define EON_PIECE_MINWAVES 4
 #endif
+// EON_PIECE_NEGSUM=0 builds the round-5 loop (madd29_unchecked, radix-2^32 base negation): A/B
+#ifndef EON_PIECE_NEGSUM
+#define EON_PIECE_NEGSUM 1
+#endif
 
 // Thread t sums the sorted pairs [t 2^log_chunk, (t+1) 2^log_chunk) (nonzero digits only): one
 // partial per bucket run, stored at piece_off[b] + t - (start[b] >> log_chunk).  The XYZZ
@@ -370,14 +375,34 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
         uint32_t run = e0;  // first pair of the current bucket run
         G1X29 acc;
         bool inf = true;
+#if EON_PIECE_NEGSUM
+        // the accumulator holds (-1)^flip times the run's sum (madd29_negsum returns the negated
+        // sum; a run opening with a negative digit starts from the unnegated base with flip set)
+        bool flip = false;
+#endif
         auto flush = [&](uint32_t e_end) __attribute__((always_inline)) {
-            if (!inf && is_zero_mod29<FqP>(acc.ZZ)) inf = piece_run29(vals, pts29, run, e_end, acc);
+            if (!inf && is_zero_mod29<FqP>(acc.ZZ)) {
+                inf = piece_run29(vals, pts29, run, e_end, acc);
+#if EON_PIECE_NEGSUM
+                flip = false;
+#endif
+            }
+#if EON_PIECE_NEGSUM
+            if (flip) acc.ZZZ = neg29_lazy<3>(acc.ZZZ);  // ZZZ < 2p normalised -> 3p - ZZZ
+#endif
             const uint32_t bb = bucket_of(b, c, groups, nb);
             G1Raw29* dst = piece_raw + piece_off[bb] + t - (start[bb] >> log_chunk);
+#if EON_PIECE_NEGSUM
+            // an identity piece is any raw accumulator with ZZ = 0 (every reader tests ZZ alone):
+            // one store of acc either way, instead of selecting all 36 words between acc and zeros
+            if (inf) acc.ZZ = F29{};
+            st_raw29(dst, acc);
+#else
             if (inf)
                 st_raw29_inf(dst);
             else
                 st_raw29(dst, acc);
+#endif
         };
 #ifndef EON_PIECE_SCALAR_PAIRS
         // 16-byte loads of four keys and four references every fourth pair (chunks are aligned to
@@ -432,6 +457,28 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
             G1Affine a = ld_affine(pts29 + (v & 0x7fffffffu));
 #endif
             if (a.y.is_zero()) continue;
+#if EON_PIECE_NEGSUM
+            // the digit's sign and the accumulator's are applied together, as one lazy negation of
+            // the base's y in radix 2^29 (9 subtractions and 9 selects instead of a borrow chain)
+            const bool neg_digit = v >> 31;
+            const F29 ax = unpack29(a.x), ay = unpack29(a.y);
+            if (inf) {
+                acc.X = ax;
+                acc.Y = ay;
+                acc.ZZ = const29<FqP>(R29<FqP>::ONE);
+                acc.ZZZ = acc.ZZ;
+                flip = neg_digit;
+                inf = false;
+            } else {
+                const F29 ayn = neg29_lazy<2>(ay);
+                const bool ng = neg_digit != flip;
+                F29 ys;
+#pragma unroll
+                for (int i = 0; i < 9; i++) ys.l[i] = ng ? ayn.l[i] : ay.l[i];
+                madd29_negsum(acc, ax, ys);
+                flip = !flip;
+            }
+#else
             if (v >> 31) a.y = neg(a.y);
             const F29 ax = unpack29(a.x), ay = unpack29(a.y);
             if (inf) {
@@ -443,6 +490,7 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
             } else {
                 madd29_unchecked(acc, ax, ay);
             }
+#endif
         }
     }
 }
@@ -1106,15 +1154,15 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     const uint64_t E = bt.E;
     const uint32_t nb = bt.nb;
 
-    EON_HIP(wk.keys.ensure(E * 4));
-    EON_HIP(wk.vals.ensure(E * 4));
-    EON_HIP(out.keys2.ensure(E * 4));
-    EON_HIP(out.vals2.ensure(E * 4));
-    EON_HIP(out.start.ensure((nb + 1) * 4ull));
-    EON_HIP(out.piece_off.ensure((nb + 1) * 4ull));
+    EON_HIP(ctx_ensure(ctx, wk.keys, E * 4));
+    EON_HIP(ctx_ensure(ctx, wk.vals, E * 4));
+    EON_HIP(ctx_ensure(ctx, out.keys2, E * 4));
+    EON_HIP(ctx_ensure(ctx, out.vals2, E * 4));
+    EON_HIP(ctx_ensure(ctx, out.start, (nb + 1) * 4ull));
+    EON_HIP(ctx_ensure(ctx, out.piece_off, (nb + 1) * 4ull));
     bt.sort_bytes = radix_sort_temp_bytes(E, bt.key_bits);
     bt.scan_bytes = exclusive_scan_temp_bytes(nb + 1);
-    EON_HIP(wk.temp.ensure(std::max(bt.sort_bytes, bt.scan_bytes)));
+    EON_HIP(ctx_ensure(ctx, wk.temp, std::max(bt.sort_bytes, bt.scan_bytes)));
     bt.log_chunk = LOG_CHUNK_MIN;
     while (bt.log_chunk < LOG_CHUNK_MAX && (E >> (bt.log_chunk + 1)) >= (1ull << 20)) bt.log_chunk++;
     // few buckets for many pairs (a bucket would collect more than ~8 pieces): longer chunks while
@@ -1142,7 +1190,8 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
                        hist);
     prof->end(st);
     EON_HIP(hipGetLastError());
-    prof->begin("radix_sort_pairs", E * 16, st);
+    // every pass reads and writes each (key, value) pair once: 16 bytes per pair and pass
+    prof->begin("radix_sort_pairs", E * 16 * radix_sort_passes(bt.key_bits).passes, st);
     EON_HIP(sort_pairs(wk.temp.p, wk.keys.as<uint32_t>(), out.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
                        out.vals2.as<uint32_t>(), E, bt.key_bits, st, true));
     prof->end(st);
@@ -1151,7 +1200,7 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
                        out.keys2.as<uint32_t>(), E, bt.c, bt.groups, nb, out.start.as<uint32_t>());
     prof->end(st);
     // the most pieces one bucket holds fixes the combine levels (no read-backs in the reduction)
-    EON_HIP(wk.stat.ensure(16));
+    EON_HIP(ctx_ensure(ctx, wk.stat, 16));
     EON_HIP(hipMemsetAsync(wk.stat.p, 0, 16, st));
     EON_HIP(exclusive_scan_chunk_counts(wk.temp.p, out.start.as<uint32_t>(), nb, bt.log_chunk,
                                         out.piece_off.as<uint32_t>(), wk.stat.as<uint32_t>(), st));
@@ -1214,15 +1263,15 @@ static bool sums_reduce(const Batch& bt) {
 // piece sums of one sorted batch against bases `b` (asynchronous); wk supplies the piece buffers
 static Status batch_pieces(eon_ctx* ctx, const eon_msm_bases* b, Batch& bt, const SortedRef& sr,
                            MsmWork& wk, hipStream_t st) {
-    EON_HIP(wk.piece_sums.ensure(std::max<uint64_t>(bt.max_pieces * sizeof(G1Xyzz), (uint64_t)bt.nb * sizeof(G1Raw29))));
-    EON_HIP(wk.piece_sums2.ensure(bt.max_pieces * sizeof(G1Xyzz)));
-    EON_HIP(wk.owner.ensure(bt.max_pieces * 4));
-    EON_HIP(wk.bucket_sums.ensure((uint64_t)bt.nb * sizeof(G1Xyzz)));
-    EON_HIP(wk.off2.ensure((bt.nb + 1) * 4ull));
-    EON_HIP(wk.off3.ensure((bt.nb + 1) * 4ull));
-    EON_HIP(wk.count.ensure((bt.nb + 1) * 4ull));
-    EON_HIP(wk.temp.ensure(bt.scan_bytes));
-    EON_HIP(wk.piece_raw.ensure(bt.max_pieces * sizeof(G1Raw29)));
+    EON_HIP(ctx_ensure(ctx, wk.piece_sums, std::max<uint64_t>(bt.max_pieces * sizeof(G1Xyzz), (uint64_t)bt.nb * sizeof(G1Raw29))));
+    EON_HIP(ctx_ensure(ctx, wk.piece_sums2, bt.max_pieces * sizeof(G1Xyzz)));
+    EON_HIP(ctx_ensure(ctx, wk.owner, bt.max_pieces * 4));
+    EON_HIP(ctx_ensure(ctx, wk.bucket_sums, (uint64_t)bt.nb * sizeof(G1Xyzz)));
+    EON_HIP(ctx_ensure(ctx, wk.off2, (bt.nb + 1) * 4ull));
+    EON_HIP(ctx_ensure(ctx, wk.off3, (bt.nb + 1) * 4ull));
+    EON_HIP(ctx_ensure(ctx, wk.count, (bt.nb + 1) * 4ull));
+    EON_HIP(ctx_ensure(ctx, wk.temp, bt.scan_bytes));
+    EON_HIP(ctx_ensure(ctx, wk.piece_raw, bt.max_pieces * sizeof(G1Raw29)));
     if (!wk.host_counts) EON_HIP(hipHostMalloc(reinterpret_cast<void**>(&wk.host_counts), 64));
     const G1Affine* pts = b->piece_source();
     // algorithmic bytes: n (64 + 32) B per MSM of n terms -- each
@@ -1270,15 +1319,15 @@ static Status reduce_segments(eon_ctx* ctx, const MsmLayout& L, const Batch& bt,
                               MsmWork& wk, hipStream_t st, bool fused, bool sums29 = false) {
     const uint32_t nseg = bt.B / SEG;  // c >= 4, so B >= SEG
     const uint32_t groups = bt.groups;
-    EON_HIP(wk.red_a.ensure((uint64_t)groups * nseg * sizeof(G1Xyzz)));
-    EON_HIP(wk.red_b.ensure((uint64_t)groups * nseg * sizeof(G1Xyzz)));
+    EON_HIP(ctx_ensure(ctx, wk.red_a, (uint64_t)groups * nseg * sizeof(G1Xyzz)));
+    EON_HIP(ctx_ensure(ctx, wk.red_b, (uint64_t)groups * nseg * sizeof(G1Xyzz)));
     ctx->prof.begin("k_segment_sum", (uint64_t)bt.nb * 128 + (uint64_t)groups * nseg * 128, st);
     if (sums29) {
         // raw bucket sums (k_bucket_sums29, in wk.piece_sums as G1Raw29) -> one raw partial per
         // 256 segments -> one point per group, all in radix 2^29
         const uint32_t seg = std::min(bt.B, seg29_for((uint64_t)bt.B * groups));
         const uint32_t bpg = (bt.B / seg + SEG_BLOCK - 1) / SEG_BLOCK;
-        EON_HIP(wk.red_b.ensure((uint64_t)groups * bpg * sizeof(G1Raw29)));
+        EON_HIP(ctx_ensure(ctx, wk.red_b, (uint64_t)groups * bpg * sizeof(G1Raw29)));
         hipLaunchKernelGGL(k_segment_sum29, dim3(groups * bpg), dim3(SEG_BLOCK), 0, st, wk.piece_sums.as<G1Raw29>(),
                            bt.B, seg, bpg, wk.red_b.as<G1Raw29>());
         hipLaunchKernelGGL(k_tree_sum29, dim3(groups), dim3(SEG_BLOCK), 0, st, wk.red_b.as<G1Raw29>(), bpg,
@@ -1351,8 +1400,8 @@ static Status prepare_deferred(eon_ctx* ctx, const MsmLayout& L, uint64_t rows, 
     if (B < SEG) return Status::ok();
     df.nseg = B / SEG;
     df.log_seg = 31 - __builtin_clz(SEG);
-    EON_HIP(ctx->fin_T.ensure(rows * df.nseg * sizeof(G1Raw29)));
-    EON_HIP(ctx->fin_U.ensure(rows * df.nseg * sizeof(G1Raw29)));
+    EON_HIP(ctx_ensure(ctx, ctx->fin_T, rows * df.nseg * sizeof(G1Raw29)));
+    EON_HIP(ctx_ensure(ctx, ctx->fin_U, rows * df.nseg * sizeof(G1Raw29)));
     df.T = ctx->fin_T.as<G1Raw29>();
     df.U = ctx->fin_U.as<G1Raw29>();
     df.out_base = out_base;
@@ -1586,134 +1635,6 @@ static SortedBufs& wks_sorted(eon_ctx* ctx, size_t w) {
 // host anyway, so they are converted there: Montgomery batch inversion with 64-bit limbs (the same
 // R = 2^256 residues, so the bytes equal the device conversion's).
 namespace hostq {
-
-struct F {
-    uint64_t l[4];
-};
-
-static const F& P() {
-    static const F p = [] {
-        F r;
-        for (int i = 0; i < 4; i++) r.l[i] = (uint64_t)FqP::P[2 * i] | ((uint64_t)FqP::P[2 * i + 1] << 32);
-        return r;
-    }();
-    return p;
-}
-
-static uint64_t inv64() {
-    static const uint64_t v = [] {
-        uint64_t x = 1;
-        for (int i = 0; i < 6; i++) x *= 2 - P().l[0] * x;
-        return ~x + 1;
-    }();
-    return v;
-}
-
-static bool is_zero(const F& a) { return (a.l[0] | a.l[1] | a.l[2] | a.l[3]) == 0; }
-
-// a b 2^-256 mod p, canonical (CIOS)
-static F mul(const F& a, const F& b) {
-    const F& p = P();
-    const uint64_t inv = inv64();
-    uint64_t t[6] = {0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < 4; i++) {
-        unsigned __int128 c = 0;
-        for (int j = 0; j < 4; j++) {
-            c += (unsigned __int128)a.l[j] * b.l[i] + t[j];
-            t[j] = (uint64_t)c;
-            c >>= 64;
-        }
-        c += t[4];
-        t[4] = (uint64_t)c;
-        t[5] = (uint64_t)(c >> 64);
-        const uint64_t m = t[0] * inv;
-        c = (unsigned __int128)m * p.l[0] + t[0];
-        c >>= 64;
-        for (int j = 1; j < 4; j++) {
-            c += (unsigned __int128)m * p.l[j] + t[j];
-            t[j - 1] = (uint64_t)c;
-            c >>= 64;
-        }
-        c += t[4];
-        t[3] = (uint64_t)c;
-        t[4] = t[5] + (uint64_t)(c >> 64);
-    }
-    F r{{t[0], t[1], t[2], t[3]}}, d;
-    uint64_t borrow = 0;
-    for (int i = 0; i < 4; i++) {
-        const unsigned __int128 x = (unsigned __int128)t[i] - p.l[i] - borrow;
-        d.l[i] = (uint64_t)x;
-        borrow = (uint64_t)(x >> 64) & 1;
-    }
-    return (t[4] || !borrow) ? d : r;
-}
-
-static bool is_one(const F& a) { return a.l[0] == 1 && (a.l[1] | a.l[2] | a.l[3]) == 0; }
-static bool geq(const F& a, const F& b) {
-    for (int i = 3; i >= 0; i--)
-        if (a.l[i] != b.l[i]) return a.l[i] > b.l[i];
-    return true;
-}
-static void sub_in(F& a, const F& b) {  // a -= b (a >= b)
-    unsigned __int128 br = 0;
-    for (int i = 0; i < 4; i++) {
-        const unsigned __int128 x = (unsigned __int128)a.l[i] - b.l[i] - (uint64_t)br;
-        a.l[i] = (uint64_t)x;
-        br = (x >> 64) & 1;
-    }
-}
-static void add_in(F& a, const F& b) {  // a += b (no overflow: both below 2^255)
-    unsigned __int128 c = 0;
-    for (int i = 0; i < 4; i++) {
-        c += (unsigned __int128)a.l[i] + b.l[i];
-        a.l[i] = (uint64_t)c;
-        c >>= 64;
-    }
-}
-static void shr1(F& a) {
-    for (int i = 0; i < 3; i++) a.l[i] = (a.l[i] >> 1) | (a.l[i + 1] << 63);
-    a.l[3] >>= 1;
-}
-// x / 2 mod p for x < p
-static void half_mod(F& x) {
-    if (x.l[0] & 1) add_in(x, P());
-    shr1(x);
-}
-// x - y mod p for x, y < p
-static void sub_mod(F& x, const F& y) {
-    if (!geq(x, y)) add_in(x, P());
-    sub_in(x, y);
-}
-
-// the Montgomery-form inverse of a = x 2^256 (a != 0): the binary extended Euclid algorithm gives
-// a^-1 mod p (~2 log2 p shift / subtract steps, against ~380 products for a^(p-2)), and one
-// Montgomery product by 2^768 mod p brings it to x^-1 2^256
-static F inverse(const F& a) {
-    static const F r3 = [] {
-        F r2;
-        for (int i = 0; i < 4; i++) r2.l[i] = (uint64_t)FqP::R2[2 * i] | ((uint64_t)FqP::R2[2 * i + 1] << 32);
-        return mul(r2, r2);  // 2^512 2^512 2^-256
-    }();
-    F u = a, v = P(), x1{{1, 0, 0, 0}}, x2{{0, 0, 0, 0}};
-    while (!is_one(u) && !is_one(v)) {
-        while (!(u.l[0] & 1)) {
-            shr1(u);
-            half_mod(x1);
-        }
-        while (!(v.l[0] & 1)) {
-            shr1(v);
-            half_mod(x2);
-        }
-        if (geq(u, v)) {
-            sub_in(u, v);
-            sub_mod(x1, x2);
-        } else {
-            sub_in(v, u);
-            sub_mod(x2, x1);
-        }
-    }
-    return mul(is_one(u) ? x1 : x2, r3);
-}
 
 static F from_dev(const Fq& a) {
     F r;

@@ -94,6 +94,9 @@ struct Profiler {
 inline Fr ntt_scale_form(const Fr& c) { return mul(c, from_u64<FrP>(32)); }
 
 hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof = nullptr);
+// the number of passes (launches) run_network makes for `s`: a one-pass network exchanges nothing
+// between passes and needs no NetworkSpec::mid
+uint32_t network_passes(const NetworkSpec& s);
 hipError_t launch_powers(Fr* out, uint64_t n, const Fr& base, const Fr& scale, uint32_t rev_log,
                          hipStream_t st);
 hipError_t launch_twiddles(Fr* tw, uint32_t* twq, uint32_t L, const Fr& root_L, hipStream_t st);

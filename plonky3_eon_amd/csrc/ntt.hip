@@ -412,14 +412,26 @@ static uint32_t pick_log_cb(uint64_t width) {
     return 0;
 }
 
-hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
-    const uint32_t log_cb = s.log_cb_override >= 0 ? (uint32_t)s.log_cb_override : pick_log_cb(s.width);
+// stages per pass at most, and the pass count, of the network run_network launches for `s`
+static uint32_t plan_passes(const NetworkSpec& s, uint32_t log_cb, uint32_t* n_st_out) {
     const uint32_t log_tile = s.log_tile ? s.log_tile : 10;  // 2^10 elements per tile: 32 KiB of LDS
     uint32_t kmax = log_tile > log_cb ? log_tile - log_cb : 1;
     if (s.max_stages_per_pass && s.max_stages_per_pass < kmax) kmax = s.max_stages_per_pass;
+    const uint32_t n_st = s.log_m > s.first_stage ? s.log_m - s.first_stage : 0;
+    if (n_st_out) *n_st_out = n_st;
+    return n_st == 0 ? 1 : (n_st + kmax - 1) / kmax;
+}
+
+uint32_t network_passes(const NetworkSpec& s) {
+    return plan_passes(s, s.log_cb_override >= 0 ? (uint32_t)s.log_cb_override : pick_log_cb(s.width), nullptr);
+}
+
+hipError_t run_network(const NetworkSpec& s, hipStream_t st, Profiler* prof) {
+    const uint32_t log_cb = s.log_cb_override >= 0 ? (uint32_t)s.log_cb_override : pick_log_cb(s.width);
+    const uint32_t log_tile = s.log_tile ? s.log_tile : 10;
     const uint32_t lo_stage = s.first_stage;
-    const uint32_t n_st = s.log_m > lo_stage ? s.log_m - lo_stage : 0;
-    const uint32_t passes = n_st == 0 ? 1 : (n_st + kmax - 1) / kmax;
+    uint32_t n_st = 0;
+    const uint32_t passes = plan_passes(s, log_cb, &n_st);
     const uint64_t col_tiles = (s.width + (1u << log_cb) - 1) >> log_cb;
     // balanced chunk sizes, assigned bottom-up (stage ranges ascending)
     uint32_t ks[32], s0s[32];

@@ -83,6 +83,24 @@ int eon_rccl_collective_init(uint32_t rank, uint32_t world, const uint8_t id[128
     return EON_OK;
 }
 
+int eon_rccl_collective_info(const eon_collective* coll, int32_t* count, int32_t* user_rank, int32_t* device,
+                             char* pci_bus_id, uint32_t pci_len) {
+    if (!coll || !coll->user || coll->all_gather != rccl_all_gather) return EON_E_ARG;
+    ncclComm_t comm = static_cast<ncclComm_t>(coll->user);
+    int n = -1, r = -1, d = -1;
+    if (ncclCommCount(comm, &n) != ncclSuccess || ncclCommUserRank(comm, &r) != ncclSuccess ||
+        ncclCommCuDevice(comm, &d) != ncclSuccess)
+        return EON_E_DEVICE;
+    if (count) *count = n;
+    if (user_rank) *user_rank = r;
+    if (device) *device = d;
+    if (pci_bus_id && pci_len > 0) {
+        pci_bus_id[0] = 0;
+        if (hipDeviceGetPCIBusId(pci_bus_id, (int)pci_len, d) != hipSuccess) return EON_E_DEVICE;
+    }
+    return EON_OK;
+}
+
 void eon_rccl_collective_finalize(eon_collective* coll) {
     if (!coll || !coll->user) return;
     ncclCommDestroy(static_cast<ncclComm_t>(coll->user));

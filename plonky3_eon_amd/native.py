@@ -50,6 +50,9 @@ SIGNATURES = {
     "eon_kzg_pcs_last_error": (ctypes.c_char_p, [_P]),
     "eon_rccl_unique_id": (_INT, [_P]),
     "eon_rccl_collective_init": (_INT, [_U32, _U32, _P, ctypes.POINTER(eon_collective)]),
+    "eon_rccl_collective_info": (_INT, [ctypes.POINTER(eon_collective), ctypes.POINTER(ctypes.c_int32),
+                                        ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                        ctypes.c_char_p, _U32]),
     "eon_rccl_collective_finalize": (None, [ctypes.POINTER(eon_collective)]),
     "eon_emulated_collective_init": (_INT, [_U32, _U32, ctypes.POINTER(eon_collective)]),
     "eon_prove_p2air": (_INT, [_P, _P, _P, _U64, _P, _P, _U32, ctypes.POINTER(eon_collective),
@@ -117,8 +120,20 @@ class NativeKzgPcs:
             pass
 
 
+class RcclInitError(RuntimeError):
+    """The RCCL communicator could not be made on every rank; raised on EVERY rank alike, so all of
+    them can fall back together (a rank-local failure would leave the others in a collective)."""
+
+
 class RcclCollective:
-    """eon_collective backed by the driver's RCCL communicator."""
+    """eon_collective backed by the driver's RCCL communicator.
+
+    Construction is itself collective over the torch process group `group` and ends the same way
+    on every rank: rank 0 broadcasts the unique id -- or a failure sentinel when
+    eon_rccl_unique_id fails, so the other ranks never wait in a broadcast rank 0 skipped -- every
+    rank initialises its communicator, and the ranks then agree on the outcome (an all-gather of
+    the init codes).  If any rank failed, every rank finalises the communicator it may have made
+    and raises RcclInitError."""
 
     def __init__(self, rank: int, world: int, group=None):
         import torch.distributed as dist
@@ -126,18 +141,44 @@ class RcclCollective:
         self.lib = load()
         self.c = None
         idbuf = (ctypes.c_uint8 * 128)()
+        id_rc = 0
         if rank == 0:
-            rc = self.lib.eon_rccl_unique_id(idbuf)
-            if rc != 0:
-                raise _lib.EonError(rc, "eon_rccl_unique_id")
+            id_rc = self.lib.eon_rccl_unique_id(idbuf)
         if world > 1:
-            obj = [bytes(idbuf)]
+            obj = [bytes(idbuf) if id_rc == 0 else None]
             dist.broadcast_object_list(obj, src=0, group=group)
+            if obj[0] is None:
+                raise RcclInitError("eon_rccl_unique_id failed on rank 0")
             idbuf = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
-        self.c = eon_collective()
-        rc = self.lib.eon_rccl_collective_init(rank, world, idbuf, ctypes.byref(self.c))
+        elif id_rc != 0:
+            raise RcclInitError(f"eon_rccl_unique_id failed ({id_rc})")
+        c = eon_collective()
+        try:
+            rc = self.lib.eon_rccl_collective_init(rank, world, idbuf, ctypes.byref(c))
+        except Exception:  # ctypes-level failure: report it to the other ranks like an error code
+            rc = -1
+        codes = [rc]
+        if world > 1:
+            codes = [None] * world
+            dist.all_gather_object(codes, rc, group=group)
+        if any(x != 0 for x in codes):
+            if rc == 0:
+                self.lib.eon_rccl_collective_finalize(ctypes.byref(c))
+            bad = [g for g, x in enumerate(codes) if x != 0]
+            raise RcclInitError(f"eon_rccl_collective_init failed on ranks {bad} (codes {[codes[g] for g in bad]})")
+        self.c = c
+
+    def info(self) -> dict:
+        """ncclCommCount / ncclCommUserRank / ncclCommCuDevice and the device's PCI bus id, as the
+        communicator reports them (bench.py's N > 1 line carries these per rank)."""
+        n, r, d = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        pci = ctypes.create_string_buffer(64)
+        rc = self.lib.eon_rccl_collective_info(ctypes.byref(self.c), ctypes.byref(n), ctypes.byref(r),
+                                               ctypes.byref(d), pci, 64)
         if rc != 0:
-            raise _lib.EonError(rc, "eon_rccl_collective_init")
+            raise _lib.EonError(rc, "eon_rccl_collective_info")
+        return {"nccl_comm_count": n.value, "nccl_user_rank": r.value, "nccl_cu_device": d.value,
+                "nccl_pci_bus_id": pci.value.decode()}
 
     def close(self):
         if getattr(self, "c", None) is not None and self.c.user:

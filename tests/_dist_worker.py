@@ -397,6 +397,53 @@ def run_openshard(rank, world, group):
     return None
 
 
+def run_rcclagree(rank, world, group):
+    """native.RcclCollective's collective agreement on a fake libeonprove (no GPU): EON_T_FAIL=id
+    fails rank 0's eon_rccl_unique_id, init1 fails rank 1's eon_rccl_collective_init, none fails
+    nothing.  Every rank must end the same way (all raise RcclInitError, or all succeed), and a
+    rank whose own init succeeded must finalise it when another rank failed."""
+    from plonky3_eon_amd import native
+
+    fail = os.environ["EON_T_FAIL"]
+    calls = []
+
+    class FakeLib:
+        def eon_rccl_unique_id(self, buf):
+            calls.append("id")
+            if fail == "id":
+                return -3
+            buf[0] = 42
+            return 0
+
+        def eon_rccl_collective_init(self, r, w, idbuf, out):
+            calls.append("init")
+            if idbuf[0] != 42:
+                return -9  # the id did not arrive
+            return -3 if (fail == "init1" and r == 1) else 0
+
+        def eon_rccl_collective_finalize(self, c):
+            calls.append("finalize")
+
+    saved = native.load
+    native.load = lambda: FakeLib()
+    try:
+        try:
+            native.RcclCollective(rank, world, group)
+            outcome = "ok"
+        except native.RcclInitError:
+            outcome = "raised"
+    finally:
+        native.load = saved
+    want = "ok" if fail == "none" else "raised"
+    if outcome != want:
+        return f"rank {rank}: {outcome}, expected {want} ({calls})"
+    if fail == "id" and "init" in calls:
+        return f"rank {rank} initialised after a failed unique id ({calls})"
+    if fail == "init1" and rank != 1 and "finalize" not in calls:
+        return f"rank {rank} kept its communicator after rank 1 failed ({calls})"
+    return None
+
+
 def main():
     import torch.distributed as dist
 
@@ -414,7 +461,8 @@ def main():
     try:
         fn = {"cpu": run_cpu, "gpu": run_gpu, "a2a": run_a2a, "fourstep": run_fourstep,
               "msmshard": run_msmshard, "native": run_native, "openshard": run_openshard,
-              "fourstep_full": run_fourstep_full, "msmshard_full": run_msmshard_full}[mode]
+              "fourstep_full": run_fourstep_full, "msmshard_full": run_msmshard_full,
+              "rcclagree": run_rcclagree}[mode]
         why = fn(rank, world, None)
     except Exception:
         why = traceback.format_exc()

@@ -51,3 +51,13 @@ def test_shard_range_partition():
         for world in (1, 2, 3, 8):
             r = [D.shard_range(n, g, world) for g in range(world)]
             assert r[0][0] == 0 and r[-1][1] == n and all(a[1] == b[0] for a, b in zip(r, r[1:]))
+
+
+@pytest.mark.parametrize("fail", ["none", "id", "init1"])
+def test_rccl_init_outcome_agreed_gloo(fail):
+    """native.RcclCollective ends the same way on every rank: a failed unique id on
+    rank 0 or a failed communicator init on rank 1 makes every rank raise RcclInitError (so
+    bench.py's fallback to torch.distributed is taken by all ranks together), and no rank waits in
+    a broadcast rank 0 skipped.  Fake driver library, gloo world 3."""
+    res = run_world("rcclagree", 3, timeout=300, extra_env={"EON_T_FAIL": fail})
+    assert all(r["ok"] for r in res), [r["why"] for r in res]

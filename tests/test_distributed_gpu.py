@@ -55,3 +55,35 @@ def test_rccl_process_group_world1(mode, env):
     layouts are the gloo tests above."""
     res = run_world(mode, 1, timeout=900, extra_env=dict(env, EON_T_BACKEND="nccl"))
     assert all(r["ok"] for r in res), [r["why"] for r in res]
+
+
+def test_rccl_collective_info_world1():
+    """The driver's own RCCL communicator at world 1 reports itself (ncclCommCount 1, user rank 0,
+    device 0, that device's PCI bus id), and bench.py's per-rank record of the same process carries
+    those fields beside torch's own PCI address of the device -- the evidence an N-GPU line holds
+    for every rank (bench.py rank_evidence)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    code = (
+        "import json, sys, torch; sys.path.insert(0, %r)\n"
+        "torch.cuda.set_device(0)\n"
+        "import bench\n"
+        "from plonky3_eon_amd.native import RcclCollective\n"
+        "c = RcclCollective(0, 1)\n"
+        "class W: pass\n"
+        "w = W(); w.coll = c; w.collective_kind = 'rccl'\n"
+        "w.throughput = lambda world, ms: ({'stage_ms': {'x': 1.0}}, None)\n"
+        "rec = bench.rank_evidence(w, 0, 0, torch.device('cuda', 0), 0.5, 5, 1)\n"
+        "c.close()\n"
+        "print(json.dumps(rec))\n" % str(root))
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rec["nccl_comm_count"] == 1 and rec["nccl_user_rank"] == 0 and rec["nccl_cu_device"] == 0, rec
+    assert rec["nccl_pci_bus_id"].lower() == rec["pci_bus_id"].lower(), rec  # RCCL's device = torch's
+    assert rec["collective"] == "rccl" and rec["ms_per_step"] == 100.0
+    assert rec["stage_ms"] == {"x": 1.0}

@@ -63,3 +63,11 @@ def test_bench_self_launch_ranks(gpus, extra):
     d = json.loads(lines[0])
     assert d["n_gpus"] == gpus and d["steps"] == 2 and d["cpu_baseline"] is None
     assert d["value"] > 0 and d["roofline"]["achieved"] > 0
+    # the per-rank evidence of an N > 1 line: every rank's record, here all on the one device
+    ranks = d["ranks"]
+    assert [r["rank"] for r in ranks] == list(range(gpus))
+    assert d["distinct_gpus"] == 1 and all(r["device"] == 0 and r["pci_bus_id"] for r in ranks)
+    assert all(r["collective"] == "torch" and r["ms_per_step"] > 0 for r in ranks)
+    assert max(r["ms_per_step"] for r in ranks) <= d["ms_per_step"] + 1e-3
+    if "--workload" not in extra:  # the prove's stages, per rank
+        assert all("commit to trace data" in r["stage_ms"] for r in ranks)

@@ -94,6 +94,33 @@ def test_c2_full_size_properties(gpu_ctx):
         np.testing.assert_array_equal(lh[k, col], C.eval_poly_col(ch, col, pt))
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("order", ["natural", "bitrev"])
+def test_c2_full_size_bit_exact(gpu_ctx, order):
+    """configs[1] at its full size, element for element: the GPU coset LDE of a 2^20 x 64 matrix
+    (added_bits 1, shift GENERATOR = 5) equals the C restatement's -- natural order against
+    coset_lde_batch (Radix2Dit, dft/src/radix_2_dit.rs:61-122 via the trait default
+    dft/src/traits.rs:226-249), bit-reversed storage against Radix2DitParallel's own two-half
+    schedule (dft/src/radix_2_dit_parallel.rs:169-228).  The oracle takes ~8 s on 16 threads."""
+    import torch
+
+    log_n, w, b = 20, 64, 1
+    n = 1 << log_n
+    xh = C.random_fr(2021 + (order == "bitrev"), n * w).reshape(n, w, 4)
+    x = torch.from_numpy(xh.view(np.int64)).to("cuda:0")
+    if order == "natural":
+        got = Radix2Dit(gpu_ctx).coset_lde_batch(x, b, gen()).cpu().numpy().view(np.uint64)
+        want = C.coset_lde_batch(xh, b, gen())
+    else:
+        got = Radix2DitParallel(gpu_ctx).coset_lde_batch(x, b, gen()).storage
+        got = got.cpu().numpy().view(np.uint64) if hasattr(got, "cpu") else got
+        want = C.r2dp_coset_lde_batch(xh, b, gen())
+    del x
+    assert got.shape == want.shape == (n << b, w, 4)
+    bad = np.flatnonzero((got != want).any(axis=(1, 2)))
+    assert bad.size == 0, f"{bad.size} rows differ, first {bad[:8]}"
+
+
 # p - 1 as raw limbs: the largest canonical representation, the worst case of the lazy NTT bounds
 # (DIT outputs grow by < 3p per stage, DIF sums are reduced every other stage; DESIGN.md section 4)
 P_MINUS_1 = np.array([0x43E1F593F0000000, 0x2833E84879B97091, 0xB85045B68181585D, 0x30644E72E131A029],

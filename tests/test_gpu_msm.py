@@ -146,6 +146,29 @@ def test_kzg_identity_full_size(gpu_ctx):
     np.testing.assert_array_equal(MsmBases(pts, gpu_ctx, precompute=False).msm(s), want)
 
 
+@pytest.mark.slow
+def test_msm_full_size_vs_c_pippenger(gpu_ctx):
+    """configs[2] at its full size, bit for bit: the 2^20-point MSM over the alpha = 12345 SRS
+    (fixed-base tables, and the plain bases) equals the C signed-window Pippenger restatement's
+    affine result (G1::multi_exp, bn254/src/curve.rs:158-179; the sum is unique, so the bytes are
+    the reference's), for uniform scalars and for scalars below 2^64 (kzg/benches/kzg_benches.rs)."""
+    import torch
+
+    n = 1 << 20
+    pts = srs_powers(n, 12345, gpu_ctx)
+    bases = MsmBases(pts, gpu_ctx, precompute=True)
+    plain = MsmBases(pts, gpu_ctx, precompute=False)
+    for seed, small in ((2022, False), (2023, True)):
+        s = C.random_fr(seed, n)
+        if small:
+            s = np.stack([C.fr_from_u64(int(v)) for v in
+                          np.random.default_rng(seed).integers(0, 2**63, size=n, dtype=np.int64)])
+        want = C.g1_msm(pts, s)
+        st = torch.from_numpy(s.view(np.int64)).to("cuda:0")
+        np.testing.assert_array_equal(bases.msm(st), want)
+        np.testing.assert_array_equal(plain.msm(s), want)
+
+
 @pytest.mark.parametrize("precompute", [True, False])
 def test_msm_columns_vs_c(gpu_ctx, precompute):
     """KzgPcs::commit's per-column commit_column loop (kzg/src/pcs.rs:244-251) as one batched call."""

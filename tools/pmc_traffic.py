@@ -1,6 +1,9 @@
 """Turns two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) into per-launch HBM traffic of one
-kernel, corrected as MI355X_MICROARCH.md prescribes: counters are in KB (x1024), and on gfx950
-FETCH_SIZE reports half the bytes of a wide coalesced streaming read (x2).
+kernel.  Counters are in KB (x1024).  `bytes_per_launch` is the RAW sum FETCH_SIZE + WRITE_SIZE:
+the guide's x2 on FETCH_SIZE is calibrated for wide coalesced streaming reads (16 B per lane),
+and the MSM piece sums' reads are scattered 16/64-byte table gathers, for which it over-counts
+(DESIGN.md section 4); the x2 figure is kept beside it as `bytes_per_launch_x2_streaming`, an
+upper bound.
 
 usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <kernel-substring> <workload | bench.json> <out.json>
 (a bench.json argument supplies config.workload from that bench line)
@@ -40,8 +43,11 @@ def main():
         "dispatches": {"fetch": len(fetch), "write": len(write)},
         "fetch_size_kb_per_launch": f_kb,
         "write_size_kb_per_launch": w_kb,
-        "bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024),
-        "correction": "bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (gfx950 FETCH_SIZE halves wide reads)",
+        "bytes_per_launch": int(f_kb * 1024 + w_kb * 1024),
+        "bytes_per_launch_x2_streaming": int(2 * f_kb * 1024 + w_kb * 1024),
+        "correction": "bytes = (FETCH_SIZE + WRITE_SIZE) * 1024, raw: the x2 streaming-read correction of "
+                      "FETCH_SIZE does not apply to scattered 16/64-B gathers (bytes_per_launch_x2_streaming "
+                      "applies it, an upper bound)",
         "commit": os.environ.get("EON_COMMIT", "unknown"),
     }
     json.dump(res, open(out, "w"), indent=1)

@@ -147,6 +147,11 @@ typedef struct {
  * report the shader clock the chip held (median over blocks of the last launch) and the product
  * rate (MI355X_MICROARCH.md, DVFS item 6).  Synchronous. */
 int eon_diag_clock_probe(eon_ctx* ctx, uint32_t launches, uint32_t iters, eon_clock_probe* out);
+/* Self-check of the whole-product asm statements the MSM piece sums use (prod_asm.h) against the
+ * column-block products, bit for bit, on n pseudo-random operands of each kind at their limb
+ * bounds (half of them at the maximum limb); mismatches[0..2] = mismatching mul / sqr / sum2
+ * cases. */
+int eon_diag_prod_asm_check(eon_ctx* ctx, uint32_t n, uint32_t seed, uint32_t mismatches[3]);
 
 /* ABI version; bumped on any signature or struct-layout change (4: the verifier pairings and their
  * eon_g2_affine / eon_fq12 types; 3: eon_collective's all_to_all field).  Bindings must check it

@@ -88,6 +88,7 @@ SIGNATURES = {
     "eon_ctx_synchronize": (_INT, [_P]),
     "eon_ctx_trim": (_INT, [_P]),
     "eon_diag_clock_probe": (_INT, [_P, _U32, _U32, _P]),
+    "eon_diag_prod_asm_check": (_INT, [_P, _U32, _U32, _P]),
     "eon_ctx_profile": (_INT, [_P, _INT]),
     "eon_ctx_profile_report": (_INT, [_P, ctypes.c_char_p, _U64]),
     "eon_ctx_set_serial": (_INT, [_P, _INT]),

@@ -54,6 +54,50 @@ __global__ void __launch_bounds__(PROBE_THREADS) k_clock_probe(uint32_t iters, u
     if (h == 0x5bd1e995u) sink[0] = tid;  // keeps both chains live
 }
 
+// The whole-product asm statements (prod_asm.h) against the column-block products of field29.h,
+// bit for bit, on n pseudo-random operands per kind at their contracts' limb bounds (mul29 /
+// sqr29: limbs < 2^30; mul29_sum2: a, c, d < 2^29, b < 2^31) -- every other thread's limbs all at
+// the bound's maximum, the worst column sums.  mism[k] counts the mismatching threads of kind k
+// (0 mul, 1 sqr, 2 sum2).
+__global__ void __launch_bounds__(256) k_prod_asm_check(uint32_t n, uint32_t seed, uint32_t* mism) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    uint32_t s = (t ^ seed) * 2654435761u + 0x9e3779b9u;
+    auto rnd = [&](uint32_t bits) {
+        s ^= s << 13;
+        s ^= s >> 17;
+        s ^= s << 5;
+        const uint32_t m = (1u << bits) - 1;
+        return (t & 1) ? m : (s * 2654435761u) & m;
+    };
+    F29 a, b, c, d;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        a.l[i] = rnd(30);
+        b.l[i] = rnd(30);
+    }
+    const F29 m1 = mul29<FqP>(a, b), m2 = mul29_asm<FqP>(a, b);
+    const F29 q1 = sqr29<FqP>(a), q2 = sqr29_asm<FqP>(a);
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        a.l[i] = rnd(29);
+        b.l[i] = rnd(31);
+        c.l[i] = rnd(29);
+        d.l[i] = rnd(29);
+    }
+    const F29 s1 = mul29_sum2<FqP>(a, b, c, d), s2 = mul29_sum2_asm<FqP>(a, b, c, d);
+    uint32_t e0 = 0, e1 = 0, e2 = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        e0 |= m1.l[i] ^ m2.l[i];
+        e1 |= q1.l[i] ^ q2.l[i];
+        e2 |= s1.l[i] ^ s2.l[i];
+    }
+    if (e0) atomicAdd(mism + 0, 1u);
+    if (e1) atomicAdd(mism + 1, 1u);
+    if (e2) atomicAdd(mism + 2, 1u);
+}
+
 int finish(eon_ctx* ctx, const Status& s) {
     if (s.bad()) ctx->last_error = s.msg;
     return s.code;
@@ -110,6 +154,26 @@ extern "C" int eon_diag_clock_probe(eon_ctx* ctx, uint32_t launches, uint32_t it
         out->clock_mhz_max = mhz.back();
         out->ms_per_launch = ms / launches;
         out->products_per_s = (double)PROBE_BLOCKS * PROBE_THREADS * 2.0 * iters * launches / (ms * 1e-3);
+        return Status::ok();
+    }();
+    return finish(ctx, s);
+}
+
+extern "C" int eon_diag_prod_asm_check(eon_ctx* ctx, uint32_t n, uint32_t seed, uint32_t mismatches[3]) {
+    if (!ctx) return EON_E_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return EON_E_DEVICE;
+    Status s = [&]() -> Status {
+        if (!mismatches) return Status::err(EON_E_ARG, "null argument");
+        DevBuf cnt;
+        PoolScope ps(ctx->pool, ctx->stream);
+        EON_HIP(ps.take(cnt, 64));
+        EON_HIP(hipMemsetAsync(cnt.p, 0, 16, ctx->stream));
+        if (n) hipLaunchKernelGGL(k_prod_asm_check, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, n, seed,
+                                  cnt.as<uint32_t>());
+        EON_HIP(hipGetLastError());
+        EON_HIP(hipMemcpyAsync(mismatches, cnt.p, 12, hipMemcpyDeviceToHost, ctx->stream));
+        EON_HIP(hipStreamSynchronize(ctx->stream));
         return Status::ok();
     }();
     return finish(ctx, s);

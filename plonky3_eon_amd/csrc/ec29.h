@@ -83,19 +83,23 @@ __device__ __forceinline__ void madd29_unchecked(G1X29& acc, const F29& ax, cons
 // (neg_zzz29_lazy).  Same bounds as madd29: X3 < 8p, Y3 < 2p, ZZ3, ZZZ3 < 2p normalised; ay may be
 // a lazy negation (limbs < 2^30, value < 2p: it only feeds mul29).
 __device__ __forceinline__ void madd29_negsum(G1X29& acc, const F29& ax, const F29& ay) {
-    const F29 U2 = mul29<FqP>(ax, acc.ZZ);            // < 2p
-    const F29 Pn = sub29<FqP, 2>(acc.X, U2);          // X - U2 + 2p < 10p
-    const F29 PP = sqr29<FqP>(Pn);                     // < 2p
-    const F29 PPPn = mul29<FqP>(Pn, PP);              // -PPP, < 2p
-    const F29 Q = mul29<FqP>(acc.X, PP);              // < 2p
-    const F29 S2 = mul29<FqP>(ay, acc.ZZZ);           // < 2p
+    F29 U2 = ax;
+    mul29_ip<FqP>(U2, acc.ZZ);                         // < 2p
+    F29 Pn = sub29<FqP, 2>(acc.X, U2);                // X - U2 + 2p < 10p
+    const F29 PP = sqr29_x<FqP>(Pn);                   // < 2p
+    F29 Q = acc.X;
+    mul29_ip<FqP>(Q, PP);                              // < 2p
+    F29 S2 = ay;
+    mul29_ip<FqP>(S2, acc.ZZZ);                        // < 2p
     const F29 R = sub29<FqP, 4>(S2, acc.Y);           // < 6p
-    acc.ZZ = mul29<FqP>(acc.ZZ, PP);                  // < 2p
-    acc.ZZZ = mul29<FqP>(acc.ZZZ, PPPn);              // -ZZZ3, < 2p
+    mul29_ip<FqP>(acc.ZZ, PP);                         // < 2p
+    mul29_ip<FqP>(Pn, PP);                             // PPPn = -PPP, < 2p
+    const F29 PPPn = Pn;
+    mul29_ip<FqP>(acc.ZZZ, PPPn);                      // -ZZZ3, < 2p
     // X3 = R^2 + PPPn - 2Q + 4p (2Q < 4p, lazy limbs < 2^30): < 8p
-    const F29 X3 = sub29<FqP, 4>(add29_lazy(sqr29<FqP>(R), PPPn), add29_lazy(Q, Q));
+    const F29 X3 = sub29<FqP, 4>(add29_lazy(sqr29_x<FqP>(R), PPPn), add29_lazy(Q, Q));
     // Y3 = R (Q - X3 + 9p) + Y PPPn, one shared reduction (6p 11p + 4p 2p < p 2^261), < 2p
-    acc.Y = mul29_sum2<FqP>(R, sub29_lazy<FqP, 9>(Q, X3), acc.Y, PPPn);
+    mul29_sum2_ip<FqP>(R, sub29_lazy<FqP, 9>(Q, X3), acc.Y, PPPn);
     acc.X = X3;
 }
 

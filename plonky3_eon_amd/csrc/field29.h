@@ -854,6 +854,58 @@ EON_HD F29 uniform29(const F29& a) {
     return r;
 }
 
+// Whole products as one asm statement each (prod_asm.h, generated by tools/gen_prod_asm.py): the
+// same column schedule and results as mul29 / sqr29 / mul29_sum2, without the wait state hipcc
+// puts after every asm statement (one per column above).  EON_PRODUCT_ASM=0 routes the *_x
+// entry points to the column-block versions (A/B).
+#ifndef EON_PRODUCT_ASM
+#define EON_PRODUCT_ASM 1
+#endif
+}  // namespace eon
+#include "prod_asm.h"
+namespace eon {
+template <class M>
+EON_HD F29 mul29_x(const F29& a, const F29& b) {
+#if defined(__HIP_DEVICE_COMPILE__) && EON_PRODUCT_ASM
+    return mul29_asm<M>(a, b);
+#else
+    return mul29<M>(a, b);
+#endif
+}
+template <class M>
+EON_HD F29 sqr29_x(const F29& a) {
+#if defined(__HIP_DEVICE_COMPILE__) && EON_PRODUCT_ASM && EON_SQR_DOUBLED
+    return sqr29_asm<M>(a);
+#else
+    return sqr29<M>(a);
+#endif
+}
+template <class M>
+EON_HD F29 mul29_sum2_x(const F29& a, const F29& b, const F29& c, const F29& d) {
+#if defined(__HIP_DEVICE_COMPILE__) && EON_PRODUCT_ASM
+    return mul29_sum2_asm<M>(a, b, c, d);
+#else
+    return mul29_sum2<M>(a, b, c, d);
+#endif
+}
+// in place: a = a b, c = a b + c d (a loop-carried accumulator updated without a register copy)
+template <class M>
+EON_HD void mul29_ip(F29& a, const F29& b) {
+#if defined(__HIP_DEVICE_COMPILE__) && EON_PRODUCT_ASM
+    mul29_asm_ip<M>(a, b);
+#else
+    a = mul29<M>(a, b);
+#endif
+}
+template <class M>
+EON_HD void mul29_sum2_ip(const F29& a, const F29& b, F29& c, const F29& d) {
+#if defined(__HIP_DEVICE_COMPILE__) && EON_PRODUCT_ASM
+    mul29_sum2_asm_ip<M>(a, b, c, d);
+#else
+    c = mul29_sum2<M>(a, b, c, d);
+#endif
+}
+
 // ---- compile-time overflow guard for the unmasked Montgomery multipliers --------------------------
 // Worst case of every 64-bit column accumulator of mul29 / sqr29 / mul29_sum2: every operand limb
 // at its contract maximum (`prod_max` = the operand products one column position can add), every

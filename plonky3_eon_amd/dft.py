@@ -80,6 +80,13 @@ class Context:
         self.check(self.lib.eon_diag_clock_probe(self._h, int(launches), int(iters), ctypes.byref(r)))
         return {k: getattr(r, k) for k, _ in r._fields_}
 
+    def prod_asm_check(self, n: int = 1 << 20, seed: int = 1) -> list:
+        """Diagnostic (eon_diag_prod_asm_check): mismatching cases of the whole-product asm
+        statements against the column-block products (mul, sqr, sum2), n random operands each."""
+        r = (ctypes.c_uint32 * 3)()
+        self.check(self.lib.eon_diag_prod_asm_check(self._h, int(n), int(seed), r))
+        return list(r)
+
     def close(self):
         if getattr(self, "_h", None):
             self.lib.eon_ctx_destroy(self._h)

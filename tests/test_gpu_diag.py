@@ -44,3 +44,11 @@ def test_trim_between_msms_keeps_results(gpu_ctx):
         np.testing.assert_array_equal(bases.msm(scal), want)
         bases.close()
         gpu_ctx.trim()
+
+
+def test_prod_asm_matches_column_products(gpu_ctx):
+    """The whole-product asm statements of the piece sums (prod_asm.h, tools/gen_prod_asm.py) equal
+    the column-block mul29 / sqr29 / mul29_sum2 bit for bit on 2^22 operands of each kind at the
+    contracts' limb bounds, half of them with every limb at its maximum."""
+    for seed in (1, 2, 3, 4):
+        assert gpu_ctx.prod_asm_check(1 << 20, seed) == [0, 0, 0]

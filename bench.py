@@ -58,6 +58,13 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # 1.80e11/s; the radix-2^32 FIPS product of the quotient kernel peaks at 1.29e11/s,
 # tools/ubench_mulmod.hip)
 MULMOD_PEAK_PER_S = 1.80e11
+# k_piece_sum29's instruction-issue cost per wave-addition: its gfx950 ISA (the addition block, the
+# per-pair loads / unpack / key logic, the flush and run-start paths weighted by how often a wave
+# takes them) priced with the measured SIMD cycles per wave-instruction at 4 waves per SIMD
+SIMDS = 1024  # 256 CUs x 4 SIMDs
+PIECE_ISSUE_CYCLES = 9550
+PIECE_ISSUE_SOURCE = ("tools/isa_count.py --costs profiles/r06/s4/ubench_isa2.txt over the round-6 build: "
+                      "addition block 9067 + per pair ~250 + (flush ~206 + run start ~93) x 0.77 (profiles/r06/s5/INDEX.md)")
 # PMC traffic files are read from this round's profile directory only (see main())
 TRAFFIC_ROUND = "r06"
 FR_P = [0x43E1F593F0000001, 0x2833E84879B97091, 0xB85045B68181585D, 0x30644E72E131A029]
@@ -1076,6 +1083,19 @@ def main() -> int:
             # the same kernel against the product rate this box sustained at the clock it held
             roof["valu"]["peak_live_mulmod_per_s"] = round(clock["products_per_s"], 1)
             roof["valu"]["frac_live"] = round(rate / clock["products_per_s"], 4)
+            if kname == "k_piece_sum":
+                # the piece sums against their own instruction-issue floor at this clock: the gfx950
+                # ISA of the loop weighted by the measured issue cost of each instruction
+                # (tools/isa_count.py --costs, tools/ubench_isa2.hip)
+                adds = rate / 10  # 10 algorithmic products per XYZZ mixed addition
+                floor = SIMDS * 64 * clock["clock_mhz_median"] * 1e6 / PIECE_ISSUE_CYCLES
+                roof["valu"]["issue_floor"] = {
+                    "cycles_per_wave_addition": PIECE_ISSUE_CYCLES,
+                    "additions_per_s": round(adds, 1),
+                    "floor_additions_per_s": round(floor, 1),
+                    "frac": round(adds / floor, 4),
+                    "source": PIECE_ISSUE_SOURCE,
+                }
     if mulmods is not None:
         roof["valu_whole_step"] = {
             "achieved_mulmod_per_s": round(mulmods / (gpu_total_ms * 1e-3), 1),

@@ -85,7 +85,10 @@ __global__ void __launch_bounds__(256) k_valu(const uint32_t* ys, W w, uint32_t*
             acc >>= 29;
         }
         r[17] = (uint32_t)acc;
-        y[0] ^= r[3] & 1u;  // a dependence between repetitions (keeps the loop honest)
+        // the next repetition multiplies the high half of this product: every limb depends on the
+        // previous one (a single-bit feedback let the compiler hoist the other limbs' products)
+#pragma unroll
+        for (int i = 0; i < 9; i++) y[i] = r[9 + i] & (i == 8 ? 0x3fffffu : M29);
     }
 #pragma unroll
     for (int i = 0; i < 18; i++) out[t * 18 + i] = r[i];
@@ -159,7 +162,8 @@ __global__ void __launch_bounds__(256) k_mfma(const uint32_t* ys, W w, uint32_t*
             acc >>= 29;
         }
         r[17] = (uint32_t)acc;
-        y[0] ^= r[3] & 1u;  // a dependence between repetitions
+#pragma unroll
+        for (int i = 0; i < 9; i++) y[i] = r[9 + i] & (i == 8 ? 0x3fffffu : M29);
         __syncthreads();
     }
 #pragma unroll
@@ -191,8 +195,8 @@ int main() {
     hipMalloc(&o2, (size_t)n * 18 * 4);
     hipMemcpy(dy, hy.data(), hy.size() * 4, hipMemcpyHostToDevice);
     // correctness: one repetition each
-    hipLaunchKernelGGL(k_valu, dim3(blocks), dim3(256), 0, 0, dy, w, o1, 1);
-    hipLaunchKernelGGL(k_mfma, dim3(blocks), dim3(256), 0, 0, dy, w, o2, 1);
+    hipLaunchKernelGGL(k_valu, dim3(blocks), dim3(256), 0, 0, dy, w, o1, 3);
+    hipLaunchKernelGGL(k_mfma, dim3(blocks), dim3(256), 0, 0, dy, w, o2, 3);
     hipDeviceSynchronize();
     std::vector<uint32_t> h1((size_t)n * 18), h2((size_t)n * 18);
     hipMemcpy(h1.data(), o1, h1.size() * 4, hipMemcpyDeviceToHost);

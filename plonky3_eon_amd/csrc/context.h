@@ -141,6 +141,7 @@ struct SortedBufs {
 struct MsmWork {
     DevBuf keys, vals, count, off2, off3, owner, piece_sums, piece_sums2, bucket_sums, red_a, red_b,
         temp, results, piece_raw, stat;
+    DevBuf canon;  // canonical scalars, column-major (the fused digit sort, msm.hip)
     SortedBufs sorted;
     uint32_t* host_counts = nullptr;  // pinned read-back slots
     hipEvent_t counts_ev = nullptr;   // recorded after the count read-back's copies
@@ -153,7 +154,7 @@ struct MsmWork {
         if (counts_ev) (void)hipEventDestroy(counts_ev);
         counts_ev = nullptr;
         for (DevBuf* b : {&keys, &vals, &count, &off2, &off3, &owner, &piece_sums, &piece_sums2,
-                          &bucket_sums, &red_a, &red_b, &temp, &results, &piece_raw, &stat})
+                          &bucket_sums, &red_a, &red_b, &temp, &results, &piece_raw, &stat, &canon})
             b->release();
         sorted.release();
     }

@@ -44,6 +44,7 @@
 #include "ec29.h"
 #include "msm.h"
 #include "sort.h"
+#include "sort_pass.h"
 #include "fq_host.h"
 
 using namespace eon;
@@ -120,7 +121,7 @@ __global__ void __launch_bounds__(256) k_msm_digits(const Fr* scalars, uint64_t 
                                                     uint32_t cols, uint32_t c, uint32_t windows,
                                                     uint32_t ref_windows, uint32_t precomputed,
                                                     uint32_t tile_cols, uint32_t* keys, uint32_t* vals,
-                                                    RadixPasses pb, uint32_t* hist) {
+                                                    RadixPasses pb, uint32_t* hist, Fr* /* k_msm_digits4's */) {
     __shared__ uint32_t h[RADIX_SORT_MAX_PASSES][256];
     for (uint32_t j = threadIdx.x; j < RADIX_SORT_MAX_PASSES * 256; j += 256) (&h[0][0])[j] = 0;
     __syncthreads();
@@ -174,12 +175,15 @@ __global__ void __launch_bounds__(256) k_msm_digits(const Fr* scalars, uint64_t 
 // The same pairs with four consecutive rows per thread (n a multiple of 4): a lane writes a
 // window's four keys and four references as one 16-byte store each, so a store instruction covers
 // tile_cols runs of 16 * 4 rows (256 contiguous bytes per column) instead of tile_cols runs of 64
-// bytes.  A tile is 256 / tile_cols row quads of tile_cols adjacent columns.
+// bytes.  A tile is 256 / tile_cols row quads of tile_cols adjacent columns.  WRITE = false: the
+// histograms and the canonical scalars column-major (canon[col n + i]) instead of the pairs, for
+// the fused first sort pass (k_digit_sort_pass computes the pairs again from them).
+template <bool WRITE>
 __global__ void __launch_bounds__(256) k_msm_digits4(const Fr* scalars, uint64_t n, uint64_t ld,
                                                      uint32_t cols, uint32_t c, uint32_t windows,
                                                      uint32_t ref_windows, uint32_t precomputed,
                                                      uint32_t tile_cols, uint32_t* keys, uint32_t* vals,
-                                                     RadixPasses pb, uint32_t* hist) {
+                                                     RadixPasses pb, uint32_t* hist, Fr* canon) {
     __shared__ uint32_t h[RADIX_SORT_MAX_PASSES][256];
     for (uint32_t j = threadIdx.x; j < RADIX_SORT_MAX_PASSES * 256; j += 256) (&h[0][0])[j] = 0;
     __syncthreads();
@@ -193,6 +197,10 @@ __global__ void __launch_bounds__(256) k_msm_digits4(const Fr* scalars, uint64_t
         for (int r = 0; r < 4; r++) {
             s[r] = canonical_from_mont(ld_pinned(scalars + (i + r) * ld + col));
             pin(s[r]);
+        }
+        if (!WRITE) {  // the canonical scalars, column-major, for the fused first sort pass
+#pragma unroll
+            for (int r = 0; r < 4; r++) st_vec(canon + (uint64_t)col * n + i + r, s[r]);
         }
         uint32_t carry[4] = {0, 0, 0, 0};
         for (uint32_t w = 0; w < windows; w++) {
@@ -223,9 +231,11 @@ __global__ void __launch_bounds__(256) k_msm_digits4(const Fr* scalars, uint64_t
                 for (uint32_t p = 0; p < RADIX_SORT_MAX_PASSES; p++)
                     if (p < pb.passes) atomicAdd(&h[p][(key[r] >> pb.shift[p]) & ((1u << pb.bits[p]) - 1)], 1u);
             }
-            const uint64_t e = ((uint64_t)col * windows + w) * n + i;
-            *reinterpret_cast<uint4*>(keys + e) = make_uint4(key[0], key[1], key[2], key[3]);
-            *reinterpret_cast<uint4*>(vals + e) = make_uint4(val[0], val[1], val[2], val[3]);
+            if (WRITE) {
+                const uint64_t e = ((uint64_t)col * windows + w) * n + i;
+                *reinterpret_cast<uint4*>(keys + e) = make_uint4(key[0], key[1], key[2], key[3]);
+                *reinterpret_cast<uint4*>(vals + e) = make_uint4(val[0], val[1], val[2], val[3]);
+            }
         }
     }
     __syncthreads();
@@ -233,6 +243,55 @@ __global__ void __launch_bounds__(256) k_msm_digits4(const Fr* scalars, uint64_t
         const uint32_t v = (&h[0][0])[j];
         if (v) atomicAdd(hist + j, v);
     }
+}
+
+// The first (low-byte) pass of the digit sort fused with the digit extraction, for fixed-base
+// tables with c = 16 and 16 windows: the pairs are ranked as they are computed from the scalars,
+// never written unsorted nor read back (k_msm_digits4 + the first k_sort_pass moved 8 + 16 bytes
+// per pair; this pass reads 2 of canonical scalar, coalesced, and writes 8; the histogram kernel
+// before it writes the canonical scalars column-major).  Tile t covers rows [r0, r0 + SORT_THREADS)
+// of column col = t / tiles_per_col (r0 = (t % tiles_per_col) SORT_THREADS, n a multiple of
+// SORT_THREADS): thread (w, lane) takes row r0 + 64 w + lane and its 16 window digits are its 16
+// items.  Within a column the pairs are ranked in another order than k_msm_digits' (window-major),
+// but the tiles run column by column, so after both passes every bucket (digit, column) is still
+// one contiguous run -- the only order the piece sums rely on (a bucket's sum is order-free).
+struct DigitSource {
+    const Fr* canon;  // canonical scalars, column-major (k_msm_digits4<false>)
+    uint64_t n;
+    uint32_t tiles_per_col, ref_windows;
+    template <bool FULL>
+    __device__ __forceinline__ void load(uint32_t tile, uint32_t w, uint32_t lane, uint32_t,
+                                         uint32_t (&key)[sortpass::SORT_ITEMS],
+                                         uint32_t (&val)[sortpass::SORT_ITEMS]) const {
+        static_assert(sortpass::SORT_ITEMS == 16, "one item per 16-bit window of a 256-bit scalar");
+        const uint32_t col = tile / tiles_per_col;
+        const uint64_t i = (uint64_t)(tile - col * tiles_per_col) * sortpass::SORT_THREADS + w * 64 + lane;
+        const Fr s = ld_pinned(canon + (uint64_t)col * n + i);
+        uint32_t carry = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 16; j++) {
+            const uint32_t raw = ((s.v[j >> 1] >> (16 * (j & 1))) & 0xffffu) + carry;
+            uint32_t mag, neg;
+            if (raw > (1u << 15)) {  // signed digit raw - 2^16, carry into the next window
+                mag = (1u << 16) - raw;
+                neg = 1;
+                carry = 1;
+            } else {
+                mag = raw;
+                neg = 0;
+                carry = 0;
+            }
+            key[j] = mag ? (col << 16 | (mag - 1)) : 0xFFFFFFFFu;
+            val[j] = mag ? ((uint32_t)(i * ref_windows + j) | neg << 31) : 0u;
+        }
+    }
+};
+
+__global__ void __launch_bounds__(sortpass::SORT_THREADS) k_digit_sort_pass(DigitSource src, uint32_t* kd, uint32_t* vd,
+                                                                            uint32_t n, uint32_t shift,
+                                                                            const uint32_t* base, uint64_t* status,
+                                                                            uint32_t* tile_ctr) {
+    sortpass::sort_pass_tile<8>(src, kd, vd, n, shift, 8, base, status, tile_ctr);
 }
 
 // OR of every canonical scalar into or_out[8] (zeroed before): its top set bit bounds the
@@ -1017,6 +1076,13 @@ Status bases_create(eon_ctx* ctx, const eon_g1_affine* bases, uint64_t n, uint32
         if (e != hipSuccess) return fail(Status::err(EON_E_DEVICE, hipGetErrorString(e)));
     }
     b->precomputed = (flags & EON_MSM_PRECOMPUTE) != 0 && n > 0;
+    // EON_MSM_FORCE_C (tests): the window width of a fixed-base table, e.g. c = 16 at sizes whose
+    // own choice is narrower, so the fused digit sort (batch_sort) runs at test sizes
+    if (!force_c && b->precomputed) {
+        const char* fc = getenv("EON_MSM_FORCE_C");
+        const int v = fc ? atoi(fc) : 0;
+        if (v >= 4 && v <= 20) force_c = (uint32_t)v;
+    }
     b->c = force_c ? force_c : choose_c(n ? n : 1, b->precomputed);
     b->windows = (255 + b->c - 1) / b->c;
     if (b->precomputed) {
@@ -1130,6 +1196,12 @@ static std::vector<Batch> make_batches(const Fr* scalars, uint32_t width, uint64
     return batches;
 }
 
+// EON_MSM_FUSED_SORT (default 1): the digit sort's first pass ranks the digits as k_digit_sort_pass
+// computes them (batch_sort); 0 restores k_msm_digits4 + two k_sort_pass passes
+#ifndef EON_MSM_FUSED_SORT
+#define EON_MSM_FUSED_SORT 1
+#endif
+
 // The digit sort: sort.hip's stable LSD radix sort (two 8-bit passes for c = 16)
 static hipError_t sort_pairs(void* temp, const uint32_t* k_in, uint32_t* k_out, const uint32_t* v_in,
                              uint32_t* v_out, uint64_t n, uint32_t bits, hipStream_t st, bool hist_ready) {
@@ -1175,7 +1247,6 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     Profiler* prof = &ctx->prof;
     uint32_t* hist = radix_sort_histograms(wk.temp.p, E);
     EON_HIP(hipMemsetAsync(hist, 0, RADIX_SORT_MAX_PASSES * 256 * 4, st));
-    prof->begin("k_msm_digits", n * bt.cols * 32 + E * 8, st);
     const uint32_t tile_cols = bt.cols >= DIGIT_COLS ? DIGIT_COLS : (bt.cols >= 2 ? 2 : 1);
     // four rows per thread (16-byte stores) when n allows it, k_msm_digits otherwise: 6.2 vs 10.4 ms
     // of digits per prove (round 4, profiles/r04/s19)
@@ -1184,17 +1255,49 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     const uint32_t grid_y = (bt.cols + tile_cols - 1) / tile_cols;
     const uint64_t tiles = (n + tile_rows - 1) / tile_rows;
     const uint32_t grid_x = (uint32_t)std::min<uint64_t>(tiles, std::max<uint32_t>(1, DIGIT_BLOCKS / grid_y));
-    hipLaunchKernelGGL(quad ? k_msm_digits4 : k_msm_digits, dim3(grid_x, grid_y),
-                       dim3(256), 0, st, bt.scalars, n, ld, bt.cols, bt.c, bt.W, L.W, (uint32_t)L.precomputed,
-                       tile_cols, wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>(), radix_sort_passes(bt.key_bits),
-                       hist);
-    prof->end(st);
-    EON_HIP(hipGetLastError());
-    // every pass reads and writes each (key, value) pair once: 16 bytes per pair and pass
-    prof->begin("radix_sort_pairs", E * 16 * radix_sort_passes(bt.key_bits).passes, st);
-    EON_HIP(sort_pairs(wk.temp.p, wk.keys.as<uint32_t>(), out.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
-                       out.vals2.as<uint32_t>(), E, bt.key_bits, st, true));
-    prof->end(st);
+    // the first sort pass fused with the digits (DigitSource): fixed-base tables, c = 16, all 16
+    // windows, whole 1024-row tiles, two passes
+    const bool fused = EON_MSM_FUSED_SORT && L.precomputed && bt.c == 16 && bt.W == 16 && L.W == 16 &&
+                       n % sortpass::SORT_THREADS == 0 && radix_sort_passes(bt.key_bits).passes == 2;
+    if (fused) {
+        EON_HIP(ctx_ensure(ctx, wk.canon, n * bt.cols * sizeof(Fr)));
+        prof->begin("k_msm_digit_hist", n * bt.cols * 64, st);
+        hipLaunchKernelGGL(k_msm_digits4<false>, dim3(grid_x, grid_y), dim3(256), 0, st, bt.scalars, n, ld, bt.cols,
+                           bt.c, bt.W, L.W, 1u, tile_cols, nullptr, nullptr, radix_sort_passes(bt.key_bits), hist,
+                           wk.canon.as<Fr>());
+        prof->end(st);
+        EON_HIP(hipGetLastError());
+        EON_HIP(radix_sort_prepare(wk.temp.p, E, bt.key_bits, st));
+        const RadixPassArgs a0 = radix_sort_pass_args(wk.temp.p, E, bt.key_bits, 0);
+        // per call: the attribute is per device (another context may run on another GPU)
+        EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_digit_sort_pass),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sortpass::SORT_LDS));
+        // the pass's own traffic: 32 bytes of scalar per 16 pairs read, 8 bytes per pair written
+        prof->begin("k_digit_sort_pass", n * bt.cols * 32 + E * 8, st);
+        const DigitSource src{wk.canon.as<Fr>(), n, (uint32_t)(n / sortpass::SORT_THREADS), L.W};
+        hipLaunchKernelGGL(k_digit_sort_pass, dim3(a0.tiles), dim3(sortpass::SORT_THREADS), sortpass::SORT_LDS, st, src,
+                           wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>(), (uint32_t)E, a0.shift, a0.base, a0.status,
+                           a0.tile_ctr);
+        prof->end(st);
+        EON_HIP(hipGetLastError());
+        prof->begin("radix_sort_pairs", E * 16, st);  // the second pass
+        EON_HIP(radix_sort_tail(wk.temp.p, wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>(), out.keys2.as<uint32_t>(),
+                                out.vals2.as<uint32_t>(), E, bt.key_bits, st));
+        prof->end(st);
+    } else {
+        prof->begin("k_msm_digits", n * bt.cols * 32 + E * 8, st);
+        hipLaunchKernelGGL(quad ? k_msm_digits4<true> : k_msm_digits, dim3(grid_x, grid_y),
+                           dim3(256), 0, st, bt.scalars, n, ld, bt.cols, bt.c, bt.W, L.W, (uint32_t)L.precomputed,
+                           tile_cols, wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>(), radix_sort_passes(bt.key_bits),
+                           hist, nullptr);
+        prof->end(st);
+        EON_HIP(hipGetLastError());
+        // every pass reads and writes each (key, value) pair once: 16 bytes per pair and pass
+        prof->begin("radix_sort_pairs", E * 16 * radix_sort_passes(bt.key_bits).passes, st);
+        EON_HIP(sort_pairs(wk.temp.p, wk.keys.as<uint32_t>(), out.keys2.as<uint32_t>(), wk.vals.as<uint32_t>(),
+                           out.vals2.as<uint32_t>(), E, bt.key_bits, st, true));
+        prof->end(st);
+    }
     prof->begin("k_bucket_start", E * 4, st);
     hipLaunchKernelGGL(k_bucket_start, dim3(blocks_for(E / BS_KEYS + 1, 256)), dim3(256), 0, st,
                        out.keys2.as<uint32_t>(), E, bt.c, bt.groups, nb, out.start.as<uint32_t>());

@@ -36,6 +36,26 @@ size_t radix_sort_temp_bytes(uint64_t n, uint32_t bits);
 hipError_t radix_sort_pairs(void* temp, const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
                             uint32_t* vals_out, uint64_t n, uint32_t bits, hipStream_t st, bool hist_ready = false);
 
+// A sort whose FIRST pass is run by the producer of the pairs over pairs it computes instead of
+// stored ones (sort_pass.h's sort_pass_tile over its own source, one block of SORT_THREADS threads
+// and SORT_LDS bytes of LDS per tile, radix_sort_pass_args(.., 0).tiles tiles; the MSM's digit
+// pairs, msm.hip).  The histograms of every pass ready in radix_sort_histograms(temp, n):
+//   radix_sort_prepare  the digit offsets of every pass and the zeroed look-back state;
+//   (the producer's first pass, with radix_sort_pass_args(temp, n, bits, 0))
+//   radix_sort_tail     passes 1 .. from the first pass's output (>= 2 passes), the last one into
+//                       keys_out / vals_out.
+struct RadixPassArgs {
+    uint32_t shift, bits;
+    const uint32_t* base;  // the pass's 256 digit offsets
+    uint64_t* status;      // its tiles' look-back words (zeroed by radix_sort_prepare)
+    uint32_t* tile_ctr;    // its virtual tile counter
+    uint32_t tiles;
+};
+hipError_t radix_sort_prepare(void* temp, uint64_t n, uint32_t bits, hipStream_t st);
+RadixPassArgs radix_sort_pass_args(void* temp, uint64_t n, uint32_t bits, uint32_t q);
+hipError_t radix_sort_tail(void* temp, const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_out,
+                           uint32_t* vals_out, uint64_t n, uint32_t bits, hipStream_t st);
+
 // Scratch bytes of exclusive_scan_u32 for n elements.
 size_t exclusive_scan_temp_bytes(uint64_t n);
 

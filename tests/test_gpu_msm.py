@@ -182,6 +182,34 @@ def test_msm_columns_vs_c(gpu_ctx, precompute):
     assert not got[3].any()
 
 
+@pytest.mark.parametrize("rows", [4096, 4100])
+def test_fused_digit_sort_columns_vs_c(gpu_ctx, monkeypatch, rows):
+    """The digit sort's first pass fused with the digit extraction (k_digit_sort_pass: fixed-base
+    tables with c = 16, 16 windows, rows a multiple of 1024 -- the headline prove's shape, forced
+    here at 4096 rows by EON_MSM_FORCE_C); 4100 rows take the unfused route at the same c.  Several
+    columns per batch check that every (digit, column) bucket stays one run."""
+    monkeypatch.setenv("EON_MSM_FORCE_C", "16")
+    width = 5
+    pts = srs_powers(rows, 777, gpu_ctx)
+    mat = C.random_fr(41, rows * width).reshape(rows, width, 4)
+    mat[:, 1] = 0  # an all-zero column
+    mat[: rows // 2, 2] = mat[0, 2]  # half the rows one scalar: long runs in few buckets
+    r_minus_1 = np.array(O.int_to_limbs(O.to_mont(O.P - 1)), dtype=np.uint64)
+    mat[::3, 4] = r_minus_1  # top-heavy digits, every window negative
+    bases = MsmBases(pts, gpu_ctx, precompute=True)
+    gpu_ctx.profile(True)
+    try:
+        got = bases.msm_columns(mat)
+        kernels = gpu_ctx.profile_report()
+    finally:
+        gpu_ctx.profile(False)
+    assert ("k_digit_sort_pass" in kernels) == (rows % 1024 == 0), sorted(kernels)
+    for j in range(width):
+        np.testing.assert_array_equal(got[j], C.g1_msm(pts, mat[:, j]), err_msg=f"column {j}")
+    assert not got[1].any()
+    np.testing.assert_array_equal(bases.msm(mat[:, 0]), C.g1_msm(pts, mat[:, 0]))
+
+
 @pytest.mark.slow
 def test_msm_columns_batched_kzg_identity(gpu_ctx):
     """300 columns x 2^16 rows (split into 2 internal batches), device-resident: every column

@@ -76,6 +76,12 @@ namespace eon {
 constexpr uint32_t LOG_CHUNK_MIN = 4, LOG_CHUNK_MAX = 7;
 constexpr uint32_t PIECE = 32;   // partials per combine step
 constexpr uint32_t SEG = 8;     // buckets per reduction segment
+// buckets per segment of the call-wide (deferred-finish) reduction: k_bucket_reduce29 walks RED_SEG
+// buckets per lane, k_group_finish29 combines B / RED_SEG segments per group
+#ifndef EON_RED_SEG
+#define EON_RED_SEG 8
+#endif
+constexpr uint32_t RED_SEG = EON_RED_SEG;
 constexpr uint32_t TREE = 256;  // points per tree-reduction block
 constexpr uint32_t FINISH_THREADS = 256;  // threads per group of k_group_finish / k_group_finish29
 
@@ -383,6 +389,13 @@ __global__ void k_piece_owner(const uint32_t* piece_off, uint32_t nb, uint32_t* 
 #ifndef EON_PIECE_NEGSUM
 #define EON_PIECE_NEGSUM 1
 #endif
+// EON_PIECE_MERGE: the two pieces of every bucket straddling one chunk boundary are summed into
+// the first before k_bucket_reduce29, which then reads one piece for such a bucket -- 2 (default):
+// by k_piece_sum29's lane t for the boundary with lane t + 1 of its wave, and by k_piece_merge29
+// for the boundaries between waves; 1: all by k_piece_merge29; 0: the reduction sums them itself
+#ifndef EON_PIECE_MERGE
+#define EON_PIECE_MERGE 2
+#endif
 
 // Thread t sums the sorted pairs [t 2^log_chunk, (t+1) 2^log_chunk) (nonzero digits only): one
 // partial per bucket run, stored at piece_off[b] + t - (start[b] >> log_chunk).  The XYZZ
@@ -551,6 +564,26 @@ __global__ void __launch_bounds__(64, EON_PIECE_MINWAVES) k_piece_sum29(
             }
 #endif
         }
+#if EON_PIECE_MERGE == 2
+        // acc holds the chunk's last piece as stored.  When its bucket goes on into the next chunk
+        // and ends there (two pieces), lane t + 1 of this wave stored the bucket's second piece
+        // at its first flush -- earlier in this wave's instruction stream, every lane's pair loop
+        // having ended -- so lane t sums it in here (k_piece_merge29 covers lane 63's boundary)
+        if (e1 < n_pairs && ((t + 1) & 63u) != 0 && keys[e1] == b) {
+            const uint32_t bb = bucket_of(b, c, groups, nb);
+            const uint32_t p0 = piece_off[bb];
+            if (piece_off[bb + 1] - p0 == 2) {
+                __threadfence_block();
+                G1X29 x;
+                const bool x_inf = ld_raw29(piece_raw + p0 + 1, x);
+                acc29(acc, inf, x, x_inf);
+                if (inf) acc.ZZ = F29{};
+                st_raw29(piece_raw + p0, acc);
+                // the second piece becomes the identity, for the reductions that read every piece
+                st_raw29_inf(piece_raw + p0 + 1);
+            }
+        }
+#endif
     }
 }
 
@@ -658,7 +691,39 @@ __device__ __forceinline__ void st_point(G1Raw29* p, const G1X29& a, bool inf) {
         st_raw29(p, a);
 }
 
-template <class OutT>
+// Buckets whose pairs straddle exactly one chunk boundary hold two pieces (k_piece_sum29's thread
+// t - 1 ends the bucket's first run, thread t starts its second): here they are summed into the
+// first, one thread per chunk boundary, so that k_bucket_reduce29<.., true> reads one piece for
+// every such bucket.  In the reduction a wave walks the buckets of a segment in step, one lane
+// per group, and pays the most pieces any lane has per bucket -- two almost always (a bucket of
+// ~64 sorted pairs straddles a 128-pair chunk boundary half of the time), so its three additions
+// per bucket become two there, and this kernel's half addition per bucket runs with every lane
+// busy.  Buckets spanning three or more chunks (rare) keep all their pieces.
+// Thread i takes the boundary before chunk (i + 1) 2^log_step (log_step 6: the boundaries between
+// k_piece_sum29's waves, the rest merged there).
+__global__ void __launch_bounds__(64) k_piece_merge29(const uint32_t* keys, const uint32_t* start,
+                                                      const uint32_t* piece_off, uint32_t log_chunk,
+                                                      uint32_t log_step, uint32_t c, uint32_t groups, uint32_t nb,
+                                                      G1Raw29* pieces) {
+    const uint32_t n_pairs = start[nb];
+    const uint64_t e0 = (uint64_t)(blockIdx.x * blockDim.x + threadIdx.x + 1) << (log_chunk + log_step);
+    if (e0 >= n_pairs) return;
+    const uint32_t k = keys[e0];
+    if (keys[e0 - 1] != k) return;
+    const uint32_t bb = bucket_of(k, c, groups, nb);
+    const uint32_t p0 = piece_off[bb];
+    if (piece_off[bb + 1] - p0 != 2) return;
+    G1X29 a, x;
+    bool a_inf = ld_raw29(pieces + p0, a);
+    const bool x_inf = ld_raw29(pieces + p0 + 1, x);
+    acc29(a, a_inf, x, x_inf);
+    if (a_inf)
+        st_raw29_inf(pieces + p0);
+    else
+        st_raw29(pieces + p0, a);
+}
+
+template <class OutT, bool MERGED = false>
 __global__ void __launch_bounds__(64) k_bucket_reduce29(const G1Raw29* pieces, const uint32_t* piece_off,
                                                         uint32_t B, uint32_t seg, uint32_t groups, OutT* T,
                                                         OutT* U) {
@@ -670,8 +735,10 @@ __global__ void __launch_bounds__(64) k_bucket_reduce29(const G1Raw29* pieces, c
     bool run_inf = true, acc_inf = true;
     for (int k = (int)seg - 1; k >= 0; k--) {
         const uint32_t bp = (s * seg + (uint32_t)k) * groups + g;
-        const uint32_t e1 = piece_off[bp + 1];
-        for (uint32_t e = piece_off[bp]; e < e1; e++) {
+        const uint32_t e0 = piece_off[bp];
+        uint32_t e1 = piece_off[bp + 1];
+        if (MERGED && e1 - e0 == 2) e1 = e0 + 1;  // k_piece_merge29 summed the two into the first
+        for (uint32_t e = e0; e < e1; e++) {
             const bool inf = ld_raw29(pieces + e, x);
             acc29(run, run_inf, x, inf);
         }
@@ -1500,14 +1567,29 @@ static Status prepare_deferred(eon_ctx* ctx, const MsmLayout& L, uint64_t rows, 
     df = DeferredFinish{};
     if (!L.precomputed) return Status::ok();
     const uint32_t B = 1u << (L.c - 1);
-    if (B < SEG) return Status::ok();
-    df.nseg = B / SEG;
-    df.log_seg = 31 - __builtin_clz(SEG);
+    if (B < RED_SEG) return Status::ok();
+    df.nseg = B / RED_SEG;
+    df.log_seg = 31 - __builtin_clz(RED_SEG);
     EON_HIP(ctx_ensure(ctx, ctx->fin_T, rows * df.nseg * sizeof(G1Raw29)));
     EON_HIP(ctx_ensure(ctx, ctx->fin_U, rows * df.nseg * sizeof(G1Raw29)));
     df.T = ctx->fin_T.as<G1Raw29>();
     df.U = ctx->fin_U.as<G1Raw29>();
     df.out_base = out_base;
+    return Status::ok();
+}
+
+static Status piece_merge(eon_ctx* ctx, const Batch& bt, const SortedRef& sr, MsmWork& wk, hipStream_t st) {
+    if (!EON_PIECE_MERGE) return Status::ok();
+    const uint64_t chunks = ((uint64_t)bt.n_pairs + (1u << bt.log_chunk) - 1) >> bt.log_chunk;
+    const uint32_t log_step = EON_PIECE_MERGE == 2 ? 6 : 0;
+    const uint64_t boundaries = (chunks - 1) >> log_step;
+    if (chunks < 2 || boundaries == 0) return Status::ok();
+    // ~one addition per boundary: 2 x 144 B read, 144 B written
+    ctx->prof.begin("k_piece_merge29", boundaries * 432, st, boundaries * 14);
+    hipLaunchKernelGGL(k_piece_merge29, dim3(blocks_for(boundaries, 64)), dim3(64), 0, st, sr.keys, sr.start,
+                       sr.piece_off, bt.log_chunk, log_step, bt.c, bt.groups, bt.nb, wk.piece_raw.as<G1Raw29>());
+    ctx->prof.end(st);
+    EON_HIP(hipGetLastError());
     return Status::ok();
 }
 
@@ -1518,12 +1600,14 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
                            MsmWork& wk, hipStream_t st, bool fused, DeferredFinish* df = nullptr) {
     Profiler* prof = &ctx->prof;
     const uint32_t nb = bt.nb, groups = bt.groups, B = bt.B;
-    if (df && df->T && fused && groups >= 64 && B >= SEG && L.precomputed) {
+    if (df && df->T && fused && groups >= 64 && B >= RED_SEG && L.precomputed) {
         // first level only; the finish runs once per call (run_deferred_finish)
         const uint64_t row0 = (uint64_t)(bt.out - df->out_base);
+        EON_TRY(piece_merge(ctx, bt, sr, wk, st));
         prof->begin("bucket_reduce", (uint64_t)nb * 128 + (uint64_t)nb / SEG * 256, st);
-        hipLaunchKernelGGL(k_bucket_reduce29<G1Raw29>, dim3(blocks_for((uint64_t)df->nseg * groups, 64)), dim3(64),
-                           0, st, wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, SEG, groups, df->T + row0 * df->nseg,
+        hipLaunchKernelGGL((k_bucket_reduce29<G1Raw29, EON_PIECE_MERGE != 0>),
+                           dim3(blocks_for((uint64_t)df->nseg * groups, 64)), dim3(64), 0, st,
+                           wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, RED_SEG, groups, df->T + row0 * df->nseg,
                            df->U + row0 * df->nseg);
         prof->end(st);
         EON_HIP(hipGetLastError());
@@ -1576,10 +1660,11 @@ static Status batch_reduce(eon_ctx* ctx, const MsmLayout& L, const Batch& bt, co
     prof->begin("bucket_reduce", (uint64_t)nb * 128 + (uint64_t)nb / SEG * 256, st);
     const uint32_t seg = B < SEG ? B : SEG;
     const uint32_t nseg = B / seg;
-    if (fused)
-        hipLaunchKernelGGL(k_bucket_reduce29<G1Xyzz>, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
-                           wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, seg, groups, T, u_buf);
-    else
+    if (fused) {
+        EON_TRY(piece_merge(ctx, bt, sr, wk, st));
+        hipLaunchKernelGGL((k_bucket_reduce29<G1Xyzz, EON_PIECE_MERGE != 0>), dim3(blocks_for((uint64_t)nseg * groups, 64)),
+                           dim3(64), 0, st, wk.piece_raw.as<G1Raw29>(), sr.piece_off, B, seg, groups, T, u_buf);
+    } else
         hipLaunchKernelGGL(k_seg_level, dim3(blocks_for((uint64_t)nseg * groups, 64)), dim3(64), 0, st,
                            wk.bucket_sums.as<G1Xyzz>(), B, seg, groups, T, u_buf);
     G1Xyzz* per_group = wk.red_a.as<G1Xyzz>();

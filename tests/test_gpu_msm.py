@@ -264,6 +264,30 @@ def test_columns_fused_reduce_edge_cases(gpu_ctx):
         assert as_py(got2[j]) == (O.g1_mul(P, k) if k else O.INF), j
 
 
+@pytest.mark.parametrize("rows", [24, 32, 48])
+@pytest.mark.parametrize("cancel", [False, True])
+def test_columns_piece_merge(gpu_ctx, rows, cancel):
+    """Buckets straddling piece-sum chunk boundaries (k_piece_sum29's in-wave merge and
+    k_piece_merge29 between waves, msm.hip): 64 columns of `rows` equal scalars over bases all P
+    (or P then -P), so every bucket is a run of `rows` sorted pairs laid end to end and the
+    16-pair chunks cut them -- 24 rows: two unequal pieces, a run across the chunk-64 wave
+    boundary; 32: two equal pieces (the merge doubles); 48: three pieces (no merge); with -P
+    the pieces cancel (the merge's identity)."""
+    g = O.G1_GEN
+    P = O.g1_mul(g, 987654321)
+    width = 64
+    bases_pts = [P] * rows if not cancel else [P] * (rows // 2) + [O.g1_neg(P)] * (rows - rows // 2)
+    bases = MsmBases(np.stack([pt(p) for p in bases_pts]), gpu_ctx, precompute=True)
+    rng = O.SplitMix64(rows * 2 + cancel)
+    scal = [O.from_mont(rng.fr_mont()) for _ in range(width)]
+    mat = np.stack([np.stack([fr(scal[j]) for j in range(width)]) for _ in range(rows)])
+    got = bases.msm_columns(mat)
+    mult = rows if not cancel else (rows // 2) - (rows - rows // 2)
+    for j in range(width):
+        k = scal[j] * mult % O.P
+        assert as_py(got[j]) == (O.g1_mul(P, k) if k else O.INF), j
+
+
 def test_all_windows_knob_same_result():
     """EON_MSM_ALL_WINDOWS=1 (digitise every window, not only those the largest scalar reaches)
     gives the same MSMs: window-boundary scalars and full-range ones, in a fresh process (the knob

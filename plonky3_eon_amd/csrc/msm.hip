@@ -74,6 +74,10 @@ namespace eon {
 // sorted pairs per k_piece_sum thread: 2^log_chunk, sized so a batch launches ~2^20 threads
 // (>= 4 waves on every SIMD) within [2^4, 2^7]
 constexpr uint32_t LOG_CHUNK_MIN = 4, LOG_CHUNK_MAX = 7;
+// a batch's chunks grow while its piece sums keep >= 2^EON_PIECE_THREADS_LOG threads
+#ifndef EON_PIECE_THREADS_LOG
+#define EON_PIECE_THREADS_LOG 20
+#endif
 constexpr uint32_t PIECE = 32;   // partials per combine step
 constexpr uint32_t SEG = 8;     // buckets per reduction segment
 // buckets per segment of the call-wide (deferred-finish) reduction: k_bucket_reduce29 walks RED_SEG
@@ -292,6 +296,62 @@ struct DigitSource {
         }
     }
 };
+
+// The lean tile's source (EON_SORT_LEAN, sort_pass.h): LEAN_THREADS x 2 pairs per tile, i.e.
+// LEAN_THREADS / 8 rows of one column; thread t takes row r0 + t % R and the windows 2 (t / R),
+// 2 (t / R) + 1 (R = LEAN_THREADS / 8), both in the scalar's word t / R.  The carry into window 2j
+// of the signed recoding is 1 exactly when the scalar's low 32 j bits exceed 0x8000...8000 (every
+// 16-bit window at 2^15: the largest low part the digits [-(2^15 - 1), 2^15] represent), a
+// comparison the words below decide from the top -- almost always word j - 1 alone.
+struct DigitSourceLean {
+    const Fr* canon;
+    uint64_t n;
+    uint32_t tiles_per_col, ref_windows;
+    template <bool FULL, uint32_t THREADS, uint32_t ITEMS>
+    __device__ __forceinline__ void load(uint32_t tile, uint32_t w, uint32_t lane, uint32_t, uint32_t (&key)[ITEMS],
+                                         uint32_t (&val)[ITEMS]) const {
+        static_assert(ITEMS == 2, "two 16-bit windows per thread");
+        constexpr uint32_t R = THREADS / 8;  // rows per tile
+        const uint32_t t = w * 64 + lane;
+        const uint32_t col = tile / tiles_per_col;
+        const uint64_t i = (uint64_t)(tile - col * tiles_per_col) * R + t % R;
+        const uint32_t j = t / R;  // the scalar's word: windows 2 j, 2 j + 1
+        const uint32_t* s = reinterpret_cast<const uint32_t*>(canon + (uint64_t)col * n + i);
+        const uint32_t word = s[j];
+        uint32_t carry = 0;
+        for (int k = (int)j - 1; k >= 0; k--) {  // low part > 0x8000..8000 ?
+            const uint32_t x = s[k];
+            if (x != 0x80008000u) {
+                carry = x > 0x80008000u;
+                break;
+            }
+        }
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint32_t raw = ((word >> (16 * h)) & 0xffffu) + carry;
+            uint32_t mag, neg;
+            if (raw > (1u << 15)) {
+                mag = (1u << 16) - raw;
+                neg = 1;
+                carry = 1;
+            } else {
+                mag = raw;
+                neg = 0;
+                carry = 0;
+            }
+            key[h] = mag ? (col << 16 | (mag - 1)) : 0xFFFFFFFFu;
+            val[h] = mag ? ((uint32_t)(i * ref_windows + 2 * j + h) | neg << 31) : 0u;
+        }
+    }
+};
+
+__global__ void __launch_bounds__(sortpass::LEAN_THREADS) k_digit_sort_pass_lean(DigitSourceLean src, uint32_t* kd,
+                                                                                 uint32_t* vd, uint32_t n, uint32_t shift,
+                                                                                 const uint32_t* base, uint64_t* status,
+                                                                                 uint32_t* tile_ctr) {
+    sortpass::sort_pass_tile<8, DigitSourceLean, sortpass::LEAN_THREADS, sortpass::LEAN_ITEMS>(src, kd, vd, n, shift, 8,
+                                                                                             base, status, tile_ctr);
+}
 
 __global__ void __launch_bounds__(sortpass::SORT_THREADS) k_digit_sort_pass(DigitSource src, uint32_t* kd, uint32_t* vd,
                                                                             uint32_t n, uint32_t shift,
@@ -1303,7 +1363,7 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     bt.scan_bytes = exclusive_scan_temp_bytes(nb + 1);
     EON_HIP(ctx_ensure(ctx, wk.temp, std::max(bt.sort_bytes, bt.scan_bytes)));
     bt.log_chunk = LOG_CHUNK_MIN;
-    while (bt.log_chunk < LOG_CHUNK_MAX && (E >> (bt.log_chunk + 1)) >= (1ull << 20)) bt.log_chunk++;
+    while (bt.log_chunk < LOG_CHUNK_MAX && (E >> (bt.log_chunk + 1)) >= (1ull << EON_PIECE_THREADS_LOG)) bt.log_chunk++;
     // few buckets for many pairs (a bucket would collect more than ~8 pieces): longer chunks while
     // the piece sums keep 2^18 threads (4 waves per SIMD)
     while (bt.log_chunk < LOG_CHUNK_MAX && (E >> bt.log_chunk) > 8ull * nb && (E >> (bt.log_chunk + 1)) >= (1ull << 18))
@@ -1325,7 +1385,8 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
     // the first sort pass fused with the digits (DigitSource): fixed-base tables, c = 16, all 16
     // windows, whole 1024-row tiles, two passes
     const bool fused = EON_MSM_FUSED_SORT && L.precomputed && bt.c == 16 && bt.W == 16 && L.W == 16 &&
-                       n % sortpass::SORT_THREADS == 0 && radix_sort_passes(bt.key_bits).passes == 2;
+                       n % (EON_SORT_LEAN ? sortpass::LEAN_THREADS / 8 : sortpass::SORT_THREADS) == 0 &&
+                       radix_sort_passes(bt.key_bits).passes == 2;
     if (fused) {
         EON_HIP(ctx_ensure(ctx, wk.canon, n * bt.cols * sizeof(Fr)));
         prof->begin("k_msm_digit_hist", n * bt.cols * 64, st);
@@ -1337,14 +1398,22 @@ static Status batch_sort(eon_ctx* ctx, const MsmLayout& L, uint64_t n, uint64_t 
         EON_HIP(radix_sort_prepare(wk.temp.p, E, bt.key_bits, st));
         const RadixPassArgs a0 = radix_sort_pass_args(wk.temp.p, E, bt.key_bits, 0);
         // per call: the attribute is per device (another context may run on another GPU)
-        EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_digit_sort_pass),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sortpass::SORT_LDS));
         // the pass's own traffic: 32 bytes of scalar per 16 pairs read, 8 bytes per pair written
         prof->begin("k_digit_sort_pass", n * bt.cols * 32 + E * 8, st);
+#if EON_SORT_LEAN
+        const DigitSourceLean src{wk.canon.as<Fr>(), n, (uint32_t)(n / (sortpass::LEAN_THREADS / 8)), L.W};
+        hipLaunchKernelGGL(k_digit_sort_pass_lean, dim3(a0.tiles), dim3(sortpass::LEAN_THREADS), sortpass::LEAN_LDS, st,
+                           src, wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>(), (uint32_t)E, a0.shift, a0.base,
+                           a0.status, a0.tile_ctr);
+#else
+        // per call: the attribute is per device (another context may run on another GPU)
+        EON_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_digit_sort_pass),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sortpass::SORT_LDS));
         const DigitSource src{wk.canon.as<Fr>(), n, (uint32_t)(n / sortpass::SORT_THREADS), L.W};
         hipLaunchKernelGGL(k_digit_sort_pass, dim3(a0.tiles), dim3(sortpass::SORT_THREADS), sortpass::SORT_LDS, st, src,
                            wk.keys.as<uint32_t>(), wk.vals.as<uint32_t>(), (uint32_t)E, a0.shift, a0.base, a0.status,
                            a0.tile_ctr);
+#endif
         prof->end(st);
         EON_HIP(hipGetLastError());
         prof->begin("radix_sort_pairs", E * 16, st);  // the second pass

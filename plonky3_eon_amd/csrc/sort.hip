@@ -89,6 +89,16 @@ __global__ void __launch_bounds__(SORT_THREADS) k_sort_pass(const uint32_t* __re
     sort_pass_tile<DBITS>(PairSource{ks, vs}, kd, vd, n, shift, dbits_rt, base, status, tile_ctr);
 }
 
+// the lean tile (sort_pass.h: LEAN_THREADS x LEAN_ITEMS pairs, at most 32 VGPRs)
+template <uint32_t DBITS>
+__global__ void __launch_bounds__(LEAN_THREADS) __attribute__((amdgpu_num_vgpr(32)))
+k_sort_pass_lean(const uint32_t* __restrict__ ks, const uint32_t* __restrict__ vs, uint32_t* __restrict__ kd,
+                 uint32_t* __restrict__ vd, uint32_t n, uint32_t shift, uint32_t dbits_rt,
+                 const uint32_t* __restrict__ base, uint64_t* status, uint32_t* tile_ctr) {
+    sort_pass_tile<DBITS, PairSource, LEAN_THREADS, LEAN_ITEMS>(PairSource{ks, vs}, kd, vd, n, shift, dbits_rt, base,
+                                                                status, tile_ctr);
+}
+
 // ---- exclusive scan ---------------------------------------------------------------------------
 
 constexpr uint32_t SCAN_THREADS = 256, SCAN_ITEMS = 16, SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
@@ -188,11 +198,18 @@ uint32_t* radix_sort_histograms(void* temp, uint64_t n) {
     return reinterpret_cast<uint32_t*>(static_cast<char*>(temp) + 2 * align256(n * 4));
 }
 
+// tiles of a pass over n pairs (q: the pass index)
+static uint64_t pass_tiles(uint64_t n, uint32_t q) {
+    (void)q;
+    const uint32_t tile = EON_SORT_LEAN ? LEAN_TILE : SORT_TILE;
+    return (n + tile - 1) / tile;
+}
+
 // per pass: a 64-byte tile counter and the tiles' status words, every pass's zeroed by one memset
 static size_t pass_state_bytes(uint64_t tiles) { return 64 + align256(tiles * 256 * 8); }
 
 size_t radix_sort_temp_bytes(uint64_t n, uint32_t bits) {
-    const uint64_t tiles = (n + SORT_TILE - 1) / SORT_TILE;
+    const uint64_t tiles = std::max(pass_tiles(n, 0), pass_tiles(n, 1));
     const uint32_t passes = bits ? split_bits(bits).passes : 1;
     return 2 * align256(n * 4) + 2 * align256(MAX_PASSES * 256 * 4) + 256 + passes * pass_state_bytes(tiles);
 }
@@ -212,7 +229,7 @@ struct SortLayout {
 
 SortLayout sort_layout(void* temp, uint64_t n) {
     SortLayout L;
-    L.tiles = (uint32_t)((n + SORT_TILE - 1) / SORT_TILE);
+    L.tiles = (uint32_t)pass_tiles(n, 0);
     char* p = static_cast<char*>(temp);
     L.ktmp = reinterpret_cast<uint32_t*>(p);
     p += align256(n * 4);
@@ -224,7 +241,7 @@ SortLayout sort_layout(void* temp, uint64_t n) {
     p += align256(MAX_PASSES * 256 * 4);
     p += 256;
     L.state = p;
-    L.psb = pass_state_bytes(L.tiles);
+    L.psb = pass_state_bytes(std::max(pass_tiles(n, 0), pass_tiles(n, 1)));
     return L;
 }
 
@@ -247,9 +264,14 @@ hipError_t run_passes(const SortLayout& L, const PassBits& pb, uint32_t q0, cons
         const bool to_out = ((pb.passes - 1 - q) & 1) == 0;
         uint32_t* dk = to_out ? keys_out : L.ktmp;
         uint32_t* dv = to_out ? vals_out : L.vtmp;
-        hipLaunchKernelGGL(pb.bits[q] == 8 ? k_sort_pass<8> : k_sort_pass<0>, dim3(L.tiles), dim3(SORT_THREADS), SORT_LDS,
-                           st, sk, sv, dk, dv, (uint32_t)n, pb.shift[q], pb.bits[q], L.base + q * 256, L.status(q),
-                           L.ctr(q));
+        if (EON_SORT_LEAN)
+            hipLaunchKernelGGL(pb.bits[q] == 8 ? k_sort_pass_lean<8> : k_sort_pass_lean<0>, dim3((uint32_t)pass_tiles(n, q)),
+                               dim3(LEAN_THREADS), LEAN_LDS, st, sk, sv, dk, dv, (uint32_t)n, pb.shift[q], pb.bits[q],
+                               L.base + q * 256, L.status(q), L.ctr(q));
+        else
+            hipLaunchKernelGGL(pb.bits[q] == 8 ? k_sort_pass<8> : k_sort_pass<0>, dim3(L.tiles), dim3(SORT_THREADS),
+                               SORT_LDS, st, sk, sv, dk, dv, (uint32_t)n, pb.shift[q], pb.bits[q], L.base + q * 256,
+                               L.status(q), L.ctr(q));
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         sk = dk;

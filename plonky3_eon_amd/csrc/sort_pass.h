@@ -36,6 +36,21 @@ constexpr uint64_t ST_AGG = 1ull << 62, ST_INC = 2ull << 62, ST_COUNT = (1ull <<
 static_assert(SORT_THREADS == 512 || SORT_THREADS == 1024, "tile threads");
 static_assert(RADIX_SORT_MAX_PAIRS <= (1ull << 32) - SORT_TILE, "the last tile's indices must not wrap");
 constexpr size_t SORT_LDS = (size_t)SORT_TILE * 8 + SORT_WAVES * 256 * 4 + 2 * 256 * 4 + 64;
+// LDS bytes of a tile of THREADS x ITEMS pairs
+constexpr size_t sort_lds_bytes(uint32_t threads, uint32_t items) {
+    return (size_t)threads * items * 8 + threads / 64 * 256 * 4 + 2 * 256 * 4 + 64;
+}
+// The lean tile (EON_SORT_LEAN): 256 threads x 2 pairs in <= 32 VGPRs, so that a block fits beside
+// the piece sums (4 waves x 120 VGPRs per SIMD) and the pass runs under them instead of alone
+// EON_SORT_LEAN=1: every pass of the digit sort (and the MSM's fused digit pass) runs in lean tiles
+#ifndef EON_SORT_LEAN
+#define EON_SORT_LEAN 0
+#endif
+#ifndef EON_SORT_LEAN_ITEMS
+#define EON_SORT_LEAN_ITEMS 2
+#endif
+constexpr uint32_t LEAN_THREADS = 256, LEAN_ITEMS = EON_SORT_LEAN_ITEMS, LEAN_TILE = LEAN_THREADS * LEAN_ITEMS;
+constexpr size_t LEAN_LDS = sort_lds_bytes(LEAN_THREADS, LEAN_ITEMS);
 
 // inclusive scan of one value per lane across a wave64
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -74,12 +89,12 @@ __device__ __forceinline__ uint64_t ld_status(uint64_t* p) {
 struct PairSource {
     const uint32_t* __restrict__ ks;
     const uint32_t* __restrict__ vs;
-    template <bool FULL>
+    template <bool FULL, uint32_t THREADS = SORT_THREADS, uint32_t ITEMS = SORT_ITEMS>
     __device__ __forceinline__ void load(uint32_t tile, uint32_t w, uint32_t lane, uint32_t n,
-                                         uint32_t (&key)[SORT_ITEMS], uint32_t (&val)[SORT_ITEMS]) const {
-        const uint32_t wbase = tile * SORT_TILE + w * 64 * SORT_ITEMS;
+                                         uint32_t (&key)[ITEMS], uint32_t (&val)[ITEMS]) const {
+        const uint32_t wbase = tile * (THREADS * ITEMS) + w * 64 * ITEMS;
 #pragma unroll
-        for (uint32_t j = 0; j < SORT_ITEMS; j++) {
+        for (uint32_t j = 0; j < ITEMS; j++) {
             const uint32_t i = wbase + j * 64 + lane;
             key[j] = (FULL || i < n) ? ks[i] : 0u;
             val[j] = (FULL || i < n) ? vs[i] : 0u;
@@ -92,11 +107,14 @@ struct PairSource {
 // per-bit loop then has no branch on the width (each `b < dbits` test was a VALU compare, wait
 // states and a branch per bit and item); DBITS = 0 reads it from `dbits_rt`.  `base`: the digits'
 // first output positions (the exclusive scan of the pass's histogram); status / tile_ctr zeroed.
-template <uint32_t DBITS, class Src>
+template <uint32_t DBITS, class Src, uint32_t SORT_THREADS = sortpass::SORT_THREADS,
+          uint32_t SORT_ITEMS = sortpass::SORT_ITEMS>
 __device__ __forceinline__ void sort_pass_tile(const Src& src, uint32_t* __restrict__ kd, uint32_t* __restrict__ vd,
                                                uint32_t n, uint32_t shift, uint32_t dbits_rt,
                                                const uint32_t* __restrict__ base, uint64_t* status,
                                                uint32_t* tile_ctr) {
+    constexpr uint32_t SORT_WAVES = SORT_THREADS / 64, SORT_TILE = SORT_THREADS * SORT_ITEMS;
+    static_assert(SORT_THREADS >= 256, "the per-digit steps take threads 0..255");
     const uint32_t dbits = DBITS ? DBITS : dbits_rt;
     extern __shared__ uint32_t lds[];
     uint32_t* sk = lds;                                 // SORT_TILE keys in digit order
@@ -117,7 +135,10 @@ __device__ __forceinline__ void sort_pass_tile(const Src& src, uint32_t* __restr
     auto body = [&](auto full_tag) __attribute__((always_inline)) {
         constexpr bool FULL = decltype(full_tag)::value;
         uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rk[SORT_ITEMS];
-        src.template load<FULL>(tile, w, lane, n, key, val);
+        if constexpr (SORT_ITEMS == sortpass::SORT_ITEMS && SORT_THREADS == sortpass::SORT_THREADS)
+            src.template load<FULL>(tile, w, lane, n, key, val);
+        else
+            src.template load<FULL, SORT_THREADS, SORT_ITEMS>(tile, w, lane, n, key, val);
 #pragma unroll
         for (uint32_t j = 0; j < SORT_ITEMS; j++) {
             const bool valid = FULL || wbase + j * 64 + lane < n;

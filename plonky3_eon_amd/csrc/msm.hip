@@ -450,13 +450,11 @@ __global__ void k_piece_owner(const uint32_t* piece_off, uint32_t nb, uint32_t* 
 #define EON_PIECE_NEGSUM 1
 #endif
 // EON_PIECE_MERGE: the two pieces of every bucket straddling one chunk boundary are summed into
-// the first before k_bucket_reduce29, which then reads one piece for such a bucket -- 1 (default):
-// by k_piece_merge29, one thread per chunk boundary; 2: by k_piece_sum29's lane t for the boundary
-// with lane t + 1 of its wave (k_piece_merge29 only between waves), less kernel time in all but
-// the same timed prove (profiles/r06/s11, s19) at 128 VGPRs instead of 115; 0: the reduction sums
-// both pieces itself
+// the first before k_bucket_reduce29, which then reads one piece for such a bucket -- 2 (default):
+// by k_piece_sum29's lane t for the boundary with lane t + 1 of its wave, and by k_piece_merge29
+// for the boundaries between waves; 1: all by k_piece_merge29; 0: the reduction sums them itself
 #ifndef EON_PIECE_MERGE
-#define EON_PIECE_MERGE 1
+#define EON_PIECE_MERGE 2
 #endif
 
 // Thread t sums the sorted pairs [t 2^log_chunk, (t+1) 2^log_chunk) (nonzero digits only): one
